@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s on the Cornell box 512x512, 256 spp (BASELINE.json config 2).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step renders one full 512x512 / 256-spp frame of the reference's Cornell
+box (CPU-engine preset: cap 2 bounces, hit rule of the prebuilt CPU object,
+uniform hemisphere sampling).  The frame is cut into 32x32 tiles dealt
+round-robin to the ranks (one process per GPU); each rank renders its tiles
+with the HIP megakernel, and the per-rank tile buffers are all-gathered over
+RCCL into the full image.  The frame is fixed as N grows: strong scaling.
+
+value = total ray casts (all ranks) / max-over-ranks wall time of the K
+timed steps, in Mrays/s.  rank 0 prints one JSON line with the roofline of
+the render kernel (HIP events on the launch stream), the per-pixel MAPE vs the
+CPU restatement on a checked window, and the CPU baseline (oracle/, timed on
+this host's cores on a bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import rtmi  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
+TILE = 32
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--height", type=int, default=512)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--spp-split", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target CPU-baseline sample duration (0 disables)")
+    ap.add_argument("--no-parity", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(geom, params, cam_pos, seconds):
+    """Time the CPU restatement (oracle/, OpenMP) on a bounded strip of the same frame."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    oracle.set_threads(threads)
+    op = oracle.params_from(params)
+    ocam = oracle.camera(cam_pos)
+    w = params.width
+    rows, y0 = 4, params.height // 2 - 2
+    t0 = time.perf_counter()
+    _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
+    dt = time.perf_counter() - t0
+    rate = casts / max(dt, 1e-9)
+    # scale the strip so that the timed sample takes about `seconds`
+    per_row = casts / rows
+    rows = int(max(4, min(params.height, seconds * rate / max(per_row, 1.0))))
+    y0 = max(0, params.height // 2 - rows // 2)
+    best = None
+    for _ in range(1):
+        t0 = time.perf_counter()
+        _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return {
+        "value": round(casts / best / 1e6, 3),
+        "unit": "Mrays/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"rows {y0}..{y0 + rows - 1} of the {w}x{params.height}/{params.spp}-spp frame "
+                  f"({casts} ray casts, {best:.1f} s, OpenMP over rows)",
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group(backend="nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    ctx = rtmi.Context(local_rank)
+    geom = rtmi.cornell_geometry(rtmi.RT_PRESET_CPU)
+    scene = rtmi.Scene(ctx, geom)
+    params = rtmi.default_params(rtmi.RT_PRESET_CPU, width=args.width, height=args.height,
+                                 spp=args.spp, spp_split=args.spp_split)
+    cam_pos = rtmi.CAMERAS["cornell"]
+    cam = rtmi.camera(cam_pos)
+
+    tiles = rtmi.tiles.rank_tiles(params.width, params.height, TILE, rank, world)
+    k = tiles.shape[0]
+    out = torch.zeros((k, TILE, TILE, 3), dtype=torch.float32, device=dev)
+    casts = torch.zeros(1, dtype=torch.int64, device=dev)
+    gathered = torch.empty((world, k, TILE, TILE, 3), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def render():
+        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(),
+                                 casts.data_ptr(), stream.cuda_stream)
+
+    def step():
+        render()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    casts.zero_()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        render()
+        ev[i][1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+
+    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    rank_casts = int(casts.item())
+    stats = torch.tensor([elapsed, float(rank_casts), kernel_ms, float(rank_casts)],
+                         dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = stats[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:2].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, total_casts = float(t_max.item()), int(tot.item())
+    else:
+        total_casts = rank_casts
+
+    if world == 1:
+        gathered = out[None]
+    image = None
+    if rank == 0:
+        image = rtmi.tiles.assemble(gathered.cpu().numpy(), params.width, params.height, TILE, world)
+
+    if rank == 0:
+        n_tri = geom.n_tri
+        b_cast = 36 * n_tri + 32  # algorithmic bytes per ray cast
+        casts_per_launch = rank_casts / args.steps
+        achieved_gbs = casts_per_launch * b_cast / (kernel_ms * 1e-3) / 1e9
+        valu_tflops = casts_per_launch * n_tri * 71 / (kernel_ms * 1e-3) / 1e12
+        line = {
+            "metric": "Mrays/sec (Cornell 512^2 256spp ray casts)",
+            "value": round(total_casts / elapsed / 1e6, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "procedural Cornell box of the reference (CPU-engine preset), Philox RNG seed 1984",
+            "config": {
+                "workload": "cornell_512x512_256spp",
+                "width": params.width, "height": params.height, "spp": params.spp,
+                "max_bounces": params.max_bounces, "hit_rule": "cpu_object", "sampler": "uniform",
+                "spp_split": params.spp_split, "tile": TILE, "parallelism": f"tiles{world}",
+                "triangles": n_tri,
+            },
+            "ray_casts_per_step": total_casts // args.steps,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved_gbs, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel": "k_render<0,0,0>",
+                "kernel_ms": round(kernel_ms, 4),
+                "bytes_per_cast": b_cast,
+                "valu_tflops_est": round(valu_tflops, 2),
+                "valu_frac_est": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+            },
+        }
+        if not args.no_parity:
+            line["parity"] = parity_window(geom, params, cam_pos, image)
+        if args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+
+    scene.close()
+    ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def parity_window(geom, params, cam_pos, image):
+    """MAPE and bit-exactness of the GPU frame vs the CPU restatement on 4 windows."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    op = oracle.params_from(params)
+    ocam = oracle.camera(cam_pos)
+    wins = [(96, 64, 16, 16), (248, 248, 16, 16), (400, 300, 16, 16), (40, 440, 16, 16)]
+    worst, exact = 0.0, True
+    for (x, y, w, h) in wins:
+        if x + w > params.width or y + h > params.height:
+            continue
+        ref, _ = oracle.render(geom, ocam, op, (x, y, w, h))
+        got = image[y:y + h, x:x + w]
+        worst = max(worst, rtmi.metrics.mape_f(ref, got))
+        exact = exact and bool(np.array_equal(ref.view(np.uint32), got.view(np.uint32)))
+    return {"mape_vs_cpu": worst, "bit_exact": exact, "windows": len(wins), "window_px": 16}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,163 @@
+/*
+ * rtmi.h — C ABI of the MI355X-native path tracer (librtmi.so).
+ *
+ * The reference (callumPearce/Reinforcement-Light-Rays-Pathtracer) has no
+ * FFI; its drop-in boundary for the hot path is the C++ scene-loader /
+ * Camera / SDL frame-buffer API plus the render entry point.  Each entry
+ * point below names the reference interface it replaces (paths relative to
+ * the reference root; CPU/ = Old_CPU_Rendering_Engine/Source,
+ * GPU/ = GPU_Rendering_Engine/Source).  The C++ facade in
+ * reinforcement-light-rays-pathtracer_amd/host/ restores the reference's
+ * class/function names on top of this ABI; Python binds it with ctypes.
+ *
+ * Conventions
+ *  - every function returns RT_OK (0) or a negative RT_E* code; nothing
+ *    throws across the ABI; rt_last_error() holds a thread-local message.
+ *  - host pointers are caller-owned; device memory is owned by rt_ctx /
+ *    rt_scene.  Functions named *_device take device pointers and a
+ *    hipStream_t passed as void* and are asynchronous on that stream.
+ *  - one host thread per rt_ctx; contexts on different GPUs may run
+ *    concurrently (one process per GPU is the supported multi-GPU model).
+ */
+#ifndef RTMI_H
+#define RTMI_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_OK 0
+#define RT_E_INVALID (-1)     /* bad argument */
+#define RT_E_HIP (-2)         /* HIP runtime error */
+#define RT_E_NOMEM (-3)       /* allocation failed */
+#define RT_E_IO (-4)          /* file could not be opened / parsed */
+#define RT_E_UNSUPPORTED (-5) /* valid request this build does not implement */
+
+#define RT_HIT_NONE (-1)
+#define RT_HIT_TYPE_LIGHT 1u   /* enum IntersectionType AREA_LIGHT(_PLANE) */
+#define RT_HIT_TYPE_SURFACE 2u /* enum IntersectionType SURFACE */
+
+/* semantic presets */
+#define RT_PRESET_CPU 0 /* Old_CPU_Rendering_Engine: recursive estimator, bounce cap semantics of
+                           CPU/path_tracing/default_path_tracing.cpp:46-101 */
+#define RT_PRESET_GPU 1 /* GPU_Rendering_Engine: iterative throughput,
+                           GPU/path_tracing/default_path_tracing.cu:36-88 */
+
+#define RT_HIT_RULE_CPU 0 /* predicate of the prebuilt CPU triangle.cpp.o (t > 1e-5, t < dist + 1e-5) */
+#define RT_HIT_RULE_GPU 1 /* GPU/rays/ray.cu:38-141 (t < dist, dist starts at 999999) */
+
+#define RT_SAMPLER_UNIFORM 0 /* the reference's sampler: cos(theta) = r1, pdf 1/(2*pi) */
+#define RT_SAMPLER_COSINE 1  /* cosine-weighted: cos(theta) = sqrt(r1), pdf cos/pi */
+
+typedef struct rt_ctx rt_ctx;
+typedef struct rt_scene rt_scene;
+
+/* Camera: CPU/camera.h:11-42 (position, yaw) and GPU/camera.cuh:11-36 (yaw_y, yaw_x). */
+typedef struct {
+    float pos[4];
+    float yaw_y; /* CPU engine "yaw" */
+    float yaw_x; /* GPU engine only; 0 for the CPU preset */
+} rt_camera;
+
+/* Render parameters: the reference's compile-time constants
+ * (CPU/constants/ and GPU/constants/ headers) as a runtime struct. */
+typedef struct {
+    int32_t width, height; /* SCREEN_WIDTH / SCREEN_HEIGHT; FOCAL_LENGTH = height */
+    int32_t spp;           /* SAMPLES_PER_PIXEL */
+    int32_t max_bounces;   /* MAX_RAY_BOUNCES */
+    int32_t sampler;       /* RT_SAMPLER_* */
+    int32_t preset;        /* RT_PRESET_* */
+    int32_t hit_rule;      /* RT_HIT_RULE_* */
+    int32_t spp_split;     /* sample chunks per pixel (1,2,4,...,64; divides spp; 0 = 1).  Chunk c
+                              sums samples [c*spp/S, (c+1)*spp/S) in order; the pixel is
+                              (((P0 + P1) + P2) + ...) / spp.  Part of the result's definition:
+                              keep it fixed across GPU counts for bit-identical images. */
+    uint64_t seed;         /* Philox key; the reference's curand seed is 1984 */
+    float env_light;       /* ENVIRONMENT_LIGHT (GPU preset) */
+    float t_scale;         /* direction scale in the hit test (= SCREEN_HEIGHT in the reference) */
+} rt_params;
+
+/* Fill *p with the reference defaults of a preset:
+ *   CPU: 512x512, 16 spp, cap 2, hit rule CPU   (CPU/constants/image_settings.h:9-12,
+ *                                                monte_carlo_settings.h:8-9)
+ *   GPU: 720x720, 32 spp, cap 80, hit rule GPU  (GPU/constants/image_settings.h:9-12,
+ *                                                monte_carlo_settings.h:8-10)
+ * seed 1984 (GPU/utils/cuda_helpers.cu:24). */
+int rt_params_default(int preset, rt_params* p);
+
+/* ---- context ---------------------------------------------------------- */
+/* Replaces the device setup of GPU/main.cu:150-198 (cudaMalloc + pointer patching). */
+int rt_ctx_create(int device_ordinal, rt_ctx** out);
+int rt_ctx_destroy(rt_ctx* ctx);
+const char* rt_last_error(void);
+
+/* ---- scene construction (host side, no GPU) --------------------------- */
+/* get_cornell_shapes: CPU/scenes/cornell_box_scene.cpp:3-205 (variant RT_PRESET_CPU:
+ * one light plane, emission 1*(1,1,0.9)) and GPU/scenes/cornell_box_scene.cu:4 (variant
+ * RT_PRESET_GPU: two AreaLights, emission 14*(0.9,0.9,0.9)).
+ * Arrays must hold 36 surfaces / 2 lights (rt_cornell_counts). */
+int rt_cornell_counts(int* n_surf, int* n_light);
+int rt_cornell_geometry(int variant, float* tri_v /* n_surf x 9 */, float* albedo /* n_surf x 3 */,
+                        float* light_v /* n_light x 9 */, float* emission /* n_light x 3 */,
+                        int32_t* light_group /* n_light */);
+
+/* load_scene for OBJ files with the GPU engine's semantics:
+ * GPU/objects/object_importer.cu:8-412 (scale 2, (v1,v3,v2) order, per-scene materials and
+ * lights, lights_in_obj for complex_light_room).  `scene_kind` selects the hard-coded
+ * material/light block: 0 generic (white 0.75, no lights), 1 door_room, 2 archway,
+ * 3 complex_light_room.  Two-pass: call with NULL arrays to get counts. */
+int rt_obj_geometry(const char* path, int scene_kind, float* tri_v, float* albedo, int* n_surf,
+                    float* light_v, float* emission, int32_t* light_group, int* n_light,
+                    float* nn_vertices /* Scene::vertices order, may be NULL */, int* n_nn_floats);
+
+/* ---- device scene ------------------------------------------------------ */
+/* Scene::load_* + the H2D copies of GPU/main.cu:160-180.  Copies the host arrays;
+ * computes normals (CPU/objects/triangle.cpp:73-82) and per-triangle tangent frames. */
+int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_surf,
+                    const float* light_v, const float* emission, const int32_t* light_group,
+                    int n_light, rt_scene** out);
+int rt_scene_destroy(rt_scene* scene);
+/* Host copy of the normals the scene computed, (n_surf+n_light) x 3. */
+int rt_scene_normals(const rt_scene* scene, float* out);
+
+/* ---- the hot path -------------------------------------------------------- */
+/* Ray::closest_intersection over a ray batch (CPU/rays/ray.cpp:14-28 + the hit predicate;
+ * GPU/rays/ray.cu:16-141).  dir must be normalised (Ray::Ray does it).  out_t = hit distance
+ * in t_scale units (+inf on miss); out_hit = (type<<30)|index, RT_HIT_NONE on miss; light
+ * index = plane index (hit_rule CPU) or light-triangle index (hit_rule GPU). Host arrays. */
+int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig /* n x 3 */,
+                 const float* dir /* n x 3 */, int n, float t_scale, int hit_rule,
+                 float* out_t, int32_t* out_hit);
+/* Same, device pointers, asynchronous on `stream` (hipStream_t). */
+int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
+                        const float* d_dir, int n, float t_scale, int hit_rule, float* d_t,
+                        int32_t* d_hit, void* stream);
+
+/* draw_default_path_tracing (CPU/path_tracing/default_path_tracing.cpp:5-18;
+ * GPU kernel GPU/path_tracing/default_path_tracing.cu:7-34): render the rectangle
+ * [x0,x0+w) x [y0,y0+h) of the params->width x params->height image.
+ * out_rgb: w*h*3 floats, row-major (row = y-y0).  Synchronous; host memory. */
+int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
+              int x0, int y0, int w, int h, float* out_rgb, uint64_t* out_ray_casts);
+
+/* Tile-list render for image-tile partitioning across GPUs.  tiles: n_tiles x 2 int32
+ * (host) pixel origins of tile_size x tile_size tiles (tile_size a multiple of 16).
+ * d_out: device, n_tiles*tile_size*tile_size*3 floats, [tile][y][x][rgb].
+ * d_casts: device uint64 (accumulated into, may be NULL).  Asynchronous on `stream`. */
+int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam,
+                           const rt_params* params, const int32_t* tiles, int n_tiles,
+                           int tile_size, float* d_out, uint64_t* d_casts, void* stream);
+
+/* SDLScreen::PutPixelSDL pack rule (CPU/sdl/sdl_screen.cpp:100-112). Host arrays. */
+int rt_pack_argb(const float* rgb, int n, uint32_t* out_argb);
+
+/* SDLScreen::SDL_SaveImage replacement: 32-bit BMP of an ARGB buffer (headless). */
+int rt_save_bmp(const char* path, const uint32_t* argb, int width, int height);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RTMI_H */

@@ -1,0 +1,163 @@
+"""ctypes wrapper of the CPU restatement (rt_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker.  The product
+(reinforcement-light-rays-pathtracer_amd/) never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+_LIB = None
+_FP = ctypes.POINTER(ctypes.c_float)
+_IP = ctypes.POINTER(ctypes.c_int32)
+
+
+class OrcCamera(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 4), ("yaw_y", ctypes.c_float), ("yaw_x", ctypes.c_float)]
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+        ("max_bounces", ctypes.c_int32), ("sampler", ctypes.c_int32), ("preset", ctypes.c_int32),
+        ("hit_rule", ctypes.c_int32), ("spp_split", ctypes.c_int32), ("seed", ctypes.c_uint64),
+        ("env_light", ctypes.c_float), ("t_scale", ctypes.c_float),
+    ]
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_philox4x32_10.argtypes = [ctypes.POINTER(ctypes.c_uint32)] * 3
+        L.orc_sincos_turn.argtypes = [ctypes.c_float, _FP, _FP]
+        L.orc_triangle_normals.argtypes = [_FP, ctypes.c_int, _FP]
+        L.orc_cornell.argtypes = [ctypes.c_int, _FP, _FP, _FP, _IP, ctypes.POINTER(ctypes.c_int),
+                                  ctypes.POINTER(ctypes.c_int)]
+        L.orc_intersect.argtypes = [_FP, ctypes.c_int, ctypes.c_int, _IP, _FP, _FP, ctypes.c_int,
+                                    ctypes.c_float, ctypes.c_int, _FP, _IP]
+        L.orc_render.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int,
+                                 ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams),
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _FP,
+                                 ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_pack_argb.argtypes = [_FP, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_num_threads.restype = ctypes.c_int
+        L.orc_set_threads.argtypes = [ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _f(a):
+    return a.ctypes.data_as(_FP)
+
+
+def _i(a):
+    return a.ctypes.data_as(_IP)
+
+
+def philox(ctr, key) -> np.ndarray:
+    c = np.asarray(ctr, np.uint32)
+    k = np.asarray(key, np.uint32)
+    out = np.zeros(4, np.uint32)
+    P = ctypes.POINTER(ctypes.c_uint32)
+    lib().orc_philox4x32_10(c.ctypes.data_as(P), k.ctypes.data_as(P), out.ctypes.data_as(P))
+    return out
+
+
+def sincos_turn(r: float):
+    s, c = ctypes.c_float(), ctypes.c_float()
+    lib().orc_sincos_turn(ctypes.c_float(r), ctypes.byref(s), ctypes.byref(c))
+    return s.value, c.value
+
+
+def cornell(variant: int):
+    tri = np.zeros((38, 9), np.float32)
+    alb = np.zeros((36, 3), np.float32)
+    em = np.zeros((2, 3), np.float32)
+    grp = np.zeros(2, np.int32)
+    ns, nl = ctypes.c_int(), ctypes.c_int()
+    lib().orc_cornell(variant, _f(tri), _f(alb), _f(em), _i(grp), ctypes.byref(ns), ctypes.byref(nl))
+    return {"tri": tri[:36].copy(), "albedo": alb, "light": tri[36:].copy(), "emission": em,
+            "light_group": grp}
+
+
+def normals(tri_all: np.ndarray) -> np.ndarray:
+    t = np.ascontiguousarray(tri_all, np.float32)
+    out = np.zeros((t.shape[0], 3), np.float32)
+    lib().orc_triangle_normals(_f(t), t.shape[0], _f(out))
+    return out
+
+
+def intersect(tri, n_surf, n_light, light_group, orig, direction, t_scale, hit_rule):
+    t_all = np.ascontiguousarray(tri, np.float32)
+    g = np.ascontiguousarray(light_group, np.int32)
+    o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    out_t = np.zeros(n, np.float32)
+    out_h = np.zeros(n, np.int32)
+    lib().orc_intersect(_f(t_all), n_surf, n_light, _i(g), _f(o), _f(d), n, t_scale, hit_rule,
+                        _f(out_t), _i(out_h))
+    return out_t, out_h
+
+
+def params_from(p) -> OrcParams:
+    """Copy an rtmi RtParams (or any object with the same fields) into OrcParams."""
+    q = OrcParams()
+    for name, _ in OrcParams._fields_:
+        setattr(q, name, getattr(p, name))
+    return q
+
+
+def camera(pos, yaw_y=0.0, yaw_x=0.0) -> OrcCamera:
+    c = OrcCamera()
+    for i in range(4):
+        c.pos[i] = float(pos[i])
+    c.yaw_y = yaw_y
+    c.yaw_x = yaw_x
+    return c
+
+
+def render(geom, cam: OrcCamera, params: OrcParams, rect=None):
+    """geom: dict or object with tri/albedo/light/emission/light_group."""
+    get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
+    tri = np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32)
+    alb = np.ascontiguousarray(get("albedo"), np.float32)
+    em = np.ascontiguousarray(get("emission"), np.float32)
+    grp = np.ascontiguousarray(get("light_group"), np.int32)
+    n_surf, n_light = get("tri").shape[0], get("light").shape[0]
+    x0, y0, w, h = rect if rect is not None else (0, 0, params.width, params.height)
+    out = np.zeros((h, w, 3), np.float32)
+    casts = ctypes.c_uint64(0)
+    lib().orc_render(_f(tri), _f(alb), n_surf, _f(em), _i(grp), n_light, ctypes.byref(cam),
+                     ctypes.byref(params), x0, y0, w, h, _f(out), ctypes.byref(casts))
+    return out, int(casts.value)
+
+
+def pack_argb(rgb) -> np.ndarray:
+    a = np.ascontiguousarray(rgb, np.float32)
+    out = np.zeros(a.shape[:-1], np.uint32)
+    lib().orc_pack_argb(_f(a), a.size // 3, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+    return out
+
+
+def num_threads() -> int:
+    return int(lib().orc_num_threads())
+
+
+def set_threads(n: int) -> None:
+    lib().orc_set_threads(int(n))

@@ -1,0 +1,589 @@
+/*
+ * rt_oracle.c — CPU restatement of the reference's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the
+ * MI355X path tracer in reinforcement-light-rays-pathtracer_amd/.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * it; the product never links, includes or calls anything under oracle/.
+ *
+ * It is a clean-room restatement (plain C, written from reading the
+ * reference as text) of:
+ *   - the Cornell scene builders
+ *       CPU preset: Old_CPU_Rendering_Engine/Source/scenes/cornell_box_scene.cpp:3-205
+ *       GPU preset: GPU_Rendering_Engine/Source/scenes/cornell_box_scene.cu:4-... (emission 14*0.9, :81)
+ *   - triangle normal  normalize(cross(e2,e1))   CPU/objects/triangle.cpp:73-82
+ *   - ray construction / normalisation           CPU/rays/ray.cpp:7-11
+ *   - camera ray through a pixel + yaw rotation  CPU/path_tracing/default_path_tracing.cpp:25-34,
+ *                                                CPU/rays/ray.cpp:47-52, GPU/rays/ray.cu:143-172
+ *   - closest hit, surfaces then light planes    CPU/rays/ray.cpp:14-28, CPU/lights/area_light_plane.cpp:25-33
+ *   - the hit predicate:
+ *       rule 0 = the CPU engine's prebuilt object
+ *         Old_CPU_Rendering_Engine/CMakeFiles/Monte_Carlo_Raytracer.dir/Source/objects/triangle.cpp.o
+ *         (Triangle::intersects @0x460, disassembled):
+ *         inv = 1/detA; t,u,v = det_(t,u,v) * inv; accept iff t>=0,u>=0,v>=0,u+v<=1,
+ *         t < dist+1e-5, t > 1e-5
+ *       rule 1 = GPU/rays/ray.cu:38-141: t,u,v = det_(t,u,v) / detA; accept iff
+ *         t>=0,u>=0,v>=0,u+v<=1, t < dist (dist starts at 999999)
+ *     3x3 determinants in GLM's operation order
+ *     (glm/glm/detail/func_matrix.inl:210-220; confirmed in the .o's
+ *     compute_determinant<3,3,float> body)
+ *   - uniform hemisphere sampling + tangent frame CPU/utils/hemisphere_helpers.cpp:4-39,60-83
+ *   - Lambertian estimator, recursive (CPU)      CPU/path_tracing/default_path_tracing.cpp:46-101
+ *   - iterative throughput (GPU preset)          GPU/path_tracing/default_path_tracing.cu:36-88
+ *   - SPP mean                                   CPU/path_tracing/default_path_tracing.cpp:20-41
+ *   - ARGB pack                                  CPU/sdl/sdl_screen.cpp:100-112
+ *
+ * Random numbers: the reference draws from rand() (CPU) / cuRAND XORWOW
+ * (GPU); neither stream is reproducible on another machine or under
+ * OpenMP.  Both this oracle and the HIP kernels draw from a counter-based
+ * Philox4x32-10 keyed on (seed, global pixel, sample, event) — the spec in
+ * DESIGN.md §3.  sin/cos of 2*pi*r use the spec's own quarter-turn
+ * polynomial so host and device agree bit for bit.
+ *
+ * PARITY PINNING: the reference ships no tests and no golden outputs for
+ * this path; its code could not be compiled or run here (SURVEY.md §8(c),
+ * recorded denial).  The oracle is pinned by (1) the hit-predicate constants
+ * and operation order read from the prebuilt triangle.cpp.o, (2) the
+ * Random123 Philox known-answer vectors, (3) analytic intersection KATs,
+ * (4) the archway loader golden Radiance_Map_Data/vertices.txt, and
+ * (5) statistical agreement with the reference's committed Cornell renders
+ * (the PNGs under Images/cornell/).  See tests/.
+ *
+ * Build: gcc -O2 -ffp-contract=off -fno-fast-math -fopenmp -shared -fPIC
+ * (no FMA contraction: every float op is rounded exactly as written).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include <float.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define ORC_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------ */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants) */
+/* ------------------------------------------------------------------ */
+static void philox_round(uint32_t c[4], const uint32_t k[2]) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k[0];
+    uint32_t n2 = hi0 ^ c[3] ^ k[1];
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+}
+
+ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c[4] = {ctr_in[0], ctr_in[1], ctr_in[2], ctr_in[3]};
+    uint32_t k[2] = {key_in[0], key_in[1]};
+    for (int r = 0; r < 10; r++) {
+        philox_round(c, k);
+        k[0] += 0x9E3779B9u; k[1] += 0xBB67AE85u;
+    }
+    memcpy(out, c, sizeof(c));
+}
+
+/* uniform float in [0,1): top 24 bits */
+static float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+/* two uniforms for (pixel, sample, event) */
+static void draw2(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t event, float *a, float *b) {
+    uint32_t ctr[4] = {pixel, sample, event, 0u};
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t o[4];
+    orc_philox4x32_10(ctr, key, o);
+    *a = u01(o[0]);
+    *b = u01(o[1]);
+}
+
+/* ------------------------------------------------------------------ */
+/* sin/cos of a turn fraction (spec)                     */
+/* ------------------------------------------------------------------ */
+/* Taylor coefficients of sin(pi/2 f) and cos(pi/2 f) on f in [-1/2,1/2],
+ * rounded to float.  Horner, no contraction. */
+static const float S1 = 1.57079632679489662f;
+static const float S3 = -0.645964097506246254f;
+static const float S5 = 0.0796926262461670451f;
+static const float S7 = -0.00468175413531868810f;
+static const float S9 = 0.000160441184757112456f;
+static const float C2 = -1.23370055013616983f;
+static const float C4 = 0.253669507901048014f;
+static const float C6 = -0.0208634807633529609f;
+static const float C8 = 0.000919260274839426046f;
+static const float C10 = -0.0000252020423730606054f;
+
+ORC_API void orc_sincos_turn(float r, float *s_out, float *c_out) {
+    float x = r * 4.0f;                 /* exact */
+    float q = rintf(x);                 /* nearest quadrant (ties-to-even) */
+    float f = x - q;                    /* exact, in [-0.5, 0.5] */
+    int qi = ((int)q) & 3;
+    float f2 = f * f;
+    float sp = S9;
+    sp = sp * f2; sp = sp + S7;
+    sp = sp * f2; sp = sp + S5;
+    sp = sp * f2; sp = sp + S3;
+    sp = sp * f2; sp = sp + S1;
+    sp = sp * f;
+    float cp = C10;
+    cp = cp * f2; cp = cp + C8;
+    cp = cp * f2; cp = cp + C6;
+    cp = cp * f2; cp = cp + C4;
+    cp = cp * f2; cp = cp + C2;
+    cp = cp * f2; cp = cp + 1.0f;
+    float s, c;
+    switch (qi) {
+        case 0: s = sp; c = cp; break;
+        case 1: s = cp; c = -sp; break;
+        case 2: s = -sp; c = -cp; break;
+        default: s = -cp; c = sp; break;
+    }
+    *s_out = s; *c_out = c;
+}
+
+/* ------------------------------------------------------------------ */
+/* GLM-order vector helpers                                            */
+/* ------------------------------------------------------------------ */
+typedef struct { float x, y, z; } v3;
+
+static v3 mk(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+/* glm compute_dot<vec3>: tmp = a*b; (tmp.x + tmp.y) + tmp.z */
+static float dot3(v3 a, v3 b) { float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z; return (tx + ty) + tz; }
+/* glm normalize: v * inversesqrt(dot(v,v)), inversesqrt = 1/sqrt */
+static v3 normalize3(v3 v) {
+    float inv = 1.0f / sqrtf(dot3(v, v));
+    return mk(v.x * inv, v.y * inv, v.z * inv);
+}
+/* glm compute_cross */
+static v3 cross3(v3 x, v3 y) {
+    return mk(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+
+/* glm compute_determinant<3,3>: columns c0,c1,c2 (m[i][j] = column i, row j) */
+static float det3(v3 c0, v3 c1, v3 c2) {
+    float a = c0.x * (c1.y * c2.z - c2.y * c1.z);
+    float b = c1.x * (c0.y * c2.z - c2.y * c0.z);
+    float c = c2.x * (c0.y * c1.z - c1.y * c0.z);
+    return (a - b) + c;
+}
+
+/* ------------------------------------------------------------------ */
+/* scene                                                               */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int n_surf, n_light;
+    const float *tri;      /* (n_surf+n_light) x 9: v0,v1,v2 (surfaces first) */
+    const float *albedo;   /* n_surf x 3 */
+    const float *emission; /* n_light x 3 */
+    const int32_t *light_group; /* n_light: plane index (CPU light hit index) */
+    float *normal;         /* (n_surf+n_light) x 3, computed */
+} orc_scene;
+
+static v3 vtx(const float *tri, int i, int k) {
+    const float *p = tri + (size_t)i * 9 + k * 3;
+    return mk(p[0], p[1], p[2]);
+}
+
+/* CPU/objects/triangle.cpp:73-82 */
+ORC_API void orc_triangle_normals(const float *tri, int n, float *normal_out) {
+    for (int i = 0; i < n; i++) {
+        v3 v0 = vtx(tri, i, 0), v1 = vtx(tri, i, 1), v2 = vtx(tri, i, 2);
+        v3 e1 = mk(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
+        v3 e2 = mk(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
+        v3 n3 = normalize3(cross3(e2, e1));
+        normal_out[i * 3 + 0] = n3.x; normal_out[i * 3 + 1] = n3.y; normal_out[i * 3 + 2] = n3.z;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Cornell box builders                                                */
+/* ------------------------------------------------------------------ */
+typedef struct { float x, y, z; } p3;
+
+static void put_tri(float *dst, p3 a, p3 b, p3 c) {
+    dst[0] = a.x; dst[1] = a.y; dst[2] = a.z;
+    dst[3] = b.x; dst[4] = b.y; dst[5] = b.z;
+    dst[6] = c.x; dst[7] = c.y; dst[8] = c.z;
+}
+
+/* CPU/scenes/cornell_box_scene.cpp:161-199: v*(2/l) - 1, negate x and y. */
+static p3 cornell_xform(p3 v, float l) {
+    float s = 2.0f / l;
+    p3 r;
+    r.x = v.x * s; r.y = v.y * s; r.z = v.z * s;
+    r.x = r.x - 1.0f; r.y = r.y - 1.0f; r.z = r.z - 1.0f;
+    r.x = r.x * -1.0f; r.y = r.y * -1.0f;
+    return r;
+}
+
+/*
+ * variant 0 = CPU engine (one light plane K,I,J,L fanned into (K,I,J),(K,J,L),
+ *             emission 1*(1,1,0.9), light hit index = plane 0)
+ * variant 1 = GPU engine (two AreaLights (K,I,J),(K,J,L), emission 14*(0.9,0.9,0.9))
+ * Surfaces, in reference order: floor 2, left 2, right 2, ceiling 8, back 2,
+ * short block 10, tall block 10 = 36.
+ * Returns n_surf*9 + ... into caller arrays sized for 36 surfaces, 2 lights.
+ */
+ORC_API int orc_cornell(int variant, float *tri /*38x9*/, float *albedo /*36x3*/,
+                        float *emission /*2x3*/, int32_t *light_group /*2*/,
+                        int *n_surf, int *n_light) {
+    const float l = 555.0f;
+    p3 A = {l, 0, 0}, B = {0, 0, 0}, C = {l, 0, l}, D = {0, 0, l};
+    p3 E = {l, l, 0}, F = {0, l, 0}, G = {l, l, l}, H = {0, l, l};
+    p3 I = {l / 3.0f, l, (2.0f * l) / 3.0f}, J = {(2.0f * l) / 3.0f, l, (2.0f * l) / 3.0f};
+    p3 K = {l / 3.0f, l, l / 3.0f}, L = {(2.0f * l) / 3.0f, l, l / 3.0f};
+    const float blue[3] = {0.15f, 0.15f, 0.75f}, white[3] = {0.75f, 0.75f, 0.75f};
+    const float red[3] = {0.75f, 0.15f, 0.15f}, green[3] = {0.15f, 0.75f, 0.15f};
+    const float yellow[3] = {0.75f, 0.75f, 0.15f}, cyan[3] = {0.15f, 0.75f, 0.75f};
+    p3 raw[36][3];
+    const float *mat[36];
+    int k = 0;
+#define ADD(a, b, c, m) do { raw[k][0] = a; raw[k][1] = b; raw[k][2] = c; mat[k] = m; k++; } while (0)
+    ADD(C, B, A, green); ADD(C, D, B, green);
+    ADD(A, E, C, white); ADD(C, E, G, white);
+    ADD(F, B, D, white); ADD(H, F, D, white);
+    ADD(F, H, I, cyan); ADD(F, I, K, cyan); ADD(F, K, E, cyan); ADD(K, L, E, cyan);
+    ADD(L, G, E, cyan); ADD(L, J, G, cyan); ADD(I, G, J, cyan); ADD(H, G, I, cyan);
+    ADD(G, D, C, yellow); ADD(G, H, D, yellow);
+    {
+        p3 a = {240, 0, 234}, b = {80, 0, 185}, c = {190, 0, 392}, d = {32, 0, 345};
+        p3 e = {240, 165, 234}, f = {80, 165, 185}, g = {190, 165, 392}, h = {32, 165, 345};
+        ADD(e, b, a, blue); ADD(e, f, b, blue); ADD(f, d, b, blue); ADD(f, h, d, blue);
+        ADD(h, c, d, blue); ADD(h, g, c, blue); ADD(g, e, c, blue); ADD(e, a, c, blue);
+        ADD(g, f, e, blue); ADD(g, h, f, blue);
+    }
+    {
+        p3 a = {443, 0, 247}, b = {285, 0, 296}, c = {492, 0, 406}, d = {334, 0, 456};
+        p3 e = {443, 330, 247}, f = {285, 330, 296}, g = {492, 330, 406}, h = {334, 330, 456};
+        ADD(e, b, a, red); ADD(e, f, b, red); ADD(f, d, b, red); ADD(f, h, d, red);
+        ADD(h, c, d, red); ADD(h, g, c, red); ADD(g, e, c, red); ADD(e, a, c, red);
+        ADD(g, f, e, red); ADD(g, h, f, red);
+    }
+#undef ADD
+    for (int i = 0; i < 36; i++) {
+        put_tri(tri + i * 9, cornell_xform(raw[i][0], l), cornell_xform(raw[i][1], l), cornell_xform(raw[i][2], l));
+        albedo[i * 3 + 0] = mat[i][0]; albedo[i * 3 + 1] = mat[i][1]; albedo[i * 3 + 2] = mat[i][2];
+    }
+    p3 k2 = cornell_xform(K, l), i2 = cornell_xform(I, l), j2 = cornell_xform(J, l), l2 = cornell_xform(L, l);
+    put_tri(tri + 36 * 9, k2, i2, j2);
+    put_tri(tri + 37 * 9, k2, j2, l2);
+    if (variant == 0) {
+        /* vec3 diffuse_p = 1.f * vec3(1, 1, 0.9) */
+        for (int j = 0; j < 2; j++) {
+            emission[j * 3 + 0] = 1.0f * 1.0f; emission[j * 3 + 1] = 1.0f * 1.0f; emission[j * 3 + 2] = 1.0f * 0.9f;
+            light_group[j] = 0;
+        }
+    } else {
+        /* vec3 diffuse_p = 14.f * vec3(0.9, 0.9, 0.9) */
+        for (int j = 0; j < 2; j++) {
+            emission[j * 3 + 0] = 14.0f * 0.9f; emission[j * 3 + 1] = 14.0f * 0.9f; emission[j * 3 + 2] = 14.0f * 0.9f;
+            light_group[j] = j;
+        }
+    }
+    *n_surf = 36; *n_light = 2;
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* intersection                                                        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    float t;       /* distance in t_scale units */
+    int tri;       /* unified triangle index, -1 none */
+} hit_t;
+
+static hit_t closest_hit(const orc_scene *sc, v3 o, v3 d, float t_scale, int hit_rule) {
+    hit_t h;
+    h.tri = -1;
+    h.t = (hit_rule == 0) ? FLT_MAX : 999999.0f;
+    v3 D = mk(d.x * t_scale, d.y * t_scale, d.z * t_scale);
+    v3 nD = mk(-D.x, -D.y, -D.z);
+    int n = sc->n_surf + sc->n_light;
+    for (int i = 0; i < n; i++) {
+        v3 v0 = vtx(sc->tri, i, 0), v1 = vtx(sc->tri, i, 1), v2 = vtx(sc->tri, i, 2);
+        v3 e1 = mk(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
+        v3 e2 = mk(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
+        v3 b = mk(o.x - v0.x, o.y - v0.y, o.z - v0.z);
+        float detA = det3(nD, e1, e2);
+        if (!(detA != 0.0f)) continue;
+        float t, u, v;
+        if (hit_rule == 0) {
+            float inv = 1.0f / detA;
+            t = det3(b, e1, e2) * inv;
+            u = det3(nD, b, e2) * inv;
+            v = det3(nD, e1, b) * inv;
+            if (t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f &&
+                t < h.t + 1e-5f && t > 1e-5f) {
+                h.t = t; h.tri = i;
+            }
+        } else {
+            t = det3(b, e1, e2) / detA;
+            u = det3(nD, b, e2) / detA;
+            v = det3(nD, e1, b) / detA;
+            if (t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f && t < h.t) {
+                h.t = t; h.tri = i;
+            }
+        }
+    }
+    return h;
+}
+
+static int32_t pack_hit(const orc_scene *sc, int tri, int hit_rule) {
+    if (tri < 0) return -1;
+    if (tri < sc->n_surf) return (int32_t)((2u << 30) | (uint32_t)tri);
+    int j = tri - sc->n_surf;
+    int idx = (hit_rule == 0) ? sc->light_group[j] : j;
+    return (int32_t)((1u << 30) | (uint32_t)idx);
+}
+
+static void scene_init(orc_scene *sc, const float *tri, const float *albedo, int n_surf,
+                       const float *emission, const int32_t *light_group, int n_light) {
+    sc->n_surf = n_surf; sc->n_light = n_light;
+    sc->tri = tri; sc->albedo = albedo; sc->emission = emission; sc->light_group = light_group;
+    sc->normal = (float *)malloc(sizeof(float) * 3 * (size_t)(n_surf + n_light + 1));
+    orc_triangle_normals(tri, n_surf + n_light, sc->normal);
+}
+
+/* Ray-cast a batch: the standalone north-star kernel's contract.
+ * dir is normalised by the caller (as Ray::Ray does); t_scale = SCREEN_HEIGHT. */
+ORC_API void orc_intersect(const float *tri, int n_surf, int n_light, const int32_t *light_group,
+                           const float *orig, const float *dir, int n, float t_scale, int hit_rule,
+                           float *out_t, int32_t *out_hit) {
+    orc_scene sc;
+    scene_init(&sc, tri, NULL, n_surf, NULL, light_group, n_light);
+    #pragma omp parallel for schedule(static)
+    for (int r = 0; r < n; r++) {
+        v3 o = mk(orig[r * 3], orig[r * 3 + 1], orig[r * 3 + 2]);
+        v3 d = mk(dir[r * 3], dir[r * 3 + 1], dir[r * 3 + 2]);
+        hit_t h = closest_hit(&sc, o, d, t_scale, hit_rule);
+        out_t[r] = h.tri >= 0 ? h.t : INFINITY;
+        out_hit[r] = pack_hit(&sc, h.tri, hit_rule);
+    }
+    free(sc.normal);
+}
+
+/* ------------------------------------------------------------------ */
+/* sampling                                                            */
+/* ------------------------------------------------------------------ */
+/* CPU/utils/hemisphere_helpers.cpp:26-39 */
+static void normal_frame(v3 n, v3 *T, v3 *Bv) {
+    if (fabsf(n.x) > fabsf(n.y)) *T = normalize3(mk(n.z, 0.0f, -n.x));
+    else *T = normalize3(mk(0.0f, -n.z, n.y));
+    *Bv = cross3(n, *T);
+}
+
+/* CPU/utils/hemisphere_helpers.cpp:4-21 (sampler 0) + cosine variant (sampler 1);
+ * world = (s.x*B + s.y*N) + s.z*T, :73-77 */
+static v3 sample_dir(v3 n, float r1, float r2, int sampler, float *cos_theta) {
+    v3 T, Bv;
+    normal_frame(n, &T, &Bv);
+    float y, sin_theta;
+    if (sampler == 0) {
+        y = r1;
+        sin_theta = sqrtf(1.0f - r1 * r1);
+    } else {
+        y = sqrtf(r1);
+        sin_theta = sqrtf(1.0f - r1);
+    }
+    float sphi, cphi;
+    orc_sincos_turn(r2, &sphi, &cphi);
+    float sx = sin_theta * cphi, sz = sin_theta * sphi;
+    *cos_theta = y;
+    return mk((sx * Bv.x + y * n.x) + sz * T.x,
+              (sx * Bv.y + y * n.y) + sz * T.y,
+              (sx * Bv.z + y * n.z) + sz * T.z);
+}
+
+/* ------------------------------------------------------------------ */
+/* render                                                              */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int32_t width, height, spp, max_bounces, sampler, preset, hit_rule, spp_split;
+    uint64_t seed;
+    float env_light, t_scale;
+} orc_params;
+
+typedef struct { float pos[4]; float yaw_y, yaw_x; } orc_camera;
+
+static const float PI_F = 3.14159265358979323846f;  /* (float)M_PI */
+
+/* camera ray: CPU/path_tracing/default_path_tracing.cpp:25-34 + Ray::Ray + rotate_ray
+ * (glm mat4*vec4: (m0*v0 + m1*v1) + (m2*v2 + m3*v3), type_mat4x4.inl:561-570) */
+static void camera_ray(const orc_camera *cam, const orc_params *p, float cy, float sy, float cx, float sx,
+                       int px, int py, float r1, float r2, v3 *o, v3 *d) {
+    float x = (float)px + r1;
+    float y = (float)py + r2;
+    v3 dir = mk(x - (float)p->width / 2.0f, y - (float)p->height / 2.0f, (float)p->height);
+    dir = normalize3(dir);
+    /* yaw about y: R[0]=(c,0,s,0) R[1]=(0,1,0,0) R[2]=(-s,0,c,0) R[3]=(0,0,0,1), w=1 */
+    float w = 1.0f;
+    v3 r;
+    r.x = (cy * dir.x + 0.0f * dir.y) + (-sy * dir.z + 0.0f * w);
+    r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
+    r.z = (sy * dir.x + 0.0f * dir.y) + (cy * dir.z + 0.0f * w);
+    float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
+    if (p->preset == 1) {
+        /* GPU/rays/ray.cu:168-171: R[1]=(0,c,-s,0) R[2]=(0,s,c,0) about x */
+        v3 q;
+        q.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
+        q.y = (0.0f * r.x + cx * r.y) + (sx * r.z + 0.0f * rw);
+        q.z = (0.0f * r.x + -sx * r.y) + (cx * r.z + 0.0f * rw);
+        r = q;
+    }
+    *o = mk(cam->pos[0], cam->pos[1], cam->pos[2]);
+    *d = r;
+}
+
+/* CPU-engine recursion: path_trace_recursive / indirect_irradiance */
+static v3 trace_recursive(const orc_scene *sc, const orc_params *p, uint32_t pix, uint32_t smp,
+                          v3 o, v3 d, int bounces, uint64_t *casts) {
+    hit_t h = closest_hit(sc, o, d, p->t_scale, p->hit_rule);
+    (*casts)++;
+    if (h.tri < 0) return mk(0.0f, 0.0f, 0.0f);
+    if (h.tri >= sc->n_surf) {
+        const float *e = sc->emission + (size_t)(h.tri - sc->n_surf) * 3;
+        return mk(e[0], e[1], e[2]);
+    }
+    if (bounces == p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
+    /* position = o + t*D  (D = d*t_scale) */
+    v3 D = mk(d.x * p->t_scale, d.y * p->t_scale, d.z * p->t_scale);
+    v3 pos = mk(o.x + h.t * D.x, o.y + h.t * D.y, o.z + h.t * D.z);
+    const float *nn = sc->normal + (size_t)h.tri * 3;
+    float r1, r2;
+    draw2(p->seed, pix, smp, 1u + (uint32_t)bounces, &r1, &r2);
+    float cos_theta;
+    v3 s = sample_dir(mk(nn[0], nn[1], nn[2]), r1, r2, p->sampler, &cos_theta);
+    v3 start = mk(pos.x + 1e-5f * s.x, pos.y + 1e-5f * s.y, pos.z + 1e-5f * s.z);
+    v3 nd = normalize3(s);
+    v3 rad = trace_recursive(sc, p, pix, smp, start, nd, bounces + 1, casts);
+    const float *al = sc->albedo + (size_t)h.tri * 3;
+    v3 out;
+    if (p->sampler == 0) {
+        v3 brdf = mk(al[0] / PI_F, al[1] / PI_F, al[2] / PI_F);
+        float rho = 1.0f / (2.0f * PI_F);
+        out.x = ((rad.x * brdf.x) * cos_theta) / rho;
+        out.y = ((rad.y * brdf.y) * cos_theta) / rho;
+        out.z = ((rad.z * brdf.z) * cos_theta) / rho;
+    } else {
+        out = mk(rad.x * al[0], rad.y * al[1], rad.z * al[2]);
+    }
+    return out;
+}
+
+/* GPU-engine iteration: path_trace_iterative */
+static v3 trace_iterative(const orc_scene *sc, const orc_params *p, uint32_t pix, uint32_t smp,
+                          v3 o, v3 d, uint64_t *casts) {
+    v3 tp = mk(1.0f, 1.0f, 1.0f);
+    const float RHO = 1.0f / (2.0f * 3.1415926535f);
+    for (int i = 0; i < p->max_bounces; i++) {
+        hit_t h = closest_hit(sc, o, d, p->t_scale, p->hit_rule);
+        (*casts)++;
+        if (h.tri < 0) return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
+        if (h.tri >= sc->n_surf) {
+            const float *e = sc->emission + (size_t)(h.tri - sc->n_surf) * 3;
+            return mk(tp.x * e[0], tp.y * e[1], tp.z * e[2]);
+        }
+        v3 D = mk(d.x * p->t_scale, d.y * p->t_scale, d.z * p->t_scale);
+        v3 pos = mk(o.x + h.t * D.x, o.y + h.t * D.y, o.z + h.t * D.z);
+        const float *nn = sc->normal + (size_t)h.tri * 3;
+        float r1, r2;
+        draw2(p->seed, pix, smp, 1u + (uint32_t)i, &r1, &r2);
+        float cos_theta;
+        v3 s = sample_dir(mk(nn[0], nn[1], nn[2]), r1, r2, p->sampler, &cos_theta);
+        const float *al = sc->albedo + (size_t)h.tri * 3;
+        if (p->sampler == 0) {
+            v3 brdf = mk(al[0] / PI_F, al[1] / PI_F, al[2] / PI_F);
+            tp.x = ((tp.x * brdf.x) * cos_theta) / RHO;
+            tp.y = ((tp.y * brdf.y) * cos_theta) / RHO;
+            tp.z = ((tp.z * brdf.z) * cos_theta) / RHO;
+        } else {
+            tp = mk(tp.x * al[0], tp.y * al[1], tp.z * al[2]);
+        }
+        o = mk(pos.x + 1e-5f * s.x, pos.y + 1e-5f * s.y, pos.z + 1e-5f * s.z);
+        d = normalize3(s);
+    }
+    return mk(0.0f, 0.0f, 0.0f);
+}
+
+/*
+ * Render the rectangle [x0,x0+w) x [y0,y0+h) of a width x height image.
+ * out_rgb: w*h*3 floats, row-major (row = y - y0).  out_casts: total ray casts.
+ * Threads: OpenMP over rows (deterministic: the RNG is keyed per pixel).
+ */
+ORC_API int orc_render(const float *tri, const float *albedo, int n_surf,
+                       const float *emission, const int32_t *light_group, int n_light,
+                       const orc_camera *cam, const orc_params *p,
+                       int x0, int y0, int w, int h, float *out_rgb, uint64_t *out_casts) {
+    orc_scene sc;
+    scene_init(&sc, tri, albedo, n_surf, emission, light_group, n_light);
+    /* Camera trig evaluated once on the host in double, rounded to float
+     * (Ray::rotate_ray's cos(yaw)/sin(yaw)). */
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    uint64_t total = 0;
+    #pragma omp parallel for schedule(dynamic, 1) reduction(+:total)
+    for (int yy = 0; yy < h; yy++) {
+        for (int xx = 0; xx < w; xx++) {
+            int px = x0 + xx, py = y0 + yy;
+            uint32_t pix = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+            /* spp_split S: chunk c sums samples [c*m, (c+1)*m) in order (m = spp/S);
+             * the pixel sum is ((P0 + P1) + P2) + ...  (rtmi.h, rt_params.spp_split) */
+            int S = p->spp_split <= 0 ? 1 : p->spp_split;
+            int m = p->spp / S;
+            v3 acc = mk(0.0f, 0.0f, 0.0f);
+            uint64_t casts = 0;
+            for (int c = 0; c < S; c++) {
+                v3 part = mk(0.0f, 0.0f, 0.0f);
+                for (int s = c * m; s < (c + 1) * m; s++) {
+                    float r1, r2;
+                    draw2(p->seed, pix, (uint32_t)s, 0u, &r1, &r2);
+                    v3 o, d;
+                    camera_ray(cam, p, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                    v3 L = (p->preset == 0) ? trace_recursive(&sc, p, pix, (uint32_t)s, o, d, 0, &casts)
+                                            : trace_iterative(&sc, p, pix, (uint32_t)s, o, d, &casts);
+                    part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
+                }
+                if (c == 0) acc = part;
+                else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }
+            }
+            float fs = (float)p->spp;
+            float *dst = out_rgb + ((size_t)yy * w + xx) * 3;
+            dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+            total += casts;
+        }
+    }
+    free(sc.normal);
+    if (out_casts) *out_casts = total;
+    return 0;
+}
+
+/* CPU/sdl/sdl_screen.cpp:100-112: uint32(clamp(255*c, 0, 255)), (128<<24)+(r<<16)+(g<<8)+b */
+static uint32_t chan8(float c) {
+    float v = 255.0f * c;
+    v = v < 0.0f ? 0.0f : (v > 255.0f ? 255.0f : v);   /* glm::clamp = min(max(x,lo),hi) */
+    return (uint32_t)v;
+}
+
+ORC_API void orc_pack_argb(const float *rgb, int n, uint32_t *out) {
+    for (int i = 0; i < n; i++) {
+        out[i] = (128u << 24) + (chan8(rgb[i * 3]) << 16) + (chan8(rgb[i * 3 + 1]) << 8) + chan8(rgb[i * 3 + 2]);
+    }
+}
+
+ORC_API int orc_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
+
+ORC_API void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

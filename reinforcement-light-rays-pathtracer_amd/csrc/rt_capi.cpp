@@ -1,0 +1,427 @@
+// rt_capi.cpp — the C ABI (include/rtmi.h): contexts, device scenes,
+// launches.  Host-only code; the kernels live in rt_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/rtmi.h"
+#include "rt_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define RT_HIP(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(RT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_));       \
+    } while (0)
+
+}  // namespace
+
+namespace rt {
+int set_error(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace rt
+
+struct rt_ctx {
+    int device = 0;
+    // cached block list for rt_render_tiles_device
+    std::vector<int32_t> tiles_key;
+    int tiles_size = 0, tiles_w = 0, tiles_h = 0;
+    rt::BlockDesc* d_blocks = nullptr;
+    int n_blocks = 0;
+    int blocks_cap = 0;
+};
+
+struct rt_scene {
+    rt_ctx* ctx = nullptr;
+    rt::DeviceScene dev;
+    int n_surf = 0, n_light = 0;
+    std::vector<float> normals;  // host copy, n_tri x 3
+};
+
+namespace {
+
+int set_device(rt_ctx* ctx) {
+    RT_HIP(hipSetDevice(ctx->device));
+    return RT_OK;
+}
+
+int ensure_blocks(rt_ctx* ctx, const std::vector<rt::BlockDesc>& blocks) {
+    if ((int)blocks.size() > ctx->blocks_cap) {
+        if (ctx->d_blocks) RT_HIP(hipFree(ctx->d_blocks));
+        ctx->d_blocks = nullptr;
+        ctx->blocks_cap = 0;
+        RT_HIP(hipMalloc(&ctx->d_blocks, sizeof(rt::BlockDesc) * blocks.size()));
+        ctx->blocks_cap = (int)blocks.size();
+    }
+    if (!blocks.empty())
+        RT_HIP(hipMemcpy(ctx->d_blocks, blocks.data(), sizeof(rt::BlockDesc) * blocks.size(),
+                         hipMemcpyHostToDevice));
+    ctx->n_blocks = (int)blocks.size();
+    return RT_OK;
+}
+
+int check_params(const rt_params* p) {
+    if (!p) return fail(RT_E_INVALID, "params is NULL");
+    if (p->width <= 0 || p->height <= 0) return fail(RT_E_INVALID, "bad image size %dx%d", p->width, p->height);
+    if (p->spp <= 0) return fail(RT_E_INVALID, "spp must be > 0");
+    if (p->max_bounces < 0) return fail(RT_E_INVALID, "max_bounces must be >= 0");
+    if (p->preset != RT_PRESET_CPU && p->preset != RT_PRESET_GPU) return fail(RT_E_INVALID, "bad preset %d", p->preset);
+    if (p->sampler != RT_SAMPLER_UNIFORM && p->sampler != RT_SAMPLER_COSINE)
+        return fail(RT_E_INVALID, "bad sampler %d", p->sampler);
+    if (p->hit_rule != RT_HIT_RULE_CPU && p->hit_rule != RT_HIT_RULE_GPU)
+        return fail(RT_E_INVALID, "bad hit_rule %d", p->hit_rule);
+    if (p->preset == RT_PRESET_CPU && p->max_bounces > 2)
+        return fail(RT_E_UNSUPPORTED, "CPU preset supports max_bounces <= 2 (got %d)", p->max_bounces);
+    if (p->preset == RT_PRESET_GPU && p->max_bounces < 1)
+        return fail(RT_E_INVALID, "GPU preset needs max_bounces >= 1");
+    const int split = p->spp_split <= 0 ? 1 : p->spp_split;
+    if (split > 64 || (split & (split - 1)) != 0)
+        return fail(RT_E_INVALID, "spp_split must be a power of two <= 64 (got %d)", p->spp_split);
+    if (p->spp % split != 0) return fail(RT_E_INVALID, "spp_split %d does not divide spp %d", split, p->spp);
+    if ((int64_t)p->width * (int64_t)p->height > (int64_t)1 << 31)
+        return fail(RT_E_INVALID, "image too large");
+    return RT_OK;
+}
+
+rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p) {
+    rt::RenderLaunch a;
+    memset(&a, 0, sizeof(a));
+    a.scene = scene->dev;
+    a.width = p->width;
+    a.height = p->height;
+    a.spp = p->spp;
+    a.max_bounces = p->max_bounces;
+    a.split = p->spp_split <= 0 ? 1 : p->spp_split;
+    a.split_log2 = 0;
+    while ((1 << a.split_log2) < a.split) ++a.split_log2;
+    a.per_chunk = p->spp / a.split;
+    a.preset = p->preset;
+    a.sampler = p->sampler;
+    a.hit_rule = p->hit_rule;
+    a.seed_lo = (uint32_t)p->seed;
+    a.seed_hi = (uint32_t)(p->seed >> 32);
+    a.t_scale = p->t_scale;
+    a.env_light = p->env_light;
+    a.cam_x = cam->pos[0];
+    a.cam_y = cam->pos[1];
+    a.cam_z = cam->pos[2];
+    // Ray::rotate_ray's cos(yaw)/sin(yaw): evaluated once per frame on the host
+    a.cos_y = (float)cos((double)cam->yaw_y);
+    a.sin_y = (float)sin((double)cam->yaw_y);
+    a.cos_x = (float)cos((double)cam->yaw_x);
+    a.sin_x = (float)sin((double)cam->yaw_x);
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_last_error(void) { return g_err.c_str(); }
+
+int rt_params_default(int preset, rt_params* p) {
+    if (!p) return fail(RT_E_INVALID, "params is NULL");
+    memset(p, 0, sizeof(*p));
+    if (preset == RT_PRESET_CPU) {
+        p->width = 512; p->height = 512; p->spp = 16; p->max_bounces = 2;
+        p->hit_rule = RT_HIT_RULE_CPU;
+    } else if (preset == RT_PRESET_GPU) {
+        p->width = 720; p->height = 720; p->spp = 32; p->max_bounces = 80;
+        p->hit_rule = RT_HIT_RULE_GPU;
+    } else {
+        return fail(RT_E_INVALID, "bad preset %d", preset);
+    }
+    p->preset = preset;
+    p->sampler = RT_SAMPLER_UNIFORM;
+    p->spp_split = 1;
+    p->seed = 1984;
+    p->env_light = 0.0f;
+    p->t_scale = (float)p->height;
+    return RT_OK;
+}
+
+int rt_ctx_create(int device_ordinal, rt_ctx** out) {
+    if (!out) return fail(RT_E_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    RT_HIP(hipGetDeviceCount(&n));
+    if (device_ordinal < 0 || device_ordinal >= n)
+        return fail(RT_E_INVALID, "device %d out of range (%d devices)", device_ordinal, n);
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return fail(RT_E_NOMEM, "out of host memory");
+    c->device = device_ordinal;
+    int rc = set_device(c);
+    if (rc != RT_OK) {
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_ctx_destroy(rt_ctx* ctx) {
+    if (!ctx) return RT_OK;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->d_blocks) (void)hipFree(ctx->d_blocks);
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_surf,
+                    const float* light_v, const float* emission, const int32_t* light_group,
+                    int n_light, rt_scene** out) {
+    using rt::f3;
+    using rt::make3;
+    if (!ctx || !out) return fail(RT_E_INVALID, "ctx/out is NULL");
+    *out = nullptr;
+    if (n_surf < 0 || n_light < 0 || n_surf + n_light <= 0) return fail(RT_E_INVALID, "empty scene");
+    if ((n_surf > 0 && (!tri_v || !albedo)) || (n_light > 0 && (!light_v || !emission || !light_group)))
+        return fail(RT_E_INVALID, "missing scene arrays");
+    if (n_surf + n_light > (1 << 24)) return fail(RT_E_INVALID, "too many triangles");
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    const int n = n_surf + n_light;
+    std::vector<float4> isect((size_t)n * rt::kIsectF4);
+    std::vector<float4> shade((size_t)n * rt::kShadeF4);
+    std::vector<int32_t> code_cpu(n), code_gpu(n);
+    rt_scene* sc = new (std::nothrow) rt_scene();
+    if (!sc) return fail(RT_E_NOMEM, "out of host memory");
+    sc->ctx = ctx;
+    sc->n_surf = n_surf;
+    sc->n_light = n_light;
+    sc->normals.resize((size_t)n * 3);
+    for (int i = 0; i < n; ++i) {
+        const bool is_light = i >= n_surf;
+        const int j = is_light ? i - n_surf : i;
+        const float* v = is_light ? light_v + (size_t)j * 9 : tri_v + (size_t)j * 9;
+        const f3 v0 = make3(v[0], v[1], v[2]), v1 = make3(v[3], v[4], v[5]), v2 = make3(v[6], v[7], v[8]);
+        const f3 e1 = make3(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
+        const f3 e2 = make3(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
+        // c0 = m11*m22 - m21*m12 of [-D | e1 | e2]
+        const float c0 = e1.y * e2.z - e2.y * e1.z;
+        isect[(size_t)i * 3 + 0] = make_float4(v0.x, v0.y, v0.z, c0);
+        isect[(size_t)i * 3 + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
+        isect[(size_t)i * 3 + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+        // Triangle::compute_and_set_normal: normalize(cross(e2, e1))
+        const f3 N = rt::normalize(rt::cross(e2, e1));
+        f3 T, B;
+        rt::normal_frame(N, &T, &B);
+        sc->normals[(size_t)i * 3 + 0] = N.x;
+        sc->normals[(size_t)i * 3 + 1] = N.y;
+        sc->normals[(size_t)i * 3 + 2] = N.z;
+        shade[(size_t)i * 5 + 0] = make_float4(N.x, N.y, N.z, 0.0f);
+        shade[(size_t)i * 5 + 1] = make_float4(T.x, T.y, T.z, 0.0f);
+        shade[(size_t)i * 5 + 2] = make_float4(B.x, B.y, B.z, 0.0f);
+        if (is_light) {
+            const float* e = emission + (size_t)j * 3;
+            shade[(size_t)i * 5 + 3] = make_float4(e[0], e[1], e[2], 0.0f);
+            shade[(size_t)i * 5 + 4] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            code_cpu[i] = (int32_t)((RT_HIT_TYPE_LIGHT << 30) | (uint32_t)light_group[j]);
+            code_gpu[i] = (int32_t)((RT_HIT_TYPE_LIGHT << 30) | (uint32_t)j);
+        } else {
+            const float* al = albedo + (size_t)j * 3;
+            // BRDF = reflectance / M_PI (default_path_tracing.cpp:95)
+            shade[(size_t)i * 5 + 3] = make_float4(al[0] / rt::kPi, al[1] / rt::kPi, al[2] / rt::kPi, 0.0f);
+            shade[(size_t)i * 5 + 4] = make_float4(al[0], al[1], al[2], 0.0f);
+            code_cpu[i] = code_gpu[i] = (int32_t)((RT_HIT_TYPE_SURFACE << 30) | (uint32_t)j);
+        }
+    }
+    sc->dev.n_surf = n_surf;
+    sc->dev.n_tri = n;
+    auto cleanup = [&]() {
+        if (sc->dev.isect) (void)hipFree(sc->dev.isect);
+        if (sc->dev.shade) (void)hipFree(sc->dev.shade);
+        if (sc->dev.code_cpu) (void)hipFree(sc->dev.code_cpu);
+        if (sc->dev.code_gpu) (void)hipFree(sc->dev.code_gpu);
+        delete sc;
+    };
+    hipError_t e = hipMalloc(&sc->dev.isect, sizeof(float4) * isect.size());
+    if (e == hipSuccess) e = hipMalloc(&sc->dev.shade, sizeof(float4) * shade.size());
+    if (e == hipSuccess) e = hipMalloc(&sc->dev.code_cpu, sizeof(int32_t) * n);
+    if (e == hipSuccess) e = hipMalloc(&sc->dev.code_gpu, sizeof(int32_t) * n);
+    if (e == hipSuccess) e = hipMemcpy(sc->dev.isect, isect.data(), sizeof(float4) * isect.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sc->dev.shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sc->dev.code_cpu, code_cpu.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(sc->dev.code_gpu, code_gpu.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        cleanup();
+        return fail(RT_E_HIP, "scene upload failed: %s", hipGetErrorString(e));
+    }
+    *out = sc;
+    return RT_OK;
+}
+
+int rt_scene_destroy(rt_scene* scene) {
+    if (!scene) return RT_OK;
+    (void)hipSetDevice(scene->ctx->device);
+    (void)hipFree(scene->dev.isect);
+    (void)hipFree(scene->dev.shade);
+    (void)hipFree(scene->dev.code_cpu);
+    (void)hipFree(scene->dev.code_gpu);
+    delete scene;
+    return RT_OK;
+}
+
+int rt_scene_normals(const rt_scene* scene, float* out) {
+    if (!scene || !out) return fail(RT_E_INVALID, "scene/out is NULL");
+    memcpy(out, scene->normals.data(), sizeof(float) * scene->normals.size());
+    return RT_OK;
+}
+
+int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig, const float* d_dir,
+                        int n, float t_scale, int hit_rule, float* d_t, int32_t* d_hit, void* stream) {
+    if (!ctx || !scene) return fail(RT_E_INVALID, "ctx/scene is NULL");
+    if (n < 0) return fail(RT_E_INVALID, "n < 0");
+    if (n > 0 && (!d_orig || !d_dir || !d_t || !d_hit)) return fail(RT_E_INVALID, "NULL buffer");
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    RT_HIP(rt::launch_intersect(scene->dev, d_orig, d_dir, n, t_scale, hit_rule, d_t, d_hit,
+                                (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
+                 float t_scale, int hit_rule, float* out_t, int32_t* out_hit) {
+    if (!ctx || !scene) return fail(RT_E_INVALID, "ctx/scene is NULL");
+    if (n < 0) return fail(RT_E_INVALID, "n < 0");
+    if (n == 0) return RT_OK;
+    if (!orig || !dir || !out_t || !out_hit) return fail(RT_E_INVALID, "NULL buffer");
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
+    int32_t* d_h = nullptr;
+    const size_t b3 = sizeof(float) * 3 * (size_t)n;
+    hipError_t e = hipMalloc(&d_o, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_d, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_t, sizeof(float) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(d_o, orig, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_d, dir, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, d_t, d_h, 0);
+    if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_o);
+    (void)hipFree(d_d);
+    (void)hipFree(d_t);
+    (void)hipFree(d_h);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
+              int x0, int y0, int w, int h, float* out_rgb, uint64_t* out_ray_casts) {
+    if (!ctx || !scene || !cam || !out_rgb) return fail(RT_E_INVALID, "NULL argument");
+    int rc = check_params(params);
+    if (rc != RT_OK) return rc;
+    if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > params->width || y0 + h > params->height)
+        return fail(RT_E_INVALID, "rectangle outside the image");
+    rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    std::vector<rt::BlockDesc> blocks;
+    for (int by = 0; by < h; by += 16)
+        for (int bx = 0; bx < w; bx += 16) blocks.push_back({x0 + bx, y0 + by, bx, by});
+    rt::BlockDesc* d_blocks = nullptr;
+    float* d_out = nullptr;
+    unsigned long long* d_casts = nullptr;
+    const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
+    hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
+    if (e == hipSuccess) e = hipMalloc(&d_out, out_bytes);
+    if (e == hipSuccess) e = hipMalloc(&d_casts, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_casts, 0, sizeof(unsigned long long));
+    if (e == hipSuccess)
+        e = hipMemcpy(d_blocks, blocks.data(), sizeof(rt::BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        rt::RenderLaunch a = make_launch(scene, cam, params);
+        a.blocks = d_blocks;
+        a.n_blocks = (int)blocks.size();
+        a.clip_x1 = x0 + w;
+        a.clip_y1 = y0 + h;
+        a.out_pitch = w;
+        a.out = d_out;
+        a.casts = d_casts;
+        e = rt::launch_render(a, 0);
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, out_bytes, hipMemcpyDeviceToHost);
+    unsigned long long casts = 0;
+    if (e == hipSuccess) e = hipMemcpy(&casts, d_casts, sizeof(casts), hipMemcpyDeviceToHost);
+    (void)hipFree(d_blocks);
+    (void)hipFree(d_out);
+    (void)hipFree(d_casts);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_render: %s", hipGetErrorString(e));
+    if (out_ray_casts) *out_ray_casts = casts;
+    return RT_OK;
+}
+
+int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam,
+                           const rt_params* params, const int32_t* tiles, int n_tiles, int tile_size,
+                           float* d_out, uint64_t* d_casts, void* stream) {
+    if (!ctx || !scene || !cam) return fail(RT_E_INVALID, "NULL argument");
+    int rc = check_params(params);
+    if (rc != RT_OK) return rc;
+    if (n_tiles < 0) return fail(RT_E_INVALID, "n_tiles < 0");
+    if (n_tiles == 0) return RT_OK;
+    if (!tiles || !d_out) return fail(RT_E_INVALID, "NULL tiles/out");
+    if (tile_size <= 0 || tile_size % 16 != 0) return fail(RT_E_INVALID, "tile_size must be a positive multiple of 16");
+    for (int k = 0; k < n_tiles; ++k) {
+        const int tx = tiles[2 * k], ty = tiles[2 * k + 1];
+        if (tx < 0 || ty < 0 || tx >= params->width || ty >= params->height)
+            return fail(RT_E_INVALID, "tile %d origin (%d,%d) outside the image", k, tx, ty);
+    }
+    rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    const bool same = ctx->tiles_size == tile_size && ctx->tiles_w == params->width &&
+                      ctx->tiles_h == params->height && (int)ctx->tiles_key.size() == 2 * n_tiles &&
+                      memcmp(ctx->tiles_key.data(), tiles, sizeof(int32_t) * 2 * n_tiles) == 0;
+    if (!same) {
+        std::vector<rt::BlockDesc> blocks;
+        const int per = tile_size / 16;
+        for (int k = 0; k < n_tiles; ++k)
+            for (int sy = 0; sy < per; ++sy)
+                for (int sx = 0; sx < per; ++sx)
+                    blocks.push_back({tiles[2 * k] + 16 * sx, tiles[2 * k + 1] + 16 * sy, 16 * sx,
+                                      k * tile_size + 16 * sy});
+        rc = ensure_blocks(ctx, blocks);
+        if (rc != RT_OK) return rc;
+        ctx->tiles_key.assign(tiles, tiles + 2 * n_tiles);
+        ctx->tiles_size = tile_size;
+        ctx->tiles_w = params->width;
+        ctx->tiles_h = params->height;
+    }
+    rt::RenderLaunch a = make_launch(scene, cam, params);
+    a.blocks = ctx->d_blocks;
+    a.n_blocks = ctx->n_blocks;
+    a.clip_x1 = params->width;
+    a.clip_y1 = params->height;
+    a.out_pitch = tile_size;
+    a.out = d_out;
+    a.casts = reinterpret_cast<unsigned long long*>(d_casts);
+    RT_HIP(rt::launch_render(a, (hipStream_t)stream));
+    return RT_OK;
+}
+
+}  // extern "C"

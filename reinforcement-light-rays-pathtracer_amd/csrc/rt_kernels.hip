@@ -1,0 +1,387 @@
+// rt_kernels.hip — gfx950 kernels of the path tracer's hot path.
+//
+//  k_intersect : Ray::closest_intersection over a batch of rays (one lane per
+//                ray) — the reference's innermost loop (CPU/rays/ray.cpp:14-28,
+//                GPU/rays/ray.cu:16-141) as a standalone kernel.
+//  k_render    : the per-pixel trace loop (pixel -> SPP -> bounce) as one
+//                megakernel: camera ray, closest hit, uniform-hemisphere
+//                sampling, Lambertian estimator, SPP mean
+//                (CPU/path_tracing/default_path_tracing.cpp:5-101,
+//                GPU/path_tracing/default_path_tracing.cu:7-88).
+//
+// CDNA4 mapping:
+//  * one lane = one (pixel, sample chunk); a pixel's `split` chunks sit in
+//    adjacent lanes and are folded with wave shuffles in a fixed order; a
+//    16x16 pixel block is `split` workgroups of 256 threads.  A lane runs its
+//    chunk's samples in order and
+//    regenerates a camera ray the moment its path ends, so every lane casts a
+//    ray on every loop trip until its pixel is done (no idle lanes waiting
+//    for the longest path of the wave); the loop exit is a wave ballot.
+//  * the triangle loop index is wave-uniform: the triangle records are
+//    fetched with scalar loads (s_load_dwordx4) into SGPRs and broadcast as
+//    VALU operands — no LDS round trip and no per-lane address math.
+//  * per-pixel sums are kept in registers in sample order, so the image is
+//    bit-identical to the CPU restatement (oracle/) and to any tiling.
+//
+// Numerics: built with -ffp-contract=off and hipcc's default correctly
+// rounded fp32 division / sqrt; no fast-math (see rt_math.hpp).
+
+#include <float.h>
+
+#include "rt_internal.hpp"
+
+namespace rt {
+
+namespace {
+
+constexpr float kRho = 1.0f / (2.0f * kPi);  // RHO: GPU/constants/image_settings.h:14
+
+struct Hit {
+    float t;
+    int tri;
+};
+
+// Closest hit over the triangle soup.  D = dir * t_scale, A = [-D | e1 | e2],
+// x = (t,u,v) by Cramer's rule with GLM's determinant order
+// (glm/glm/detail/func_matrix.inl:214-217):
+//   det(c0,c1,c2) = (c0.x*(c1.y*c2.z - c2.y*c1.z) - c1.x*(c0.y*c2.z - c2.y*c0.z))
+//                   + c2.x*(c0.y*c1.z - c1.y*c0.z)
+// The minors shared between detA, det_t, det_u and det_v are evaluated once
+// (same operands, same order, so the same bits).
+// RULE 0 = CPU triangle.cpp.o predicate (inv = 1/detA; accept t>=0, u>=0, v>=0,
+//          u+v<=1, t < best+1e-5, t > 1e-5; best starts at FLT_MAX)
+// RULE 1 = GPU/rays/ray.cu:63-64 (true divisions; t < best; best starts 999999)
+template <int RULE>
+__device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n_tri, f3 o, f3 d,
+                                           float t_scale) {
+    const float nDx = -(d.x * t_scale);
+    const float nDy = -(d.y * t_scale);
+    const float nDz = -(d.z * t_scale);
+    Hit h;
+    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+    h.tri = -1;
+    for (int i = 0; i < n_tri; ++i) {
+        const float4 A = tri[i * kIsectF4 + 0];
+        const float4 E1 = tri[i * kIsectF4 + 1];
+        const float4 E2 = tri[i * kIsectF4 + 2];
+        const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
+        // detA = det(-D, e1, e2)
+        const float s1 = nDy * E2.z - E2.y * nDz;
+        const float s2 = nDy * E1.z - E1.y * nDz;
+        const float detA = (nDx * A.w - E1.x * s1) + E2.x * s2;
+        // det_t = det(b, e1, e2)
+        const float s3 = by * E2.z - E2.y * bz;
+        const float s4 = by * E1.z - E1.y * bz;
+        const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
+        float t;
+        if (RULE == 0) {
+            const float inv = 1.0f / detA;
+            t = det_t * inv;
+            const bool tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t + kEps) && (t > kEps);
+            if (tpass) {
+                // det_u = det(-D, b, e2), det_v = det(-D, e1, b)
+                const float s5 = nDy * bz - by * nDz;
+                const float s6 = E1.y * bz - by * E1.z;
+                const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+                const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+                const float u = det_u * inv;
+                const float v = det_v * inv;
+                if (u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
+                    h.t = t;
+                    h.tri = i;
+                }
+            }
+        } else {
+            t = det_t / detA;
+            const bool tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t);
+            if (tpass) {
+                const float s5 = nDy * bz - by * nDz;
+                const float s6 = E1.y * bz - by * E1.z;
+                const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+                const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+                const float u = det_u / detA;
+                const float v = det_v / detA;
+                if (u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
+                    h.t = t;
+                    h.tri = i;
+                }
+            }
+        }
+    }
+    return h;
+}
+
+template <int RULE>
+__global__ __launch_bounds__(256) void k_intersect(const float4* __restrict__ tri, int n_tri,
+                                                   const int32_t* __restrict__ code,
+                                                   const float* __restrict__ orig,
+                                                   const float* __restrict__ dir, int n,
+                                                   float t_scale, float* __restrict__ out_t,
+                                                   int32_t* __restrict__ out_hit) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const f3 o = make3(orig[3 * r + 0], orig[3 * r + 1], orig[3 * r + 2]);
+    const f3 d = make3(dir[3 * r + 0], dir[3 * r + 1], dir[3 * r + 2]);
+    const Hit h = closest_hit<RULE>(tri, n_tri, o, d, t_scale);
+    out_t[r] = (h.tri >= 0) ? h.t : __builtin_inff();
+    out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
+}
+
+// two uniforms of event `ev` of sample `smp` of pixel `pix`
+__device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, uint32_t k0,
+                                      uint32_t k1, float* a, float* b) {
+    uint32_t o[4];
+    philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
+    *a = u01(o[0]);
+    *b = u01(o[1]);
+}
+
+// Camera ray through (px+r1, py+r2): default_path_tracing.cpp:25-34, Ray::Ray
+// (ray.cpp:7-11), rotate_ray (ray.cpp:47-52; GPU/rays/ray.cu:161-172), with
+// glm's mat4*vec4 order (m0*v0 + m1*v1) + (m2*v2 + m3*v3).
+template <int PRESET>
+__device__ __forceinline__ void camera_ray(const RenderLaunch& a, int px, int py, float r1, float r2,
+                                           f3* d_out) {
+    const float x = (float)px + r1;
+    const float y = (float)py + r2;
+    f3 dir = make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height);
+    dir = normalize(dir);
+    const float w = 1.0f;
+    f3 r;
+    r.x = (a.cos_y * dir.x + 0.0f * dir.y) + (-a.sin_y * dir.z + 0.0f * w);
+    r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
+    r.z = (a.sin_y * dir.x + 0.0f * dir.y) + (a.cos_y * dir.z + 0.0f * w);
+    if (PRESET == 1) {
+        const float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
+        f3 q;
+        q.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
+        q.y = (0.0f * r.x + a.cos_x * r.y) + (a.sin_x * r.z + 0.0f * rw);
+        q.z = (0.0f * r.x + -a.sin_x * r.y) + (a.cos_x * r.z + 0.0f * rw);
+        r = q;
+    }
+    *d_out = r;
+}
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// PRESET 0: CPU engine recursion (a path's value is folded from the light
+// back to the camera: L_k = ((L_{k+1} * brdf_k) * cos_k) / rho), cap <= 2.
+// PRESET 1: GPU engine iterative throughput.
+template <int PRESET, int SAMPLER, int RULE>
+__global__ __launch_bounds__(256) void k_render(const RenderLaunch a) {
+    // workgroup -> (16x16 block, part); lane -> (pixel of the block, sample chunk)
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    const int part = blockIdx.x & (a.split - 1);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int chunk = threadIdx.x & (a.split - 1);
+    const int lane = threadIdx.x & 63;
+    const int lx = q & 15;
+    const int ly = q >> 4;
+    const int px = blk.px0 + lx;
+    const int py = blk.py0 + ly;
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+    const float4* __restrict__ tri = a.scene.isect;
+    const float4* __restrict__ shade = a.scene.shade;
+    const int n_surf = a.scene.n_surf;
+    const int n_tri = a.scene.n_tri;
+    const int s_end = (chunk + 1) * a.per_chunk;
+
+    int s = valid ? chunk * a.per_chunk : s_end;  // current sample
+    int depth = 0;              // surface bounces so far on this path
+    f3 o = make3(a.cam_x, a.cam_y, a.cam_z);
+    f3 d = make3(0.0f, 0.0f, 1.0f);
+    f3 acc = make3(0.0f, 0.0f, 0.0f);
+    f3 tp = make3(1.0f, 1.0f, 1.0f);     // PRESET 1 throughput
+    int f_tri0 = 0, f_tri1 = 0;          // PRESET 0 factors (cap <= 2)
+    float f_cos0 = 0.0f, f_cos1 = 0.0f;
+    unsigned n_casts = 0;
+
+    if (s < s_end) {
+        float r1, r2;
+        draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        camera_ray<PRESET>(a, px, py, r1, r2, &d);
+    }
+
+    for (;;) {
+        const bool active = s < s_end;
+        if (__ballot(active) == 0ull) break;
+        if (!active) continue;
+
+        const Hit h = closest_hit<RULE>(tri, n_tri, o, d, a.t_scale);
+        ++n_casts;
+
+        bool terminal = false;
+        f3 L = make3(0.0f, 0.0f, 0.0f);
+        if (h.tri < 0) {
+            terminal = true;
+            if (PRESET == 1) L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+        } else if (h.tri >= n_surf) {
+            terminal = true;
+            const float4 e = shade[h.tri * kShadeF4 + 3];
+            if (PRESET == 0) {
+                L = make3(e.x, e.y, e.z);
+                if (depth >= 2) {
+                    const float4 c = shade[f_tri1 * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
+                    if (SAMPLER == 0) {
+                        L.x = ((L.x * c.x) * f_cos1) / kRho;
+                        L.y = ((L.y * c.y) * f_cos1) / kRho;
+                        L.z = ((L.z * c.z) * f_cos1) / kRho;
+                    } else {
+                        L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
+                    }
+                }
+                if (depth >= 1) {
+                    const float4 c = shade[f_tri0 * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
+                    if (SAMPLER == 0) {
+                        L.x = ((L.x * c.x) * f_cos0) / kRho;
+                        L.y = ((L.y * c.y) * f_cos0) / kRho;
+                        L.z = ((L.z * c.z) * f_cos0) / kRho;
+                    } else {
+                        L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
+                    }
+                }
+            } else {
+                L = make3(tp.x * e.x, tp.y * e.y, tp.z * e.z);
+            }
+        } else if (PRESET == 0 && depth == a.max_bounces) {
+            terminal = true;  // bounces == MAX_RAY_BOUNCES -> vec3(0)
+        } else {
+            // surface: position, sample a direction, update the estimator
+            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+            const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+            const float4 N = shade[h.tri * kShadeF4 + 0];
+            const float4 T = shade[h.tri * kShadeF4 + 1];
+            const float4 B = shade[h.tri * kShadeF4 + 2];
+            float r1, r2;
+            draw2(pix, (uint32_t)s, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+            float cos_theta, sin_theta;
+            if (SAMPLER == 0) {
+                cos_theta = r1;
+                sin_theta = sqrtf(1.0f - r1 * r1);
+            } else {
+                cos_theta = sqrtf(r1);
+                sin_theta = sqrtf(1.0f - r1);
+            }
+            float sphi, cphi;
+            sincos_turn(r2, &sphi, &cphi);
+            const float sx = sin_theta * cphi, sz = sin_theta * sphi;
+            const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
+                                (sx * B.y + cos_theta * N.y) + sz * T.y,
+                                (sx * B.z + cos_theta * N.z) + sz * T.z);
+            if (PRESET == 0) {
+                if (depth == 0) {
+                    f_tri0 = h.tri;
+                    f_cos0 = cos_theta;
+                } else {
+                    f_tri1 = h.tri;
+                    f_cos1 = cos_theta;
+                }
+            } else {
+                if (SAMPLER == 0) {
+                    const float4 c = shade[h.tri * kShadeF4 + 3];
+                    tp.x = ((tp.x * c.x) * cos_theta) / kRho;
+                    tp.y = ((tp.y * c.y) * cos_theta) / kRho;
+                    tp.z = ((tp.z * c.z) * cos_theta) / kRho;
+                } else {
+                    const float4 c = shade[h.tri * kShadeF4 + 4];
+                    tp = make3(tp.x * c.x, tp.y * c.y, tp.z * c.z);
+                }
+            }
+            o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
+            d = normalize(sd);
+            ++depth;
+            if (PRESET == 1 && depth == a.max_bounces) terminal = true;  // loop exhausted -> 0
+        }
+
+        if (terminal) {
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+            ++s;
+            depth = 0;
+            tp = make3(1.0f, 1.0f, 1.0f);
+            o = make3(a.cam_x, a.cam_y, a.cam_z);
+            if (s < s_end) {
+                float r1, r2;
+                draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+                camera_ray<PRESET>(a, px, py, r1, r2, &d);
+            }
+        }
+    }
+
+    // fold the chunk sums of a pixel in chunk order: ((P0 + P1) + P2) + ...
+    const int base = lane & ~(a.split - 1);
+    f3 tot = acc;
+    for (int k = 1; k < a.split; ++k) {
+        const float vx = __shfl(acc.x, base + k, 64);
+        const float vy = __shfl(acc.y, base + k, 64);
+        const float vz = __shfl(acc.z, base + k, 64);
+        tot.x = tot.x + vx;
+        tot.y = tot.y + vy;
+        tot.z = tot.z + vz;
+    }
+    if (valid && chunk == 0) {
+        const float fs = (float)a.spp;
+        float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+        dst[0] = tot.x / fs;
+        dst[1] = tot.y / fs;
+        dst[2] = tot.z / fs;
+    }
+    if (a.casts != nullptr) {
+        const unsigned total = wave_sum(n_casts);
+        if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
+                            float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
+                            hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    const dim3 block(256);
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (hit_rule == 0) {
+        hipLaunchKernelGGL(k_intersect<0>, grid, block, 0, stream, s.isect, s.n_tri, s.code_cpu,
+                           orig, dir, n, t_scale, out_t, out_hit);
+    } else {
+        hipLaunchKernelGGL(k_intersect<1>, grid, block, 0, stream, s.isect, s.n_tri, s.code_gpu,
+                           orig, dir, n, t_scale, out_t, out_hit);
+    }
+    return hipGetLastError();
+}
+
+template <int PRESET, int SAMPLER, int RULE>
+static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
+    hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE>), dim3((unsigned)(a.n_blocks * a.split)),
+                       dim3(256), 0, stream, a);
+}
+
+hipError_t launch_render(const RenderLaunch& a, hipStream_t stream) {
+    if (a.n_blocks <= 0) return hipSuccess;
+    if (a.preset == 0 && a.max_bounces > 2) return hipErrorInvalidValue;
+    if (a.split < 1 || a.split > 64 || (a.split & (a.split - 1)) != 0 || (1 << a.split_log2) != a.split ||
+        a.per_chunk * a.split != a.spp)
+        return hipErrorInvalidValue;
+    const int key = a.preset * 4 + a.sampler * 2 + a.hit_rule;
+    switch (key) {
+        case 0: launch_render_t<0, 0, 0>(a, stream); break;
+        case 1: launch_render_t<0, 0, 1>(a, stream); break;
+        case 2: launch_render_t<0, 1, 0>(a, stream); break;
+        case 3: launch_render_t<0, 1, 1>(a, stream); break;
+        case 4: launch_render_t<1, 0, 0>(a, stream); break;
+        case 5: launch_render_t<1, 0, 1>(a, stream); break;
+        case 6: launch_render_t<1, 1, 0>(a, stream); break;
+        case 7: launch_render_t<1, 1, 1>(a, stream); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,118 @@
+// rt_math.hpp — scalar math shared by the host scene builder and the gfx950
+// kernels.  Every function is written so that host (x86-64, SSE) and device
+// (gfx950) evaluate the same IEEE-754 binary32 operations in the same order:
+// build with -ffp-contract=off, correctly-rounded division and sqrt (hipcc's
+// default), no fast-math.  The operation orders follow GLM 0.9.9.3 as vendored
+// by the reference (glm/glm/detail/func_geometric.inl:48-89,
+// func_matrix.inl:210-220) because the reference computes with GLM.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RT_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define RT_HD inline
+#endif
+
+namespace rt {
+
+struct f3 {
+    float x, y, z;
+};
+
+RT_HD f3 make3(float x, float y, float z) {
+    f3 r;
+    r.x = x; r.y = y; r.z = z;
+    return r;
+}
+
+// glm compute_dot<vec3>: tmp = a*b; (tmp.x + tmp.y) + tmp.z
+RT_HD float dot(f3 a, f3 b) {
+    float tx = a.x * b.x;
+    float ty = a.y * b.y;
+    float tz = a.z * b.z;
+    return (tx + ty) + tz;
+}
+
+// glm normalize: v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
+RT_HD f3 normalize(f3 v) {
+    float inv = 1.0f / sqrtf(dot(v, v));
+    return make3(v.x * inv, v.y * inv, v.z * inv);
+}
+
+// glm compute_cross
+RT_HD f3 cross(f3 x, f3 y) {
+    return make3(x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y);
+}
+
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11).  Counter
+// (pixel, sample, event, 0), key (seed_lo, seed_hi): DESIGN.md §3.
+RT_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                         uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// 24-bit uniform in [0, 1)
+RT_HD float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+
+// sin(2*pi*r), cos(2*pi*r) by quarter-turn reduction (exact) and Taylor
+// polynomials of sin(pi/2 f), cos(pi/2 f) on f in [-1/2, 1/2] (Horner, no FMA).
+RT_HD void sincos_turn(float r, float* s_out, float* c_out) {
+    const float S1 = 1.57079632679489662f, S3 = -0.645964097506246254f,
+                S5 = 0.0796926262461670451f, S7 = -0.00468175413531868810f,
+                S9 = 0.000160441184757112456f;
+    const float C2 = -1.23370055013616983f, C4 = 0.253669507901048014f,
+                C6 = -0.0208634807633529609f, C8 = 0.000919260274839426046f,
+                C10 = -0.0000252020423730606054f;
+    float x = r * 4.0f;
+    float q = rintf(x);
+    float f = x - q;
+    int qi = ((int)q) & 3;
+    float f2 = f * f;
+    float sp = S9;
+    sp = sp * f2; sp = sp + S7;
+    sp = sp * f2; sp = sp + S5;
+    sp = sp * f2; sp = sp + S3;
+    sp = sp * f2; sp = sp + S1;
+    sp = sp * f;
+    float cp = C10;
+    cp = cp * f2; cp = cp + C8;
+    cp = cp * f2; cp = cp + C6;
+    cp = cp * f2; cp = cp + C4;
+    cp = cp * f2; cp = cp + C2;
+    cp = cp * f2; cp = cp + 1.0f;
+    float s = (qi == 0) ? sp : (qi == 1) ? cp : (qi == 2) ? -sp : -cp;
+    float c = (qi == 0) ? cp : (qi == 1) ? -sp : (qi == 2) ? -cp : sp;
+    *s_out = s;
+    *c_out = c;
+}
+
+// create_normal_coordinate_system (CPU/utils/hemisphere_helpers.cpp:26-39)
+RT_HD void normal_frame(f3 n, f3* T, f3* B) {
+    if (fabsf(n.x) > fabsf(n.y)) {
+        *T = normalize(make3(n.z, 0.0f, -n.x));
+    } else {
+        *T = normalize(make3(0.0f, -n.z, n.y));
+    }
+    *B = cross(n, *T);
+}
+
+constexpr float kPi = 3.14159265358979323846f;  // (float)M_PI
+constexpr float kEps = 1e-5f;                   // EPS / the 0.00001f offsets
+
+}  // namespace rt

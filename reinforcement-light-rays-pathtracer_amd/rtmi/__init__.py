@@ -1,0 +1,22 @@
+"""rtmi — MI355X-native Monte Carlo path tracer (Python binding).
+
+The compute path is librtmi.so (hand-written HIP kernels for gfx950 behind
+the C ABI in include/rtmi.h); this package only binds it.  Importing rtmi
+does not touch the GPU.
+"""
+from ._lib import (LIB_PATH, RT_HIT_NONE, RT_HIT_RULE_CPU, RT_HIT_RULE_GPU, RT_HIT_TYPE_LIGHT,
+                   RT_HIT_TYPE_SURFACE, RT_PRESET_CPU, RT_PRESET_GPU, RT_SAMPLER_COSINE,
+                   RT_SAMPLER_UNIFORM, RtCamera, RtError, RtParams, lib)
+from .api import (CAMERAS, OBJ_KINDS, Context, Geometry, Scene, camera, cornell_geometry,
+                  default_params, intersect, intersect_device, obj_geometry, pack_argb, render,
+                  render_tiles_device, save_bmp)
+from . import metrics, tiles
+
+__all__ = [
+    "LIB_PATH", "RT_HIT_NONE", "RT_HIT_RULE_CPU", "RT_HIT_RULE_GPU", "RT_HIT_TYPE_LIGHT",
+    "RT_HIT_TYPE_SURFACE", "RT_PRESET_CPU", "RT_PRESET_GPU", "RT_SAMPLER_COSINE",
+    "RT_SAMPLER_UNIFORM", "RtCamera", "RtError", "RtParams", "lib", "CAMERAS", "OBJ_KINDS",
+    "Context", "Geometry", "Scene", "camera", "cornell_geometry", "default_params", "intersect",
+    "intersect_device", "obj_geometry", "pack_argb", "render", "render_tiles_device", "save_bmp",
+    "metrics", "tiles",
+]

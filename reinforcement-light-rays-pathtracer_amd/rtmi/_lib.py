@@ -1,0 +1,117 @@
+"""ctypes binding of librtmi.so (include/rtmi.h).
+
+The product path is the HIP library; there is no Python or CPU fallback.  If
+the library is missing, `lib()` raises so a caller can never silently run
+something else.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG_DIR, "build", "librtmi.so")
+
+RT_OK = 0
+RT_E_INVALID = -1
+RT_E_HIP = -2
+RT_E_NOMEM = -3
+RT_E_IO = -4
+RT_E_UNSUPPORTED = -5
+
+RT_PRESET_CPU = 0
+RT_PRESET_GPU = 1
+RT_HIT_RULE_CPU = 0
+RT_HIT_RULE_GPU = 1
+RT_SAMPLER_UNIFORM = 0
+RT_SAMPLER_COSINE = 1
+RT_HIT_NONE = -1
+RT_HIT_TYPE_LIGHT = 1
+RT_HIT_TYPE_SURFACE = 2
+
+# every symbol include/rtmi.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "rt_params_default", "rt_ctx_create", "rt_ctx_destroy", "rt_last_error",
+    "rt_cornell_counts", "rt_cornell_geometry", "rt_obj_geometry",
+    "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
+    "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
+    "rt_pack_argb", "rt_save_bmp",
+)
+
+
+class RtCamera(ctypes.Structure):
+    _fields_ = [("pos", ctypes.c_float * 4), ("yaw_y", ctypes.c_float), ("yaw_x", ctypes.c_float)]
+
+
+class RtParams(ctypes.Structure):
+    _fields_ = [
+        ("width", ctypes.c_int32), ("height", ctypes.c_int32), ("spp", ctypes.c_int32),
+        ("max_bounces", ctypes.c_int32), ("sampler", ctypes.c_int32), ("preset", ctypes.c_int32),
+        ("hit_rule", ctypes.c_int32), ("spp_split", ctypes.c_int32), ("seed", ctypes.c_uint64),
+        ("env_light", ctypes.c_float), ("t_scale", ctypes.c_float),
+    ]
+
+    def to_dict(self) -> dict:
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rtmi error {code}: {msg}")
+        self.code = code
+
+
+_LIB = None
+_P = ctypes.c_void_p
+_FP = ctypes.POINTER(ctypes.c_float)
+_IP = ctypes.POINTER(ctypes.c_int32)
+_UP = ctypes.POINTER(ctypes.c_uint32)
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+
+
+def _declare(lib):
+    i, f = ctypes.c_int, ctypes.c_float
+    sig = {
+        "rt_params_default": (i, [i, ctypes.POINTER(RtParams)]),
+        "rt_ctx_create": (i, [i, ctypes.POINTER(_P)]),
+        "rt_ctx_destroy": (i, [_P]),
+        "rt_last_error": (ctypes.c_char_p, []),
+        "rt_cornell_counts": (i, [ctypes.POINTER(i), ctypes.POINTER(i)]),
+        "rt_cornell_geometry": (i, [i, _FP, _FP, _FP, _FP, _IP]),
+        "rt_obj_geometry": (i, [ctypes.c_char_p, i, _FP, _FP, ctypes.POINTER(i), _FP, _FP, _IP,
+                                ctypes.POINTER(i), _FP, ctypes.POINTER(i)]),
+        "rt_scene_create": (i, [_P, _FP, _FP, i, _FP, _FP, _IP, i, ctypes.POINTER(_P)]),
+        "rt_scene_destroy": (i, [_P]),
+        "rt_scene_normals": (i, [_P, _FP]),
+        "rt_intersect": (i, [_P, _P, _FP, _FP, i, f, i, _FP, _IP]),
+        "rt_intersect_device": (i, [_P, _P, _P, _P, i, f, i, _P, _P, _P]),
+        "rt_render": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
+                          _FP, _U64P]),
+        "rt_render_tiles_device": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams),
+                                       _IP, i, i, _P, _P, _P]),
+        "rt_pack_argb": (i, [_FP, i, _UP]),
+        "rt_save_bmp": (i, [ctypes.c_char_p, _UP, i, i]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+
+
+def lib():
+    """The loaded librtmi.so; raises if it has not been built."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `make -C {_PKG_DIR}` "
+                "(or __graft_entry__.build()); there is no fallback path")
+        handle = ctypes.CDLL(LIB_PATH)
+        _declare(handle)
+        _LIB = handle
+    return _LIB
+
+
+def check(rc: int) -> None:
+    if rc != RT_OK:
+        raise RtError(rc, lib().rt_last_error().decode(errors="replace"))

@@ -1,0 +1,80 @@
+"""Regenerate the committed fixtures under tests/golden/ from the reference.
+
+Run in the build container only (the reference is not on the GPU box):
+    python tests/golden/make_goldens.py [/root/reference]
+
+Fixtures (all data, no reference source):
+  archway_vertices.txt   copy of Radiance_Map_Data/vertices.txt: the GPU
+                         engine's archway scene after loading (96 surfaces in
+                         Surface(v1,v3,v2) order, then 6 lights), written by
+                         Scene::save_vertices_to_file (GPU/scenes/scene.cu:63-88)
+  triangle_o_pin.json    constants of Triangle::intersects read from the
+                         prebuilt CPU object triangle.cpp.o (.rodata words the
+                         function's relocations point at) and the order of its
+                         accept tests, as disassembled
+  cornell_ref_stats.json block means of Images/cornell/*.png (statistical
+                         reference renders of the GPU engine, 720x720)
+"""
+import json
+import os
+import re
+import shutil
+import struct
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def rodata_words(obj):
+    out = subprocess.run(["objdump", "-s", "-j", ".rodata", obj], capture_output=True, text=True,
+                         check=True).stdout
+    data = bytearray()
+    for line in out.splitlines():
+        m = re.match(r"^\s*([0-9a-f]{4,})\s+((?:[0-9a-f]{1,8}\s?){1,4})", line)
+        if m:
+            data += bytes.fromhex("".join(m.group(2).split()))
+    return bytes(data)
+
+
+def main(ref):
+    shutil.copy(os.path.join(ref, "Radiance_Map_Data", "vertices.txt"),
+                os.path.join(HERE, "archway_vertices.txt"))
+
+    obj = os.path.join(ref, "Old_CPU_Rendering_Engine", "CMakeFiles", "Monte_Carlo_Raytracer.dir",
+                       "Source", "objects", "triangle.cpp.o")
+    ro = rodata_words(obj)
+    # relocations of Triangle::intersects: .rodata+0x20 (D scale), +0x14 (1.0), +0x24 (eps);
+    # R_X86_64_PC32 addend -4 convention -> the word at addend+4
+    word = lambda off: struct.unpack_from("<I", ro, off)[0]
+    pin = {
+        "t_scale_word": hex(word(0x24)),        # 512.0f = SCREEN_HEIGHT
+        "one_word": hex(word(0x18)),            # 1.0f (u + v <= 1)
+        "eps_word": hex(word(0x28)),            # 1e-5f
+        "accept_order": ["detA != 0", "t >= 0", "u >= 0", "v >= 0", "u + v <= 1",
+                         "t < dist + eps", "t > eps"],
+        "solve": "inv = 1/detA; t = det_t*inv; u = det_u*inv; v = det_v*inv",
+        "determinant": "((m00*(m11*m22 - m21*m12)) - m10*(m01*m22 - m21*m02)) + m20*(m01*m12 - m11*m02)",
+    }
+    with open(os.path.join(HERE, "triangle_o_pin.json"), "w") as f:
+        json.dump(pin, f, indent=1)
+
+    try:
+        import numpy as np
+        from PIL import Image
+        stats = {}
+        for name in ("2048_2_default.png", "2048_300_default.png", "reference.png"):
+            p = os.path.join(ref, "Images", "cornell", name)
+            a = np.asarray(Image.open(p).convert("RGB"), np.float64)
+            h, w, _ = a.shape
+            b = 45  # 16x16 grid of 45x45 blocks
+            blocks = a[: h // b * b, : w // b * b].reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3))
+            stats[name] = {"shape": [h, w], "block": b, "means": blocks.round(4).tolist()}
+        with open(os.path.join(HERE, "cornell_ref_stats.json"), "w") as f:
+            json.dump(stats, f)
+    except ImportError:
+        pass
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "/root/reference")

@@ -1,0 +1,176 @@
+"""Parity of the HIP path (through the C ABI) with the CPU restatement.
+
+Integer/index results (hit codes, ray-cast counts) must be bit-exact; the
+float image is required bit-exact too (same Philox stream, same operation
+order, no contraction), with the MAPE <= 1e-3 gate of BASELINE.md asserted
+alongside so a failure reports its size.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS
+
+pytestmark = pytest.mark.gpu
+
+CORNELL_CAM = (0.0, 0.0, -3.0, 1.0)
+
+
+def primary_rays(width, height, cam, seed=3):
+    """One jittered camera ray per pixel (the reference's camera model, yaw 0)."""
+    rng = np.random.default_rng(seed)
+    ys, xs = np.meshgrid(np.arange(height), np.arange(width), indexing="ij")
+    x = xs.astype(np.float32) + rng.random(xs.shape, dtype=np.float32)
+    y = ys.astype(np.float32) + rng.random(ys.shape, dtype=np.float32)
+    d = np.stack([x - np.float32(width / 2), y - np.float32(height / 2),
+                  np.full_like(x, np.float32(height))], axis=-1).reshape(-1, 3)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    o = np.tile(np.asarray(cam[:3], np.float32), (d.shape[0], 1))
+    return o, d
+
+
+def random_rays(n, seed, lo=-1.2, hi=1.2):
+    rng = np.random.default_rng(seed)
+    o = rng.uniform(lo, hi, size=(n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    return o, d
+
+
+def scene_for(rtmi, kind):
+    if kind in ("cornell_cpu", "cornell_gpu"):
+        return rtmi.cornell_geometry(0 if kind == "cornell_cpu" else 1)
+    return rtmi.obj_geometry(os.path.join(MODELS, f"{kind}.obj"), kind)
+
+
+def check_intersect(rtmi, oracle, ctx, geom, o, d, t_scale, rule):
+    with rtmi.Scene(ctx, geom) as sc:
+        t_gpu, h_gpu = rtmi.intersect(ctx, sc, o, d, t_scale, rule)
+    t_cpu, h_cpu = oracle.intersect(geom.all_triangles(), geom.n_surf, geom.n_light,
+                                    geom.light_group, o, d, t_scale, rule)
+    mism = np.nonzero(h_gpu != h_cpu)[0]
+    assert mism.size == 0, f"{mism.size} hit mismatches, first {mism[:5]}"
+    assert np.array_equal(t_gpu.view(np.uint32), t_cpu.view(np.uint32)), "t not bit-exact"
+    return h_gpu
+
+
+@pytest.mark.parametrize("rule", [0, 1])
+def test_intersect_cornell_primary_512(rtmi_mod, oracle_mod, gpu_ctx, rule):
+    geom = rtmi_mod.cornell_geometry(0)
+    o, d = primary_rays(512, 512, CORNELL_CAM)
+    h = check_intersect(rtmi_mod, oracle_mod, gpu_ctx, geom, o, d, 512.0, rule)
+    assert np.count_nonzero(h == -1) < h.size  # the box fills the view
+
+
+@pytest.mark.parametrize("kind", ["cornell_cpu", "cornell_gpu", "door_room", "archway",
+                                  "complex_light_room"])
+@pytest.mark.parametrize("rule", [0, 1])
+def test_intersect_random_rays(rtmi_mod, oracle_mod, gpu_ctx, kind, rule):
+    geom = scene_for(rtmi_mod, kind)
+    n = 1_000_000 if kind == "cornell_cpu" else 200_000
+    o, d = random_rays(n, seed=11 + rule)
+    check_intersect(rtmi_mod, oracle_mod, gpu_ctx, geom, o, d, 512.0, rule)
+
+
+def test_intersect_edge_cases(rtmi_mod, oracle_mod, gpu_ctx):
+    geom = rtmi_mod.cornell_geometry(0)
+    tri = geom.all_triangles().reshape(-1, 3, 3)
+    # origins exactly on vertices / edge midpoints / centroids, random directions
+    pts = np.concatenate([tri.reshape(-1, 3), tri.mean(axis=1), (tri[:, 0] + tri[:, 1]) / 2])
+    rng = np.random.default_rng(5)
+    o = np.repeat(pts, 8, axis=0).astype(np.float32)
+    d = rng.normal(size=o.shape)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    # axis-aligned and degenerate-ish directions
+    d[::5] = np.array([0, 0, 1], np.float32)
+    d[1::5] = np.array([0, -1, 0], np.float32)
+    for rule in (0, 1):
+        check_intersect(rtmi_mod, oracle_mod, gpu_ctx, geom, o, d, 512.0, rule)
+
+
+def test_intersect_empty_batch(rtmi_mod, gpu_ctx):
+    geom = rtmi_mod.cornell_geometry(0)
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        t, h = rtmi_mod.intersect(gpu_ctx, sc, np.zeros((0, 3)), np.zeros((0, 3)), 512.0, 0)
+    assert t.size == 0 and h.size == 0
+
+
+def test_scene_normals_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx):
+    for kind in ("cornell_cpu", "archway", "complex_light_room"):
+        geom = scene_for(rtmi_mod, kind)
+        with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+            n = sc.normals()
+        assert np.array_equal(n, oracle_mod.normals(geom.all_triangles()))
+
+
+RENDER_CASES = [
+    # (scene, preset, overrides, rect)
+    ("cornell_cpu", 0, dict(width=64, height=64, spp=16), None),
+    ("cornell_cpu", 0, dict(width=512, height=512, spp=8, spp_split=4), (200, 96, 48, 40)),
+    ("cornell_cpu", 0, dict(width=64, height=64, spp=16, sampler=1), None),
+    ("cornell_cpu", 0, dict(width=64, height=64, spp=8, max_bounces=1), None),
+    ("cornell_cpu", 0, dict(width=64, height=64, spp=8, hit_rule=1), None),
+    ("cornell_gpu", 1, dict(width=48, height=48, spp=8), None),
+    ("cornell_gpu", 1, dict(width=48, height=48, spp=8, sampler=1, spp_split=2), None),
+    ("door_room", 1, dict(width=40, height=40, spp=4), None),
+    ("archway", 1, dict(width=40, height=40, spp=4, hit_rule=0), None),
+    ("complex_light_room", 1, dict(width=40, height=40, spp=4), None),
+]
+
+
+@pytest.mark.parametrize("kind,preset,over,rect", RENDER_CASES)
+def test_render_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx, kind, preset, over, rect):
+    geom = scene_for(rtmi_mod, kind)
+    cam_key = "cornell" if kind.startswith("cornell") else kind
+    yaw = 0.1 if kind == "door_room" else 0.0
+    p = rtmi_mod.default_params(preset, **over)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS[cam_key], yaw_y=yaw, yaw_x=-0.05 * (preset == 1))
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        img, casts = rtmi_mod.render(gpu_ctx, sc, cam, p, rect)
+    ocam = oracle_mod.camera(rtmi_mod.CAMERAS[cam_key], yaw_y=yaw, yaw_x=-0.05 * (preset == 1))
+    ref, ref_casts = oracle_mod.render(geom, ocam, oracle_mod.params_from(p), rect)
+    assert casts == ref_casts
+    assert rtmi_mod.metrics.mape_f(ref, img) <= 1e-3
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), "image not bit-exact"
+    assert img.max() > 0  # the light is reached
+
+
+def test_tile_render_equals_rect_render(rtmi_mod, gpu_ctx):
+    torch = pytest.importorskip("torch")
+    geom = rtmi_mod.cornell_geometry(0)
+    p = rtmi_mod.default_params(0, width=96, height=64, spp=8, spp_split=2)
+    cam = rtmi_mod.camera(CORNELL_CAM)
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        full, casts_full = rtmi_mod.render(gpu_ctx, sc, cam, p)
+        tiles = rtmi_mod.tiles.tile_origins(96, 64, 32)
+        out = torch.zeros((len(tiles), 32, 32, 3), dtype=torch.float32, device="cuda")
+        casts = torch.zeros(1, dtype=torch.int64, device="cuda")
+        stream = torch.cuda.current_stream().cuda_stream
+        rtmi_mod.render_tiles_device(gpu_ctx, sc, cam, p, tiles, 32, out.data_ptr(),
+                                     casts.data_ptr(), stream)
+        torch.cuda.synchronize()
+    gathered = out.cpu().numpy()[None]
+    img = rtmi_mod.tiles.assemble(gathered, 96, 64, 32, 1)
+    assert np.array_equal(img, full)
+    assert int(casts.item()) == casts_full
+
+
+def test_full_size_properties(rtmi_mod, oracle_mod, gpu_ctx):
+    """BASELINE config 2 at full size (Cornell 512^2, 256 spp): deterministic,
+    tiling-invariant, and bit-exact on an oracle-checked window."""
+    geom = rtmi_mod.cornell_geometry(0)
+    p = rtmi_mod.default_params(0, width=512, height=512, spp=256, spp_split=8)
+    cam = rtmi_mod.camera(CORNELL_CAM)
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        a, ca = rtmi_mod.render(gpu_ctx, sc, cam, p)
+        b, cb = rtmi_mod.render(gpu_ctx, sc, cam, p)
+        win, cw = rtmi_mod.render(gpu_ctx, sc, cam, p, (240, 120, 16, 16))
+    assert np.array_equal(a, b) and ca == cb
+    assert np.array_equal(a[120:136, 240:256], win)
+    # at most 3 casts per sample (cap 2), at least 1
+    assert 512 * 512 * 256 <= ca <= 3 * 512 * 512 * 256
+    ref, rc = oracle_mod.render(geom, oracle_mod.camera(CORNELL_CAM), oracle_mod.params_from(p),
+                                (240, 120, 16, 16))
+    assert rc == cw
+    assert np.array_equal(win, ref)
