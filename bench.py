@@ -122,7 +122,7 @@ def main():
     def step():
         render()
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            rtmi.dist.gather_tiles(out, gathered)
 
     for _ in range(args.warmup):
         step()
@@ -139,7 +139,7 @@ def main():
         render()
         ev[i][1].record(stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
+            rtmi.dist.gather_tiles(out, gathered)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
