@@ -150,6 +150,50 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
                            const rt_params* params, const int32_t* tiles, int n_tiles,
                            int tile_size, float* d_out, uint64_t* d_casts, void* stream);
 
+/* ---- DQN Q-value sampling (BASELINE config 4) ---------------------------- */
+typedef struct rt_dqn rt_dqn;
+
+/* DyNet TextFileSaver format reader (the reference loads RMD/<scene>.model with
+ * dynet::TextFileLoader, GPU/deep_learning/pre_trained_pathtracer.cu:45-53).  Parameters in
+ * file order; each returned row-major [rows][cols] (DyNet stores column-major).  Call with
+ * values = NULL to size: *n_params, *n_values. */
+int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols, float* values,
+                  int* n_params, int64_t* n_values);
+
+/* DQNetwork::initialize + the parameters it loads (NN_Builders/dq_network.cu:8-33,
+ * fc_layer.cu:29-35): ReLU(W x + b) x 4, n_in -> hidden[0] -> hidden[1] -> hidden[2] -> n_out.
+ * W[l]: row-major [out][in] fp32, b[l]: [out].  nn_vertices: Scene::vertices (n_in floats);
+ * the network input is nn_vertices - ray position (nn_rendering_helpers.cu:280-298).
+ * Stored on the device as bf16 for the MFMA forward.  n_out must be 144. */
+int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t* hidden /* 3 */,
+                  int n_out, const float* const* W /* 4 */, const float* const* b /* 4 */,
+                  rt_dqn** out);
+int rt_dqn_destroy(rt_dqn* dqn);
+/* DQNetwork::network_inference on n ray positions (host arrays): q = n x 144. */
+int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc /* n x 3 */, int n, float* q);
+/* importance_sample_direction (nn_rendering_helpers.cu:391-489) for n rays given their Q
+ * values (host arrays; q is overwritten with Q*cos as in the reference).  tri: surface the
+ * ray sits on; pix: global pixel id (RNG key); tp updated in place; action -1 = none. */
+int rt_dqn_sample(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float* q, const float* loc,
+                  const int32_t* tri, const uint32_t* pix, int n, int sample, int bounce, float* tp,
+                  float* dir_out, int32_t* action);
+/* PretrainedPathtracer::render_frame (pre_trained_pathtracer.cu:188-376), GPU-engine preset:
+ * rectangle render into host memory, and tile-list render into device memory (stream-ordered;
+ * synchronises the stream every few bounces to stop once all paths have ended). */
+int rt_render_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_camera* cam,
+                  const rt_params* params, int x0, int y0, int w, int h, float* out_rgb,
+                  uint64_t* out_ray_casts);
+int rt_render_dqn_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn,
+                               const rt_camera* cam, const rt_params* params, const int32_t* tiles,
+                               int n_tiles, int tile_size, float* d_out, uint64_t* d_casts,
+                               void* stream);
+
+/* Device self-tests of numeric building blocks (no reference counterpart).
+ * RT_SELFTEST_RCP: the kernels' correctly-rounded reciprocal vs IEEE 1.0f/x over
+ * all 2^32 floats; result[0] = mismatches, result[1] = first mismatching bits. */
+#define RT_SELFTEST_RCP 1
+int rt_selftest(rt_ctx* ctx, int which, uint64_t* result /* 2 */);
+
 /* SDLScreen::PutPixelSDL pack rule (CPU/sdl/sdl_screen.cpp:100-112). Host arrays. */
 int rt_pack_argb(const float* rgb, int n, uint32_t* out_argb);
 

@@ -161,3 +161,85 @@ def num_threads() -> int:
 
 def set_threads(n: int) -> None:
     lib().orc_set_threads(int(n))
+
+
+# ---- DQN path -----------------------------------------------------------------
+
+def read_dynet(path):
+    """Independent numpy reader of a DyNet text model: [(rows, cols, row-major array)]."""
+    params, shape = [], None
+    with open(path) as f:
+        for line in f:
+            if line.startswith("#Parameter#") or line.startswith("#LookupParameter#"):
+                dims = line[line.index("{") + 1:line.index("}")].split(",")
+                shape = tuple(int(x) for x in dims)
+            elif shape is not None:
+                v = np.array(line.split(), np.float32)
+                r = shape[0]
+                c = shape[1] if len(shape) > 1 else 1
+                a = v.reshape(c, r).T  # column-major storage
+                params.append(a if c > 1 else a[:, 0])
+                shape = None
+    return params
+
+
+def _ptrs(arrs):
+    return (_FP * len(arrs))(*[a.ctypes.data_as(_FP) for a in arrs])
+
+
+def dqn_forward(W, b, verts, loc, bf16=False):
+    L = lib()
+    L.orc_dqn_forward.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(_FP), ctypes.POINTER(_FP), _FP, _FP,
+                                                        ctypes.c_int, ctypes.c_int, _FP]
+    W = [np.ascontiguousarray(w, np.float32) for w in W]
+    b = [np.ascontiguousarray(x, np.float32) for x in b]
+    v = np.ascontiguousarray(verts, np.float32)
+    x = np.ascontiguousarray(loc, np.float32).reshape(-1, 3)
+    q = np.zeros((x.shape[0], W[3].shape[0]), np.float32)
+    L.orc_dqn_forward(W[0].shape[1], W[0].shape[0], W[1].shape[0], W[2].shape[0], W[3].shape[0], _ptrs(W),
+                      _ptrs(b), _f(v), _f(x), x.shape[0], int(bf16), _f(q))
+    return q
+
+
+def dqn_sample(tri_all, q, loc, tri, pix, sample, bounce, seed, tp):
+    L = lib()
+    U32 = ctypes.POINTER(ctypes.c_uint32)
+    L.orc_dqn_sample.argtypes = [_FP, ctypes.c_int, _FP, _FP, _IP, U32, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_uint64, _FP, _FP, _IP]
+    t_all = np.ascontiguousarray(tri_all, np.float32)
+    q = np.ascontiguousarray(q, np.float32).copy()
+    loc = np.ascontiguousarray(loc, np.float32)
+    tri = np.ascontiguousarray(tri, np.int32)
+    pix = np.ascontiguousarray(pix, np.uint32)
+    tp = np.ascontiguousarray(tp, np.float32).copy()
+    n = q.shape[0]
+    d = np.zeros((n, 3), np.float32)
+    a = np.zeros(n, np.int32)
+    L.orc_dqn_sample(_f(t_all), t_all.shape[0], _f(q), _f(loc), _i(tri), pix.ctypes.data_as(U32), n, sample,
+                     bounce, seed, _f(tp), _f(d), _i(a))
+    return q, tp, d, a
+
+
+def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False):
+    L = lib()
+    L.orc_render_dqn.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.c_int, ctypes.c_int, ctypes.POINTER(_FP), ctypes.POINTER(_FP), _FP,
+                                 ctypes.c_int, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams),
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _FP,
+                                 ctypes.POINTER(ctypes.c_uint64)]
+    get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
+    tri = np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32)
+    alb = np.ascontiguousarray(get("albedo"), np.float32)
+    em = np.ascontiguousarray(get("emission"), np.float32)
+    grp = np.ascontiguousarray(get("light_group"), np.int32)
+    W = [np.ascontiguousarray(w, np.float32) for w in W]
+    b = [np.ascontiguousarray(x, np.float32) for x in b]
+    v = np.ascontiguousarray(verts, np.float32)
+    x0, y0, w, h = rect if rect is not None else (0, 0, params.width, params.height)
+    out = np.zeros((h, w, 3), np.float32)
+    casts = ctypes.c_uint64(0)
+    L.orc_render_dqn(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp), get("light").shape[0],
+                     W[0].shape[1], W[0].shape[0], W[1].shape[0], W[2].shape[0], _ptrs(W), _ptrs(b), _f(v),
+                     int(bf16), ctypes.byref(cam), ctypes.byref(params), x0, y0, w, h, _f(out),
+                     ctypes.byref(casts))
+    return out, int(casts.value)

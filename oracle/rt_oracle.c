@@ -587,3 +587,266 @@ ORC_API void orc_set_threads(int n) {
     (void)n;
 #endif
 }
+
+/* ================================================================== */
+/* DQN path (BASELINE config 4)                                        */
+/* ================================================================== */
+/*
+ * Restates:
+ *   DQNetwork::network_inference  NN_Builders/dq_network.cu:36-49 and
+ *   FCLayer::run_inference        NN_Builders/fc_layer.cu:40-72: h = ReLU(W h + b) x 4
+ *   NN input                      GPU/deep_learning/nn_rendering_helpers.cu:280-298: v - x
+ *   importance_sample_direction   nn_rendering_helpers.cu:391-489
+ *   sample_ray_for_grid_index     nn_rendering_helpers.cu:38-57
+ *   convert_grid_pos_to_direction_random + map (Chiu)  GPU/utils/hemisphere_helpers.cu:95-226,
+ *     restated in turns: cos(theta) = 1 - xx^2, sin(theta) = xx*sqrt(2 - xx^2),
+ *     phi = offset + (yy/xx)/8 turns (identical mathematically)
+ *   render_frame / initialise_ray / trace_ray  GPU/deep_learning/pre_trained_pathtracer.cu:188-491
+ * RNG: event 1+b of bounce b >= 1: Philox counter word 3 = 0 gives rv,
+ * = 1 + a/2 the jitter of cells a (pairs), = 73 the final jitter.
+ * The forward pass accumulates in double (bf16 = 0) or emulates the kernel's bf16
+ * operand / activation rounding with double accumulation (bf16 = 1).
+ */
+typedef struct {
+    int n_in, h1, h2, h3, n_out;
+    const float *W[4], *b[4]; /* row-major [out][in] */
+    const float *verts;       /* n_in: Scene::vertices */
+} orc_dqn;
+
+static float bf16_round(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) { u |= 0x400000u; u &= 0xffff0000u; }
+    else { u += 0x7fffu + ((u >> 16) & 1u); u &= 0xffff0000u; }
+    float r;
+    memcpy(&r, &u, 4);
+    return r;
+}
+
+static void dqn_forward_one(const orc_dqn *net, const float *loc, int bf16, float *q_out, float *scratch) {
+    int dims[5] = {net->n_in, net->h1, net->h2, net->h3, net->n_out};
+    float *in = scratch, *out = scratch + 1024;
+    for (int k = 0; k < net->n_in; k++) {
+        float x = net->verts[k] - loc[k % 3];
+        in[k] = bf16 ? bf16_round(x) : x;
+    }
+    for (int l = 0; l < 4; l++) {
+        const float *W = net->W[l], *b = net->b[l];
+        for (int o = 0; o < dims[l + 1]; o++) {
+            double acc = 0.0;
+            const float *w = W + (size_t)o * dims[l];
+            for (int i = 0; i < dims[l]; i++) {
+                float wv = bf16 ? bf16_round(w[i]) : w[i];
+                acc += (double)wv * (double)in[i];
+            }
+            float v = (float)acc + b[o];
+            v = v > 0.0f ? v : 0.0f;
+            out[o] = (bf16 && l < 3) ? bf16_round(v) : v;
+        }
+        float *t = in; in = out; out = t;
+    }
+    memcpy(q_out, in, sizeof(float) * (size_t)net->n_out);
+}
+
+ORC_API void orc_dqn_forward(int n_in, int h1, int h2, int h3, int n_out, const float *const *W,
+                             const float *const *b, const float *verts, const float *loc, int n, int bf16,
+                             float *q) {
+    orc_dqn net = {n_in, h1, h2, h3, n_out, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts};
+    #pragma omp parallel
+    {
+        float *scratch = (float *)malloc(sizeof(float) * 2048);
+        #pragma omp for schedule(static)
+        for (int r = 0; r < n; r++) dqn_forward_one(&net, loc + (size_t)r * 3, bf16, q + (size_t)r * n_out, scratch);
+        free(scratch);
+    }
+}
+
+static void chiu_map_t(float x, float y, float *xr, float *yr, float *zr) {
+    x = 2.0f * x - 1.0f;
+    y = 2.0f * y - 1.0f;
+    float xx, yy, off;
+    if (y > -x) {
+        if (y < x) {
+            xx = x;
+            if (y > 0.0f) { off = 0.0f; yy = y; } else { off = 0.875f; yy = x + y; }
+        } else {
+            xx = y;
+            if (x > 0.0f) { off = 0.125f; yy = y - x; } else { off = 0.25f; yy = -x; }
+        }
+    } else {
+        if (y > x) {
+            xx = -x;
+            if (y > 0.0f) { off = 0.375f; yy = -x - y; } else { off = 0.5f; yy = -y; }
+        } else {
+            xx = -y;
+            if (x > 0.0f) { off = 0.75f; yy = x; }
+            else if (y != 0.0f) { off = 0.625f; yy = x - y; }
+            else { *xr = 0.0f; *yr = 1.0f; *zr = 0.0f; return; }
+        }
+    }
+    float c = 1.0f - xx * xx;
+    float s = xx * sqrtf(2.0f - xx * xx);
+    float phi = off + 0.125f * (yy / xx);
+    float sp, cp;
+    orc_sincos_turn(phi, &sp, &cp);
+    *xr = s * cp;
+    *yr = c;
+    *zr = s * sp;
+}
+
+/* create_transformation_matrix(normal, position) = mat4(T, N, B, pos); world = M*(x,y,z,1);
+ * direction = normalize(world - pos) */
+static v3 grid_dir(float gx, float gy, v3 N, v3 T, v3 B, v3 pos) {
+    float xh, yh, zh;
+    chiu_map_t(gx / 12.0f, gy / 12.0f, &xh, &yh, &zh);
+    v3 w = mk((T.x * xh + N.x * yh) + (B.x * zh + pos.x * 1.0f),
+              (T.y * xh + N.y * yh) + (B.y * zh + pos.y * 1.0f),
+              (T.z * xh + N.z * yh) + (B.z * zh + pos.z * 1.0f));
+    return normalize3(mk(w.x - pos.x, w.y - pos.y, w.z - pos.z));
+}
+
+static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint32_t smp, uint32_t ev,
+                      v3 *tp, v3 *dir_out) {
+    v3 T, B;
+    normal_frame(N, &T, &B);
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {pix, smp, ev, 0u}, o[4];
+    orc_philox4x32_10(ctr, key, o);
+    float rv = u01(o[0]);
+    float total = 0.0f;
+    for (int a2 = 0; a2 < 72; a2++) {
+        ctr[3] = 1u + (uint32_t)a2;
+        orc_philox4x32_10(ctr, key, o);
+        for (int h = 0; h < 2; h++) {
+            int a = 2 * a2 + h;
+            int gxi = a / 12, gyi = a - gxi * 12;
+            v3 d = grid_dir((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]), N, T, B, pos);
+            float c = dot3(N, d);
+            float qc = q[a] * c;
+            q[a] = qc;
+            total = total + qc;
+        }
+    }
+    int act = -1;
+    float q_sum = 0.0f, qd_sel = 0.0f;
+    for (int a = 0; a < 144; a++) {
+        float qd = q[a] / total;
+        q_sum = q_sum + qd;
+        if (q_sum > rv) { act = a; qd_sel = qd; break; }
+    }
+    *dir_out = mk(0.0f, 0.0f, 0.0f);
+    if (act >= 0) {
+        ctr[3] = 73u;
+        orc_philox4x32_10(ctr, key, o);
+        int gxi = act / 12, gyi = act - gxi * 12;
+        v3 d = grid_dir((float)gxi + u01(o[0]), (float)gyi + u01(o[1]), N, T, B, pos);
+        float c = dot3(N, d);
+        const float RHO = 1.0f / (2.0f * 3.1415926535f);
+        const float GRID_RHO = 1.0f / (12.0f * 12.0f);
+        float pdf = RHO * (qd_sel / GRID_RHO);
+        tp->x = (tp->x * c) / pdf;
+        tp->y = (tp->y * c) / pdf;
+        tp->z = (tp->z * c) / pdf;
+        *dir_out = d;
+    }
+    return act;
+}
+
+ORC_API void orc_dqn_sample(const float *tri_all, int n_tri, float *q, const float *loc, const int32_t *tri,
+                            const uint32_t *pix, int n, int sample, int bounce, uint64_t seed, float *tp,
+                            float *dir_out, int32_t *action) {
+    float *nrm = (float *)malloc(sizeof(float) * 3 * (size_t)n_tri);
+    orc_triangle_normals(tri_all, n_tri, nrm);
+    #pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+        const float *nn = nrm + (size_t)tri[i] * 3;
+        v3 t = mk(tp[i * 3], tp[i * 3 + 1], tp[i * 3 + 2]), d;
+        action[i] = dqn_sample(q + (size_t)i * 144, mk(nn[0], nn[1], nn[2]),
+                               mk(loc[i * 3], loc[i * 3 + 1], loc[i * 3 + 2]), seed, pix[i], (uint32_t)sample,
+                               1u + (uint32_t)bounce, &t, &d);
+        tp[i * 3] = t.x; tp[i * 3 + 1] = t.y; tp[i * 3 + 2] = t.z;
+        dir_out[i * 3] = d.x; dir_out[i * 3 + 1] = d.y; dir_out[i * 3 + 2] = d.z;
+    }
+    free(nrm);
+}
+
+/* trace_ray: Ray(pos + dir*1e-5, dir) with the GPU hit rule; returns 1 if on a surface */
+static int dqn_trace(const orc_scene *sc, const orc_params *p, v3 pos, v3 dir, v3 *loc, int *tri, v3 *tp,
+                     uint64_t *casts) {
+    v3 o = mk(pos.x + dir.x * 1e-5f, pos.y + dir.y * 1e-5f, pos.z + dir.z * 1e-5f);
+    v3 d = normalize3(dir);
+    hit_t h = closest_hit(sc, o, d, p->t_scale, 1);
+    (*casts)++;
+    if (h.tri < 0) { *tp = mk(tp->x * p->env_light, tp->y * p->env_light, tp->z * p->env_light); return 0; }
+    if (h.tri >= sc->n_surf) {
+        const float *e = sc->emission + (size_t)(h.tri - sc->n_surf) * 3;
+        *tp = mk(tp->x * e[0], tp->y * e[1], tp->z * e[2]);
+        return 0;
+    }
+    v3 D = mk(d.x * p->t_scale, d.y * p->t_scale, d.z * p->t_scale);
+    *loc = mk(o.x + h.t * D.x, o.y + h.t * D.y, o.z + h.t * D.z);
+    *tri = h.tri;
+    const float *al = sc->albedo + (size_t)h.tri * 3;
+    *tp = mk(tp->x * (al[0] / PI_F), tp->y * (al[1] / PI_F), tp->z * (al[2] / PI_F));
+    return 1;
+}
+
+ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, const float *emission,
+                           const int32_t *light_group, int n_light, int n_in, int h1, int h2, int h3,
+                           const float *const *W, const float *const *b, const float *verts, int bf16,
+                           const orc_camera *cam, const orc_params *p, int x0, int y0, int w, int h,
+                           float *out_rgb, uint64_t *out_casts) {
+    orc_scene sc;
+    scene_init(&sc, tri, albedo, n_surf, emission, light_group, n_light);
+    orc_dqn net = {n_in, h1, h2, h3, 144, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts};
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    uint64_t total_casts = 0;
+    #pragma omp parallel reduction(+:total_casts)
+    {
+        float *scratch = (float *)malloc(sizeof(float) * 2048);
+        float q[144];
+        #pragma omp for schedule(dynamic, 1)
+        for (int yy = 0; yy < h; yy++) {
+            for (int xx = 0; xx < w; xx++) {
+                int px = x0 + xx, py = y0 + yy;
+                uint32_t pix = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+                v3 acc = mk(0.0f, 0.0f, 0.0f);
+                for (int s = 0; s < p->spp; s++) {
+                    float r1, r2;
+                    draw2(p->seed, pix, (uint32_t)s, 0u, &r1, &r2);
+                    v3 o, d;
+                    orc_params pg = *p;
+                    pg.preset = 1;
+                    camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                    v3 tp = mk(1.0f, 1.0f, 1.0f), loc = o;
+                    int tri_i = 0;
+                    int alive = dqn_trace(&sc, p, o, d, &loc, &tri_i, &tp, &total_casts);
+                    for (int bnc = 1; alive && bnc < p->max_bounces; bnc++) {
+                        float locf[3] = {loc.x, loc.y, loc.z};
+                        dqn_forward_one(&net, locf, bf16, q, scratch);
+                        const float *nn = sc.normal + (size_t)tri_i * 3;
+                        v3 dir;
+                        int act = dqn_sample(q, mk(nn[0], nn[1], nn[2]), loc, p->seed, pix, (uint32_t)s,
+                                             1u + (uint32_t)bnc, &tp, &dir);
+                        if (act < 0) {
+                            total_casts++;
+                            tp = mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
+                            alive = 0;
+                        } else {
+                            alive = dqn_trace(&sc, p, loc, dir, &loc, &tri_i, &tp, &total_casts);
+                        }
+                    }
+                    acc.x = acc.x + tp.x; acc.y = acc.y + tp.y; acc.z = acc.z + tp.z;
+                }
+                float fs = (float)p->spp;
+                float *dst = out_rgb + ((size_t)yy * w + xx) * 3;
+                dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+            }
+        }
+        free(scratch);
+    }
+    free(sc.normal);
+    if (out_casts) *out_casts = total_casts;
+    return 0;
+}

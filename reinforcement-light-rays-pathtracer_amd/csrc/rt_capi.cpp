@@ -60,6 +60,45 @@ struct rt_scene {
     std::vector<float> normals;  // host copy, n_tri x 3
 };
 
+namespace rt {
+void release_dqn_workspace(const rt_ctx* ctx);
+int ctx_device(const rt_ctx* ctx) { return ctx->device; }
+const DeviceScene& scene_device(const rt_scene* s) { return s->dev; }
+int ensure_blocks_impl(rt_ctx* ctx, const std::vector<BlockDesc>& blocks);
+// Device block list (16x16 pixel blocks) of a tile list, cached per context.
+int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
+               const BlockDesc** d_blocks, int* n_blocks) {
+    if (tile_size <= 0 || tile_size % 16 != 0)
+        return set_error(RT_E_INVALID, "tile_size must be a positive multiple of 16");
+    for (int k = 0; k < n_tiles; ++k) {
+        const int tx = tiles[2 * k], ty = tiles[2 * k + 1];
+        if (tx < 0 || ty < 0 || tx >= width || ty >= height)
+            return set_error(RT_E_INVALID, "tile origin outside the image");
+    }
+    const bool same = ctx->tiles_size == tile_size && ctx->tiles_w == width && ctx->tiles_h == height &&
+                      (int)ctx->tiles_key.size() == 2 * n_tiles &&
+                      memcmp(ctx->tiles_key.data(), tiles, sizeof(int32_t) * 2 * n_tiles) == 0;
+    if (!same) {
+        std::vector<BlockDesc> blocks;
+        const int per = tile_size / 16;
+        for (int k = 0; k < n_tiles; ++k)
+            for (int sy = 0; sy < per; ++sy)
+                for (int sx = 0; sx < per; ++sx)
+                    blocks.push_back({tiles[2 * k] + 16 * sx, tiles[2 * k + 1] + 16 * sy, 16 * sx,
+                                      k * tile_size + 16 * sy});
+        int rc = ensure_blocks_impl(ctx, blocks);
+        if (rc != RT_OK) return rc;
+        ctx->tiles_key.assign(tiles, tiles + 2 * n_tiles);
+        ctx->tiles_size = tile_size;
+        ctx->tiles_w = width;
+        ctx->tiles_h = height;
+    }
+    *d_blocks = ctx->d_blocks;
+    *n_blocks = ctx->n_blocks;
+    return RT_OK;
+}
+}  // namespace rt
+
 namespace {
 
 int set_device(rt_ctx* ctx) {
@@ -67,7 +106,9 @@ int set_device(rt_ctx* ctx) {
     return RT_OK;
 }
 
-int ensure_blocks(rt_ctx* ctx, const std::vector<rt::BlockDesc>& blocks) {
+}  // namespace
+
+int rt::ensure_blocks_impl(rt_ctx* ctx, const std::vector<rt::BlockDesc>& blocks) {
     if ((int)blocks.size() > ctx->blocks_cap) {
         if (ctx->d_blocks) RT_HIP(hipFree(ctx->d_blocks));
         ctx->d_blocks = nullptr;
@@ -81,6 +122,8 @@ int ensure_blocks(rt_ctx* ctx, const std::vector<rt::BlockDesc>& blocks) {
     ctx->n_blocks = (int)blocks.size();
     return RT_OK;
 }
+
+namespace {
 
 int check_params(const rt_params* p) {
     if (!p) return fail(RT_E_INVALID, "params is NULL");
@@ -184,6 +227,7 @@ int rt_ctx_create(int device_ordinal, rt_ctx** out) {
 int rt_ctx_destroy(rt_ctx* ctx) {
     if (!ctx) return RT_OK;
     (void)hipSetDevice(ctx->device);
+    rt::release_dqn_workspace(ctx);
     if (ctx->d_blocks) (void)hipFree(ctx->d_blocks);
     delete ctx;
     return RT_OK;
@@ -394,33 +438,44 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     }
     rc = set_device(ctx);
     if (rc != RT_OK) return rc;
-    const bool same = ctx->tiles_size == tile_size && ctx->tiles_w == params->width &&
-                      ctx->tiles_h == params->height && (int)ctx->tiles_key.size() == 2 * n_tiles &&
-                      memcmp(ctx->tiles_key.data(), tiles, sizeof(int32_t) * 2 * n_tiles) == 0;
-    if (!same) {
-        std::vector<rt::BlockDesc> blocks;
-        const int per = tile_size / 16;
-        for (int k = 0; k < n_tiles; ++k)
-            for (int sy = 0; sy < per; ++sy)
-                for (int sx = 0; sx < per; ++sx)
-                    blocks.push_back({tiles[2 * k] + 16 * sx, tiles[2 * k + 1] + 16 * sy, 16 * sx,
-                                      k * tile_size + 16 * sy});
-        rc = ensure_blocks(ctx, blocks);
-        if (rc != RT_OK) return rc;
-        ctx->tiles_key.assign(tiles, tiles + 2 * n_tiles);
-        ctx->tiles_size = tile_size;
-        ctx->tiles_w = params->width;
-        ctx->tiles_h = params->height;
-    }
+    const rt::BlockDesc* d_blocks = nullptr;
+    int n_blocks = 0;
+    rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
+    if (rc != RT_OK) return rc;
     rt::RenderLaunch a = make_launch(scene, cam, params);
-    a.blocks = ctx->d_blocks;
-    a.n_blocks = ctx->n_blocks;
+    a.blocks = d_blocks;
+    a.n_blocks = n_blocks;
     a.clip_x1 = params->width;
     a.clip_y1 = params->height;
     a.out_pitch = tile_size;
     a.out = d_out;
     a.casts = reinterpret_cast<unsigned long long*>(d_casts);
     RT_HIP(rt::launch_render(a, (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_selftest(rt_ctx* ctx, int which, uint64_t* result) {
+    if (!ctx || !result) return fail(RT_E_INVALID, "NULL argument");
+    if (which != RT_SELFTEST_RCP) return fail(RT_E_INVALID, "unknown self-test %d", which);
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    unsigned long long* d_m = nullptr;
+    unsigned* d_f = nullptr;
+    hipError_t e = hipMalloc(&d_m, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMalloc(&d_f, sizeof(unsigned));
+    if (e == hipSuccess) e = hipMemset(d_m, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_f, 0xff, sizeof(unsigned));
+    if (e == hipSuccess) e = rt::launch_selftest_rcp(d_m, d_f, 0);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned long long m = 0;
+    unsigned f = 0;
+    if (e == hipSuccess) e = hipMemcpy(&m, d_m, sizeof(m), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(&f, d_f, sizeof(f), hipMemcpyDeviceToHost);
+    (void)hipFree(d_m);
+    (void)hipFree(d_f);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_selftest: %s", hipGetErrorString(e));
+    result[0] = m;
+    result[1] = f;
     return RT_OK;
 }
 

@@ -1,0 +1,523 @@
+// rt_dqn.hip — the pretrained-DQN path tracer (BASELINE config 4) on gfx950.
+//
+// Reference: GPU/deep_learning/pre_trained_pathtracer.cu:188-491 (wavefront
+// driver, initialise_ray, trace_ray), GPU/deep_learning/nn_rendering_helpers.cu
+// (:143-172 accumulation, :280-298 NN input, :391-489 importance sampling),
+// GPU/utils/hemisphere_helpers.cu:95-226 (grid cell -> direction, Chiu's map),
+// NN_Builders/dq_network.cu + fc_layer.cu (4 ReLU affine layers).
+//
+// MI355X mapping:
+//  * k_dqn_mlp — the dense contraction.  One workgroup = 64 active rays (M),
+//    4 waves; each wave owns every M-tile and a quarter of the N-tiles, so each
+//    weight byte is fetched once per workgroup (from L2; 0.4-0.7 MB per net).
+//    v_mfma_f32_16x16x32_bf16 with fp32 accumulation; bias + ReLU fused in the
+//    epilogue; activations stay in LDS (bf16) between the four layers, so
+//    nothing but Q touches HBM.  The input x = vertices - ray_position is built
+//    in registers straight into the A fragments (never materialised; the
+//    reference writes W*H*n_in floats per bounce and ships them to DyNet on the
+//    host).  Features are ordered coordinate-major so a 32-deep K step needs
+//    one coordinate of the ray position.
+//  * k_dqn_bounce — per active ray: Q*cos over the 144 grid cells (Chiu map,
+//    one Philox draw per two cells), CDF walk, jittered direction, throughput,
+//    then the closest hit of the new ray; surviving rays are appended to the
+//    next active list (stream compaction with one atomic per wave).
+//  * rays that end are dropped from the list, so later bounces (mean path
+//    length ~24 in the thesis renders) only pay for live rays.
+
+#include <float.h>
+
+#include "rt_trace.hpp"
+
+namespace rt {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int kTileM = 64;        // rays per MLP workgroup
+constexpr int kStrideA = 320 + 8; // LDS row strides in bf16 elements (+16 B pad)
+constexpr int kStrideB = 224 + 8;
+constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
+
+__device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Append `rid` to a list with one atomic per wave (order inside the list is
+// irrelevant: every ray's result depends only on its own data).
+__device__ __forceinline__ void list_append(bool keep, int32_t rid, int32_t* list, int32_t* count) {
+    const unsigned long long m = __ballot(keep);
+    if (m == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count, __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (keep) {
+        const int rank = __popcll(m & ((1ull << lane) - 1ull));
+        list[base + rank] = rid;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MLP: one layer of 64 rows on 4 waves.  A from LDS (bf16) or, for layer 0,
+// built from the scene features and the ray positions.
+// ---------------------------------------------------------------------------
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
+                                          __bf16* out_lds, int out_stride, const float (&locm)[4][3],
+                                          float* q_rows, int rows_valid) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int K = net.K[L];
+    const int n_tiles = net.N[L] >> 4;
+    const uint16_t* __restrict__ W = net.W[L];
+    const float* __restrict__ bias = net.b[L];
+    const int r16 = lane & 15;
+    const int kg = (lane >> 4) * 8;
+    for (int chunk = wave; chunk < n_tiles; chunk += 16) {
+        // this wave's n-tiles in the chunk: chunk, chunk+4, chunk+8, chunk+12
+        int nt[4];
+        bool use[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            nt[j] = chunk + 4 * j;
+            use[j] = nt[j] < n_tiles;
+        }
+        f32x4 acc[4][4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int k0 = 0; k0 < K; k0 += 32) {
+            const int kb = k0 + kg;
+            bf16x8 a[4];
+            if (FIRST) {
+                const int c = k0 / net.vblock;  // coordinate of this K step (uniform)
+                const float4 f0 = *reinterpret_cast<const float4*>(net.feat + kb);
+                const float4 f1 = *reinterpret_cast<const float4*>(net.feat + kb + 4);
+                const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+                for (int m = 0; m < 4; ++m) {
+                    const float lc = (c == 0) ? locm[m][0] : ((c == 1) ? locm[m][1] : locm[m][2]);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) a[m][j] = (__bf16)(fv[j] - lc);
+                }
+            } else {
+#pragma unroll
+                for (int m = 0; m < 4; ++m)
+                    a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + kb);
+            }
+            bf16x8 bw[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (use[j])
+                    bw[j] = *reinterpret_cast<const bf16x8*>(W + (size_t)(nt[j] * 16 + r16) * K + kb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (use[j]) {
+#pragma unroll
+                    for (int m = 0; m < 4; ++m)
+                        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], bw[j], acc[m][j], 0, 0, 0);
+                }
+        }
+        // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!use[j]) continue;
+            const int col = nt[j] * 16 + r16;
+            const float bj = bias[col];
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int row = m * 16 + (lane >> 4) * 4 + r;
+                    float v = acc[m][j][r] + bj;
+                    v = v > 0.0f ? v : 0.0f;
+                    if (LAST) {
+                        if (row < rows_valid) q_rows[(size_t)row * kDqnActions + col] = v;
+                    } else {
+                        out_lds[row * out_stride + col] = (__bf16)v;
+                    }
+                }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
+                                                 const int32_t* __restrict__ list,
+                                                 const int32_t* __restrict__ count, int max_rows,
+                                                 float* __restrict__ q) {
+    __shared__ __attribute__((aligned(16))) __bf16 bufA[kTileM * kStrideA];
+    __shared__ __attribute__((aligned(16))) __bf16 bufB[kTileM * kStrideB];
+    const int n_rows = (count != nullptr) ? min(*count, max_rows) : max_rows;
+    const int row0 = blockIdx.x * kTileM;
+    if (row0 >= n_rows) return;
+    const int rows_valid = min(kTileM, n_rows - row0);
+    const int lane = threadIdx.x & 63;
+    float locm[4][3];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int row = m * 16 + (lane & 15);
+        if (row < rows_valid) {
+            const int rid = (list != nullptr) ? list[row0 + row] : (row0 + row);
+            locm[m][0] = loc[(size_t)rid * 3 + 0];
+            locm[m][1] = loc[(size_t)rid * 3 + 1];
+            locm[m][2] = loc[(size_t)rid * 3 + 2];
+        } else {
+            locm[m][0] = locm[m][1] = locm[m][2] = 0.0f;
+        }
+    }
+    float* q_rows = q + (size_t)row0 * kDqnActions;
+    mlp_layer<true, false>(net, 0, nullptr, 0, bufB, kStrideB, locm, nullptr, rows_valid);
+    __syncthreads();
+    mlp_layer<false, false>(net, 1, bufB, kStrideB, bufA, kStrideA, locm, nullptr, rows_valid);
+    __syncthreads();
+    mlp_layer<false, false>(net, 2, bufA, kStrideA, bufB, kStrideB, locm, nullptr, rows_valid);
+    __syncthreads();
+    mlp_layer<false, true>(net, 3, bufB, kStrideB, nullptr, 0, locm, q_rows, rows_valid);
+}
+
+// ---------------------------------------------------------------------------
+// Grid cell -> world direction (hemisphere_helpers.cu:95-121 + Chiu's map
+// :123-226), restated in turns: theta from cos = 1 - xx^2,
+// sin = xx*sqrt(2 - xx^2); phi = offset + (yy/xx)/8 turns.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void chiu_map(float x, float y, float* xr, float* yr, float* zr) {
+    x = 2.0f * x - 1.0f;
+    y = 2.0f * y - 1.0f;
+    float xx, yy, off;
+    bool origin = false;
+    if (y > -x) {
+        if (y < x) {
+            xx = x;
+            if (y > 0.0f) { off = 0.0f; yy = y; }
+            else { off = 0.875f; yy = x + y; }
+        } else {
+            xx = y;
+            if (x > 0.0f) { off = 0.125f; yy = y - x; }
+            else { off = 0.25f; yy = -x; }
+        }
+    } else {
+        if (y > x) {
+            xx = -x;
+            if (y > 0.0f) { off = 0.375f; yy = -x - y; }
+            else { off = 0.5f; yy = -y; }
+        } else {
+            xx = -y;
+            if (x > 0.0f) { off = 0.75f; yy = x; }
+            else if (y != 0.0f) { off = 0.625f; yy = x - y; }
+            else { origin = true; xx = 1.0f; yy = 0.0f; off = 0.0f; }
+        }
+    }
+    const float c = 1.0f - xx * xx;
+    const float s = xx * sqrtf(2.0f - xx * xx);
+    const float phi = off + 0.125f * (yy / xx);
+    float sp, cp;
+    sincos_turn(phi, &sp, &cp);
+    *xr = origin ? 0.0f : s * cp;
+    *yr = origin ? 1.0f : c;
+    *zr = origin ? 0.0f : s * sp;
+}
+
+// convert_grid_pos_to_direction_random: map((x+r1)/12, (y+r2)/12), then
+// world = mat4(T, N, B, pos) * (xh, yh, zh, 1) (glm order), dir = normalize(world - pos)
+__device__ __forceinline__ f3 grid_direction(float gx, float gy, f3 N, f3 T, f3 B, f3 pos) {
+    float xh, yh, zh;
+    chiu_map(gx / (float)kDqnGrid, gy / (float)kDqnGrid, &xh, &yh, &zh);
+    const f3 w = make3((T.x * xh + N.x * yh) + (B.x * zh + pos.x * 1.0f),
+                       (T.y * xh + N.y * yh) + (B.y * zh + pos.y * 1.0f),
+                       (T.z * xh + N.z * yh) + (B.z * zh + pos.z * 1.0f));
+    return normalize(make3(w.x - pos.x, w.y - pos.y, w.z - pos.z));
+}
+
+struct SampleOut {
+    int action;   // -1: no cell selected (the reference then traces a zero direction: a miss)
+    f3 dir;
+};
+
+// importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray;
+// q: its 144 Q values, overwritten with Q*cos (as the reference does in place).
+__device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, f3 N, f3 T, f3 B, f3 pos,
+                                                   uint32_t pix, uint32_t smp, uint32_t ev,
+                                                   uint32_t k0, uint32_t k1, f3* tp, bool update_tp) {
+    uint32_t o[4];
+    philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
+    const float rv = u01(o[0]);
+    float total = 0.0f;
+    for (int a2 = 0; a2 < kDqnActions / 2; ++a2) {
+        philox4x32_10(pix, smp, ev, 1u + (uint32_t)a2, k0, k1, o);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int a = 2 * a2 + h;
+            const int gxi = a / kDqnGrid;
+            const int gyi = a - gxi * kDqnGrid;
+            const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
+            const f3 d = grid_direction((float)gxi + r1, (float)gyi + r2, N, T, B, pos);
+            const float c = dot(N, d);
+            const float qc = q[a] * c;
+            q[a] = qc;
+            total = total + qc;
+        }
+    }
+    SampleOut res;
+    res.action = -1;
+    res.dir = make3(0.0f, 0.0f, 0.0f);
+    float q_sum = 0.0f;
+    float qd_sel = 0.0f;
+    for (int a = 0; a < kDqnActions; ++a) {
+        const float qd = q[a] / total;
+        q_sum = q_sum + qd;
+        if (q_sum > rv) {
+            res.action = a;
+            qd_sel = qd;
+            break;
+        }
+    }
+    if (res.action >= 0) {
+        philox4x32_10(pix, smp, ev, 1u + kDqnActions / 2, k0, k1, o);
+        const int gxi = res.action / kDqnGrid;
+        const int gyi = res.action - gxi * kDqnGrid;
+        res.dir = grid_direction((float)gxi + u01(o[0]), (float)gyi + u01(o[1]), N, T, B, pos);
+        if (update_tp) {
+            const float c = dot(N, res.dir);
+            const float pdf = kRho * (qd_sel / kGridRho);
+            tp->x = (tp->x * c) / pdf;
+            tp->y = (tp->y * c) / pdf;
+            tp->z = (tp->z * c) / pdf;
+        }
+    }
+    return res;
+}
+
+// trace_ray (pre_trained_pathtracer.cu:413-491): Ray(pos + dir*1e-5, dir), GPU hit rule.
+// Returns true if the ray continues (hit a surface).
+__device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, f3* loc_out, int* tri_out,
+                                          f3* tp) {
+    const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
+    const f3 d = normalize(dir);
+    const Hit h = closest_hit<1>(a.scene.isect, a.scene.n_tri, o, d, a.t_scale);
+    if (h.tri < 0) {
+        *tp = make3(tp->x * a.env_light, tp->y * a.env_light, tp->z * a.env_light);
+        return false;
+    }
+    const float4 c = a.scene.shade[h.tri * kShadeF4 + 3];
+    if (h.tri >= a.scene.n_surf) {
+        *tp = make3(tp->x * c.x, tp->y * c.y, tp->z * c.z);
+        return false;
+    }
+    const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+    *loc_out = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+    *tri_out = h.tri;
+    *tp = make3(tp->x * c.x, tp->y * c.y, tp->z * c.z);  // *= BRDF
+    return true;
+}
+
+__device__ __forceinline__ f3 ld3(const float* p, int i) {
+    return make3(p[(size_t)i * 3], p[(size_t)i * 3 + 1], p[(size_t)i * 3 + 2]);
+}
+__device__ __forceinline__ void st3(float* p, int i, f3 v) {
+    p[(size_t)i * 3] = v.x;
+    p[(size_t)i * 3 + 1] = v.y;
+    p[(size_t)i * 3 + 2] = v.z;
+}
+
+// ray id -> pixel of the tile list
+__device__ __forceinline__ bool ray_pixel(const DqnLaunch& a, int rid, int* px, int* py) {
+    const BlockDesc blk = a.blocks[rid >> 8];
+    const int q = rid & 255;
+    *px = blk.px0 + (q & 15);
+    *py = blk.py0 + (q >> 4);
+    return (*px < a.clip_x1) && (*py < a.clip_y1);
+}
+
+__global__ __launch_bounds__(256) void k_dqn_frame_begin(const DqnLaunch a) {
+    const int rid = blockIdx.x * 256 + threadIdx.x;
+    if (rid >= a.rays.n) return;
+    int px, py;
+    const bool valid = ray_pixel(a, rid, &px, &py);
+    a.rays.pix[rid] = valid ? (uint32_t)py * (uint32_t)a.width + (uint32_t)px : 0u;
+    st3(a.rays.total, rid, make3(0.0f, 0.0f, 0.0f));
+}
+
+// initialise_ray + the first trace_ray (bounce 0: no Q evaluation)
+__global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a, int sample) {
+    const int rid = blockIdx.x * 256 + threadIdx.x;
+    bool keep = false;
+    unsigned casts = 0;
+    if (rid < a.rays.n) {
+        int px, py;
+        const bool valid = ray_pixel(a, rid, &px, &py);
+        f3 tp = make3(valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f);
+        if (valid) {
+            float r1, r2;
+            draw2(a.rays.pix[rid], (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+            const float x = (float)px + r1, y = (float)py + r2;
+            f3 dir = normalize(make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height));
+            const float w = 1.0f;
+            f3 r;
+            r.x = (a.cos_y * dir.x + 0.0f * dir.y) + (-a.sin_y * dir.z + 0.0f * w);
+            r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
+            r.z = (a.sin_y * dir.x + 0.0f * dir.y) + (a.cos_y * dir.z + 0.0f * w);
+            const float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
+            f3 d;
+            d.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
+            d.y = (0.0f * r.x + a.cos_x * r.y) + (a.sin_x * r.z + 0.0f * rw);
+            d.z = (0.0f * r.x + -a.sin_x * r.y) + (a.cos_x * r.z + 0.0f * rw);
+            f3 loc;
+            int tri = 0;
+            keep = dqn_trace(a, make3(a.cam_x, a.cam_y, a.cam_z), d, &loc, &tri, &tp);
+            casts = 1;
+            if (keep) {
+                st3(a.rays.loc, rid, loc);
+                a.rays.tri[rid] = tri;
+            }
+        }
+        st3(a.rays.tp, rid, tp);
+    }
+    list_append(keep, rid, a.rays.list[0], a.rays.count + 0);
+    const unsigned tot = wave_sum_u(casts);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.rays.casts, (unsigned long long)tot);
+}
+
+// one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
+__global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sample, int bounce) {
+    const int cur = (bounce - 1) & 1, nxt = bounce & 1;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int n_act = a.rays.count[cur];
+    if ((int)(blockIdx.x * 256) >= n_act) return;  // uniform
+    bool keep = false;
+    unsigned casts = 0;
+    int rid = 0;
+    if (i < n_act) {
+        rid = a.rays.list[cur][i];
+        const int tri = a.rays.tri[rid];
+        const f3 pos = ld3(a.rays.loc, rid);
+        f3 tp = ld3(a.rays.tp, rid);
+        const float4 N4 = a.scene.shade[tri * kShadeF4 + 0];
+        const float4 T4 = a.scene.shade[tri * kShadeF4 + 1];
+        const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
+        const SampleOut so =
+            sample_from_q(a.rays.q + (size_t)i * kDqnActions, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                          make3(B4.x, B4.y, B4.z), pos, a.rays.pix[rid], (uint32_t)sample,
+                          1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
+        casts = 1;
+        f3 loc = pos;
+        int ntri = tri;
+        if (so.action >= 0) {
+            keep = dqn_trace(a, pos, so.dir, &loc, &ntri, &tp);
+        } else {
+            // zero direction: the reference's ray is NaN and hits nothing
+            tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+        }
+        if (keep) {
+            st3(a.rays.loc, rid, loc);
+            a.rays.tri[rid] = ntri;
+        }
+        st3(a.rays.tp, rid, tp);
+    }
+    list_append(keep, rid, a.rays.list[nxt], a.rays.count + nxt);
+    const unsigned tot = wave_sum_u(casts);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(a.rays.casts, (unsigned long long)tot);
+}
+
+// update_total_throughput (nn_rendering_helpers.cu:143-156)
+__global__ __launch_bounds__(256) void k_dqn_accumulate(const DqnLaunch a) {
+    const int rid = blockIdx.x * 256 + threadIdx.x;
+    if (rid >= a.rays.n) return;
+    const f3 t = ld3(a.rays.total, rid), p = ld3(a.rays.tp, rid);
+    st3(a.rays.total, rid, make3(t.x + p.x, t.y + p.y, t.z + p.z));
+}
+
+// update_device_buffer (nn_rendering_helpers.cu:159-172): total / SPP into the tile output
+__global__ __launch_bounds__(256) void k_dqn_finish(const DqnLaunch a) {
+    const int rid = blockIdx.x * 256 + threadIdx.x;
+    if (rid >= a.rays.n) return;
+    int px, py;
+    if (!ray_pixel(a, rid, &px, &py)) return;
+    const BlockDesc blk = a.blocks[rid >> 8];
+    const int q = rid & 255;
+    const f3 t = ld3(a.rays.total, rid);
+    const float fs = (float)a.spp;
+    float* dst = a.out + ((size_t)(blk.oy0 + (q >> 4)) * (size_t)a.out_pitch + (size_t)(blk.ox0 + (q & 15))) * 3;
+    dst[0] = t.x / fs;
+    dst[1] = t.y / fs;
+    dst[2] = t.z / fs;
+}
+
+__global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, float* q, const float* loc,
+                                                         const int32_t* tri, const uint32_t* pix, int n,
+                                                         int sample, int bounce, uint32_t k0, uint32_t k1,
+                                                         float* tp, float* dir_out, int32_t* action) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int t = tri[i];
+    const float4 N4 = s.shade[t * kShadeF4 + 0];
+    const float4 T4 = s.shade[t * kShadeF4 + 1];
+    const float4 B4 = s.shade[t * kShadeF4 + 2];
+    f3 tpv = ld3(tp, i);
+    const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, make3(N4.x, N4.y, N4.z),
+                                       make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), ld3(loc, i),
+                                       pix[i], (uint32_t)sample, 1u + (uint32_t)bounce, k0, k1, &tpv, true);
+    st3(tp, i, tpv);
+    st3(dir_out, i, so.dir);
+    action[i] = so.action;
+}
+
+}  // namespace
+
+hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
+                          int max_rows, float* q, hipStream_t stream) {
+    if (max_rows <= 0) return hipSuccess;
+    const int blocks = (max_rows + kTileM - 1) / kTileM;
+    hipLaunchKernelGGL(k_dqn_mlp, dim3((unsigned)blocks), dim3(256), 0, stream, net, loc, list, count,
+                       max_rows, q);
+    return hipGetLastError();
+}
+
+static unsigned ray_blocks(const DqnLaunch& a) { return (unsigned)((a.rays.n + 255) / 256); }
+
+hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_dqn_frame_begin, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream) {
+    hipLaunchKernelGGL(k_dqn_camera, dim3(ray_blocks(a)), dim3(256), 0, stream, a, sample);
+    return hipGetLastError();
+}
+
+hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream) {
+    const int cur = (bounce - 1) & 1;
+    hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
+                                  a.rays.q, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dqn_bounce, dim3(ray_blocks(a)), dim3(256), 0, stream, a, sample, bounce);
+    return hipGetLastError();
+}
+
+hipError_t launch_dqn_accumulate(const DqnLaunch& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_dqn_accumulate, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dqn_finish(const DqnLaunch& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_dqn_finish, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_dqn_sample_only(const DeviceScene& s, const float* q, const float* loc, const int32_t* tri,
+                                  const uint32_t* pix, int n, int sample, int bounce, uint32_t seed_lo,
+                                  uint32_t seed_hi, float* tp, float* dir_out, int32_t* action,
+                                  hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dqn_sample_only, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, s,
+                       const_cast<float*>(q), loc, tri, pix, n, sample, bounce, seed_lo, seed_hi, tp, dir_out,
+                       action);
+    return hipGetLastError();
+}
+
+}  // namespace rt

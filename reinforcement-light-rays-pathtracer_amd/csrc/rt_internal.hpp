@@ -57,9 +57,75 @@ struct RenderLaunch {
     unsigned long long* casts;
 };
 
+// ---- DQN Q-value network (dq_network/fc_layer) and its wavefront renderer ----
+// Four ReLU layers n_in -> h1 -> h2 -> h3 -> n_out (NN_Builders/dq_network.cu:8-33).
+// Device weights: bf16, row-major [out_padded][in_padded], zero padded; the input
+// features are permuted coordinate-major (all x, then all y, then all z, each
+// block padded to a multiple of 32) so a 32-wide K step needs one coordinate of
+// the ray location; W1's columns are permuted to match.
+constexpr int kDqnActions = 144;  // GRID_RESOLUTION^2 (GPU/constants/radiance_volumes_settings.h:9)
+constexpr int kDqnGrid = 12;
+
+struct DqnNet {
+    const uint16_t* W[4] = {nullptr, nullptr, nullptr, nullptr};  // bf16 bits
+    const float* b[4] = {nullptr, nullptr, nullptr, nullptr};      // fp32, padded
+    const float* feat = nullptr;  // permuted scene vertex coordinates [K[0]] (0 in padding)
+    int K[4] = {0, 0, 0, 0};      // padded input width of each layer (multiple of 32)
+    int N[4] = {0, 0, 0, 0};      // padded output width of each layer (multiple of 32; last = 144)
+    int n_vert = 0;               // vertices (n_in / 3)
+    int vblock = 0;               // padded per-coordinate block (multiple of 32)
+};
+
+// Ray state of the DQN wavefront renderer (SoA over the rays of a frame part).
+struct DqnRays {
+    float* loc = nullptr;   // [n][3] current position (GPU: ray_locations_device)
+    float* dir = nullptr;   // [n][3]
+    float* tp = nullptr;    // [n][3] throughput
+    float* total = nullptr; // [n][3] sum over samples
+    int32_t* tri = nullptr; // [n] triangle of the last surface hit (normal / frame)
+    uint32_t* pix = nullptr;   // [n] global pixel id (RNG key)
+    int32_t* list[2] = {nullptr, nullptr};  // active ray lists (ping-pong)
+    int32_t* count = nullptr;  // [2 + 1] list sizes, [2] = ray casts of this call (low 32 bits unused)
+    unsigned long long* casts = nullptr;
+    float* q = nullptr;     // [n][144] Q values of the active list (list order)
+    int n = 0;
+};
+
+struct DqnLaunch {
+    DeviceScene scene;
+    DqnNet net;
+    DqnRays rays;
+    int width, height, spp, max_bounces;
+    uint32_t seed_lo, seed_hi;
+    float t_scale, env_light;
+    float cam_x, cam_y, cam_z;
+    float cos_y, sin_y, cos_x, sin_x;
+    const BlockDesc* blocks;   // 16x16 pixel blocks (ray id = block * 256 + y*16 + x)
+    int n_blocks;
+    int clip_x1, clip_y1;
+    int out_pitch;
+    float* out;
+};
+
+hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
+                          const int32_t* count, int max_rows, float* q, hipStream_t stream);
+hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream);
+hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream);
+hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream);
+hipError_t launch_dqn_accumulate(const DqnLaunch& a, hipStream_t stream);
+hipError_t launch_dqn_finish(const DqnLaunch& a, hipStream_t stream);
+// sampler alone (parity): rows i < n, Q [n][144] (overwritten with Q*cos), pixel/tri/loc per row
+hipError_t launch_dqn_sample_only(const DeviceScene& s, const float* q, const float* loc,
+                                  const int32_t* tri, const uint32_t* pix, int n, int sample,
+                                  int bounce, uint32_t seed_lo, uint32_t seed_hi, float* tp,
+                                  float* dir_out, int32_t* action, hipStream_t stream);
+
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
                             hipStream_t stream);
+
+// exhaustive rcp_rn == 1.0f/x check over all 2^32 floats (4096 x 256 threads x 4096)
+hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream);
 
 // returns hipErrorInvalidValue for combinations the kernels do not instantiate
 hipError_t launch_render(const RenderLaunch& a, hipStream_t stream);

@@ -28,88 +28,11 @@
 
 #include <float.h>
 
-#include "rt_internal.hpp"
+#include "rt_trace.hpp"
 
 namespace rt {
 
 namespace {
-
-constexpr float kRho = 1.0f / (2.0f * kPi);  // RHO: GPU/constants/image_settings.h:14
-
-struct Hit {
-    float t;
-    int tri;
-};
-
-// Closest hit over the triangle soup.  D = dir * t_scale, A = [-D | e1 | e2],
-// x = (t,u,v) by Cramer's rule with GLM's determinant order
-// (glm/glm/detail/func_matrix.inl:214-217):
-//   det(c0,c1,c2) = (c0.x*(c1.y*c2.z - c2.y*c1.z) - c1.x*(c0.y*c2.z - c2.y*c0.z))
-//                   + c2.x*(c0.y*c1.z - c1.y*c0.z)
-// The minors shared between detA, det_t, det_u and det_v are evaluated once
-// (same operands, same order, so the same bits).
-// RULE 0 = CPU triangle.cpp.o predicate (inv = 1/detA; accept t>=0, u>=0, v>=0,
-//          u+v<=1, t < best+1e-5, t > 1e-5; best starts at FLT_MAX)
-// RULE 1 = GPU/rays/ray.cu:63-64 (true divisions; t < best; best starts 999999)
-template <int RULE>
-__device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n_tri, f3 o, f3 d,
-                                           float t_scale) {
-    const float nDx = -(d.x * t_scale);
-    const float nDy = -(d.y * t_scale);
-    const float nDz = -(d.z * t_scale);
-    Hit h;
-    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
-    h.tri = -1;
-    for (int i = 0; i < n_tri; ++i) {
-        const float4 A = tri[i * kIsectF4 + 0];
-        const float4 E1 = tri[i * kIsectF4 + 1];
-        const float4 E2 = tri[i * kIsectF4 + 2];
-        const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
-        // detA = det(-D, e1, e2)
-        const float s1 = nDy * E2.z - E2.y * nDz;
-        const float s2 = nDy * E1.z - E1.y * nDz;
-        const float detA = (nDx * A.w - E1.x * s1) + E2.x * s2;
-        // det_t = det(b, e1, e2)
-        const float s3 = by * E2.z - E2.y * bz;
-        const float s4 = by * E1.z - E1.y * bz;
-        const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
-        float t;
-        if (RULE == 0) {
-            const float inv = 1.0f / detA;
-            t = det_t * inv;
-            const bool tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t + kEps) && (t > kEps);
-            if (tpass) {
-                // det_u = det(-D, b, e2), det_v = det(-D, e1, b)
-                const float s5 = nDy * bz - by * nDz;
-                const float s6 = E1.y * bz - by * E1.z;
-                const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
-                const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
-                const float u = det_u * inv;
-                const float v = det_v * inv;
-                if (u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
-                    h.t = t;
-                    h.tri = i;
-                }
-            }
-        } else {
-            t = det_t / detA;
-            const bool tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t);
-            if (tpass) {
-                const float s5 = nDy * bz - by * nDz;
-                const float s6 = E1.y * bz - by * E1.z;
-                const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
-                const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
-                const float u = det_u / detA;
-                const float v = det_v / detA;
-                if (u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f) {
-                    h.t = t;
-                    h.tri = i;
-                }
-            }
-        }
-    }
-    return h;
-}
 
 template <int RULE>
 __global__ __launch_bounds__(256) void k_intersect(const float4* __restrict__ tri, int n_tri,
@@ -127,14 +50,6 @@ __global__ __launch_bounds__(256) void k_intersect(const float4* __restrict__ tr
     out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
 }
 
-// two uniforms of event `ev` of sample `smp` of pixel `pix`
-__device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, uint32_t k0,
-                                      uint32_t k1, float* a, float* b) {
-    uint32_t o[4];
-    philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
-    *a = u01(o[0]);
-    *b = u01(o[1]);
-}
 
 // Camera ray through (px+r1, py+r2): default_path_tracing.cpp:25-34, Ray::Ray
 // (ray.cpp:7-11), rotate_ray (ray.cpp:47-52; GPU/rays/ray.cu:161-172), with
@@ -172,7 +87,10 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 // back to the camera: L_k = ((L_{k+1} * brdf_k) * cos_k) / rho), cap <= 2.
 // PRESET 1: GPU engine iterative throughput.
 template <int PRESET, int SAMPLER, int RULE>
-__global__ __launch_bounds__(256) void k_render(const RenderLaunch a) {
+#ifndef RT_MIN_WAVES
+#define RT_MIN_WAVES 1
+#endif
+__global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch a) {
     // workgroup -> (16x16 block, part); lane -> (pixel of the block, sample chunk)
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -339,7 +257,32 @@ __global__ __launch_bounds__(256) void k_render(const RenderLaunch a) {
     }
 }
 
+// Exhaustive check of rcp_rn against IEEE division: thread g covers the
+// 4096 bit patterns [g*4096, (g+1)*4096).  Counts mismatches (ignoring NaN
+// payloads) and keeps the smallest mismatching pattern.
+__global__ __launch_bounds__(256) void k_selftest_rcp(unsigned long long* mism, unsigned* first) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    unsigned bad = 0;
+    for (uint32_t k = 0; k < 4096u; ++k) {
+        const uint32_t bits = (uint32_t)(g * 4096u + k);
+        const float x = __uint_as_float(bits);
+        const float a = rcp_rn(x);
+        const float b = 1.0f / x;
+        const bool same = (__float_as_uint(a) == __float_as_uint(b)) || (a != a && b != b);
+        if (!same) {
+            ++bad;
+            atomicMin(first, bits);
+        }
+    }
+    if (bad) atomicAdd(mism, (unsigned long long)bad);
+}
+
 }  // namespace
+
+hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream) {
+    hipLaunchKernelGGL(k_selftest_rcp, dim3(4096), dim3(256), 0, stream, mism, first);
+    return hipGetLastError();
+}
 
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, float* out_t, int32_t* out_hit,

@@ -1,0 +1,225 @@
+// rt_trace.hpp — device-side building blocks shared by the path-trace
+// megakernel (rt_kernels.hip) and the DQN wavefront kernels (rt_dqn.hip):
+// the closest-hit loop with the reference's two hit predicates, the
+// correctly-rounded reciprocal, and the Philox draws.
+#pragma once
+
+#include <float.h>
+
+#include "rt_internal.hpp"
+
+namespace rt {
+
+constexpr float kRho = 1.0f / (2.0f * kPi);  // RHO: GPU/constants/image_settings.h:14
+
+struct Hit {
+    float t;
+    int tri;
+};
+
+// Closest hit over the triangle soup.  D = dir * t_scale, A = [-D | e1 | e2],
+// x = (t,u,v) by Cramer's rule with GLM's determinant order
+// (glm/glm/detail/func_matrix.inl:214-217):
+//   det(c0,c1,c2) = (c0.x*(c1.y*c2.z - c2.y*c1.z) - c1.x*(c0.y*c2.z - c2.y*c0.z))
+//                   + c2.x*(c0.y*c1.z - c1.y*c0.z)
+// The minors shared between detA, det_t, det_u and det_v are evaluated once
+// (same operands, same order, so the same bits).
+// RULE 0 = CPU triangle.cpp.o predicate (inv = 1/detA; accept t>=0, u>=0, v>=0,
+//          u+v<=1, t < best+1e-5, t > 1e-5; best starts at FLT_MAX)
+// RULE 1 = GPU/rays/ray.cu:63-64 (true divisions; t < best; best starts 999999)
+// Build-time knobs (A/B experiments; defaults are the shipped configuration):
+//   RT_HIT_MODE 0: exact; u/v behind a branch on the t test (skipped per wave)
+//               1: exact, branch-free
+//               2: conservative approximate rejection (v_rcp_f32) first; the
+//                  exact IEEE test runs only for lanes it cannot reject
+//   RT_UNROLL   unroll factor of the triangle loop
+#ifndef RT_HIT_MODE
+#define RT_HIT_MODE 0
+#endif
+#ifndef RT_UNROLL
+#define RT_UNROLL 1
+#endif
+//   RT_FAST_RCP 1: 1/detA by rcp_rn (v_rcp_f32 + Newton, exhaustively verified)
+//   RT_RCP_STEPS Newton steps of rcp_rn
+#ifndef RT_FAST_RCP
+#define RT_FAST_RCP 0
+#endif
+#ifndef RT_RCP_STEPS
+#define RT_RCP_STEPS 1
+#endif
+#if RT_FAST_RCP
+#define RT_RCP(x) rcp_rn(x)
+#else
+#define RT_RCP(x) (1.0f / (x))
+#endif
+
+// Correctly rounded 1/x.  For |x| in [2^-125, 2^125], v_rcp_f32 (<= 1 ulp)
+// refined by Newton steps in FMA; the result equals IEEE 1.0f/x bit for bit
+// (verified over every such float by rt_selftest(RT_SELFTEST_RCP), a
+// GPU test).  Other inputs take hipcc's IEEE division sequence.
+__device__ __forceinline__ float rcp_rn(float x) {
+    const float ax = fabsf(x);
+    float r = __builtin_amdgcn_rcpf(x);
+    float e = fmaf(-x, r, 1.0f);
+    r = fmaf(e, r, r);
+#if RT_RCP_STEPS > 1
+    e = fmaf(-x, r, 1.0f);
+    r = fmaf(e, r, r);
+#endif
+    const bool out_of_range = !(ax >= 0x1p-125f && ax <= 0x1p125f);
+    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {  // wave-uniform, rare
+        const float q = 1.0f / x;
+        r = out_of_range ? q : r;
+    }
+    return r;
+}
+
+// rcp_rn's refinement of an already computed v_rcp_f32 value r0 = rcp(x)
+__device__ __forceinline__ float rcp_rn_from(float x, float r0) {
+    const float ax = fabsf(x);
+    const float e = fmaf(-x, r0, 1.0f);
+    float r = fmaf(e, r0, r0);
+    const bool out_of_range = !(ax >= 0x1p-125f && ax <= 0x1p125f);
+    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {
+        const float q = 1.0f / x;
+        r = out_of_range ? q : r;
+    }
+    return r;
+}
+
+// Exact hit test of one triangle (the reference's arithmetic, see above).
+template <int RULE>
+__device__ __forceinline__ void exact_test_inv(float detA, float inv, float det_t, float det_u,
+                                               float det_v, int i, Hit& h) {
+    // RULE 0 with inv = RN(1/detA) already computed
+    const float t = det_t * inv;
+    const float u = det_u * inv;
+    const float v = det_v * inv;
+    if ((detA != 0.0f) && (t >= 0.0f) && (u >= 0.0f) && (v >= 0.0f) && ((u + v) <= 1.0f) &&
+        (t < h.t + kEps) && (t > kEps)) {
+        h.t = t;
+        h.tri = i;
+    }
+}
+
+template <int RULE>
+__device__ __forceinline__ void exact_test(float detA, float det_t, float det_u, float det_v, int i,
+                                           Hit& h) {
+    if (RULE == 0) {
+        const float inv = RT_RCP(detA);
+        const float t = det_t * inv;
+        const float u = det_u * inv;
+        const float v = det_v * inv;
+        if ((detA != 0.0f) && (t >= 0.0f) && (u >= 0.0f) && (v >= 0.0f) && ((u + v) <= 1.0f) &&
+            (t < h.t + kEps) && (t > kEps)) {
+            h.t = t;
+            h.tri = i;
+        }
+    } else {
+        const float t = det_t / detA;
+        const float u = det_u / detA;
+        const float v = det_v / detA;
+        if ((detA != 0.0f) && (t >= 0.0f) && (u >= 0.0f) && (v >= 0.0f) && ((u + v) <= 1.0f) &&
+            (t < h.t)) {
+            h.t = t;
+            h.tri = i;
+        }
+    }
+}
+
+template <int RULE>
+__device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n_tri, f3 o, f3 d,
+                                           float t_scale) {
+    const float nDx = -(d.x * t_scale);
+    const float nDy = -(d.y * t_scale);
+    const float nDz = -(d.z * t_scale);
+    Hit h;
+    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+    h.tri = -1;
+#if RT_HIT_MODE == 2
+    // upper bound of the t window, widened by 2^-18 (RULE 0: best + eps)
+    float hi = ((RULE == 0) ? (h.t + kEps) : h.t) * (1.0f + 0x1p-18f);
+#endif
+#pragma unroll RT_UNROLL
+    for (int i = 0; i < n_tri; ++i) {
+        const float4 A = tri[i * kIsectF4 + 0];
+        const float4 E1 = tri[i * kIsectF4 + 1];
+        const float4 E2 = tri[i * kIsectF4 + 2];
+        const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
+        // detA = det(-D, e1, e2)
+        const float s1 = nDy * E2.z - E2.y * nDz;
+        const float s2 = nDy * E1.z - E1.y * nDz;
+        const float detA = (nDx * A.w - E1.x * s1) + E2.x * s2;
+        // det_t = det(b, e1, e2)
+        const float s3 = by * E2.z - E2.y * bz;
+        const float s4 = by * E1.z - E1.y * bz;
+        const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
+#if RT_HIT_MODE == 0
+        bool tpass;
+        float inv = 0.0f;
+        if (RULE == 0) {
+            inv = RT_RCP(detA);
+            const float t = det_t * inv;
+            tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t + kEps) && (t > kEps);
+        } else {
+            const float t = det_t / detA;
+            tpass = (detA != 0.0f) && (t >= 0.0f) && (t < h.t);
+        }
+        if (tpass) {
+            // det_u = det(-D, b, e2), det_v = det(-D, e1, b)
+            const float s5 = nDy * bz - by * nDz;
+            const float s6 = E1.y * bz - by * E1.z;
+            const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+            const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+            exact_test<RULE>(detA, det_t, det_u, det_v, i, h);
+        }
+#else
+        const float s5 = nDy * bz - by * nDz;
+        const float s6 = E1.y * bz - by * E1.z;
+        const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+        const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+#if RT_HIT_MODE == 1
+        exact_test<RULE>(detA, det_t, det_u, det_v, i, h);
+#else
+        // Conservative rejection: with |detA| in [2^-100, 2^100], v_rcp_f32 is
+        // within 1 ulp, so ta/ua/va differ from the exact t/u/v by < 2^-21
+        // relative.  A lane is rejected only if the exact test must fail:
+        //   ta < eps(1-2^-18) (RULE 0) or ta < -2^-90 (RULE 1)  =>  t fails
+        //   ta > hi = (best [+eps]) (1+2^-18)                   =>  t fails
+        //   ua or va < -2^-90 (no underflow to -0 possible)     =>  u/v fail
+        //   ua + va > 1 + 2^-18 (with ua, va >= -2^-90)         =>  u+v > 1
+        // NaN/inf or out-of-range detA never rejects.
+        const float r = __builtin_amdgcn_rcpf(detA);
+        const float ta = det_t * r, ua = det_u * r, va = det_v * r;
+        const float ad = fabsf(detA);
+        const float lo = (RULE == 0) ? kEps * (1.0f - 0x1p-18f) : -0x1p-90f;
+        const bool sure_miss = (ad >= 0x1p-100f) && (ad <= 0x1p100f) &&
+                               ((ta < lo) || (ta > hi) || (ua < -0x1p-90f) || (va < -0x1p-90f) ||
+                                ((ua + va) > 1.0f + 0x1p-18f));
+        if (!sure_miss) {
+#if RT_FAST_RCP
+            if (RULE == 0)
+                exact_test_inv<RULE>(detA, rcp_rn_from(detA, r), det_t, det_u, det_v, i, h);
+            else
+                exact_test<RULE>(detA, det_t, det_u, det_v, i, h);
+#else
+            exact_test<RULE>(detA, det_t, det_u, det_v, i, h);
+#endif
+            hi = ((RULE == 0) ? (h.t + kEps) : h.t) * (1.0f + 0x1p-18f);
+        }
+#endif
+#endif
+    }
+    return h;
+}
+
+// two uniforms of event `ev` of sample `smp` of pixel `pix`
+__device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, uint32_t k0,
+                                      uint32_t k1, float* a, float* b) {
+    uint32_t o[4];
+    philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
+    *a = u01(o[0]);
+    *b = u01(o[1]);
+}
+
+}  // namespace rt

@@ -35,7 +35,9 @@ EXPORTS = (
     "rt_cornell_counts", "rt_cornell_geometry", "rt_obj_geometry",
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
     "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
-    "rt_pack_argb", "rt_save_bmp",
+    "rt_pack_argb", "rt_save_bmp", "rt_selftest",
+    "rt_dynet_read", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_sample",
+    "rt_render_dqn", "rt_render_dqn_tiles_device",
 )
 
 
@@ -91,6 +93,18 @@ def _declare(lib):
                                        _IP, i, i, _P, _P, _P]),
         "rt_pack_argb": (i, [_FP, i, _UP]),
         "rt_save_bmp": (i, [ctypes.c_char_p, _UP, i, i]),
+        "rt_selftest": (i, [_P, i, _U64P]),
+        "rt_dynet_read": (i, [ctypes.c_char_p, i, _IP, _IP, _FP, ctypes.POINTER(i),
+                              ctypes.POINTER(ctypes.c_int64)]),
+        "rt_dqn_create": (i, [_P, _FP, i, _IP, i, ctypes.POINTER(_FP), ctypes.POINTER(_FP),
+                              ctypes.POINTER(_P)]),
+        "rt_dqn_destroy": (i, [_P]),
+        "rt_dqn_forward": (i, [_P, _P, _FP, i, _FP]),
+        "rt_dqn_sample": (i, [_P, _P, ctypes.c_uint64, _FP, _FP, _IP, _UP, i, i, i, _FP, _FP, _IP]),
+        "rt_render_dqn": (i, [_P, _P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i,
+                              i, i, _FP, _U64P]),
+        "rt_render_dqn_tiles_device": (i, [_P, _P, _P, ctypes.POINTER(RtCamera),
+                                           ctypes.POINTER(RtParams), _IP, i, i, _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

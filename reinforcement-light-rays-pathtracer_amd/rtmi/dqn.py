@@ -1,0 +1,135 @@
+"""DQN Q-value network (BASELINE config 4) on top of the C ABI.
+
+  read_dynet(path)        the reference's DyNet text models (Radiance_Map_Data/*.model),
+                          via rt_dynet_read; W row-major [out][in]
+  synthetic_weights(...)  seeded He-normal weights for scenes whose trained model the
+                          reference does not ship (archway: 918 inputs)
+  Dqn(ctx, nn_vertices, weights)   device network (rt_dqn_create)
+  forward / sample / render / render_tiles_device
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ._lib import check, lib
+from .api import Context, Scene, _fp, _ip
+
+HIDDEN = (200, 300, 200)  # NN_Builders/dq_network.cu:14-17
+ACTIONS = 144             # GRID_RESOLUTION^2
+
+
+def read_dynet(path: str) -> List[np.ndarray]:
+    """Parameters of a DyNet TextFileSaver model in file order (row-major)."""
+    L = lib()
+    n_params, n_values = ctypes.c_int(0), ctypes.c_int64(0)
+    check(L.rt_dynet_read(path.encode(), 0, None, None, None, ctypes.byref(n_params),
+                          ctypes.byref(n_values)))
+    rows = np.zeros(n_params.value, np.int32)
+    cols = np.zeros(n_params.value, np.int32)
+    vals = np.zeros(n_values.value, np.float32)
+    check(L.rt_dynet_read(path.encode(), n_params.value, _ip(rows), _ip(cols), _fp(vals),
+                          ctypes.byref(n_params), ctypes.byref(n_values)))
+    out, off = [], 0
+    for r, c in zip(rows, cols):
+        n = int(r) * int(c)
+        a = vals[off:off + n].reshape(int(r), int(c))
+        out.append(a[:, 0].copy() if c == 1 else a.copy())
+        off += n
+    return out
+
+
+def split_layers(params: Sequence[np.ndarray]) -> Tuple[list, list]:
+    """[W1, b1, ..., W4, b4] -> ([W1..W4], [b1..b4])"""
+    if len(params) != 8:
+        raise ValueError(f"expected 8 parameters (4 affine layers), got {len(params)}")
+    return [np.ascontiguousarray(params[i], np.float32) for i in (0, 2, 4, 6)], \
+           [np.ascontiguousarray(params[i], np.float32).ravel() for i in (1, 3, 5, 7)]
+
+
+def synthetic_weights(n_in: int, seed: int = 1984, hidden=HIDDEN, n_out: int = ACTIONS,
+                      bias: float = 0.05) -> Tuple[list, list]:
+    """He-normal (std sqrt(2/fan_in)) weights from numpy's PCG64 seeded with `seed`, constant
+    positive biases: a stand-in for models the reference does not ship."""
+    rng = np.random.default_rng(seed)
+    dims = [n_in, *hidden, n_out]
+    W = [(rng.standard_normal((dims[i + 1], dims[i])) * np.sqrt(2.0 / dims[i])).astype(np.float32)
+         for i in range(4)]
+    b = [np.full(dims[i + 1], bias, np.float32) for i in range(4)]
+    return W, b
+
+
+class Dqn:
+    def __init__(self, ctx: Context, nn_vertices: np.ndarray, W: Sequence[np.ndarray],
+                 b: Sequence[np.ndarray]):
+        self.ctx = ctx
+        self.nn_vertices = np.ascontiguousarray(nn_vertices, np.float32).ravel()
+        self.W = [np.ascontiguousarray(w, np.float32) for w in W]
+        self.b = [np.ascontiguousarray(x, np.float32).ravel() for x in b]
+        self.n_in = int(self.W[0].shape[1])
+        if self.nn_vertices.size != self.n_in:
+            raise ValueError(f"network has {self.n_in} inputs, scene has {self.nn_vertices.size}")
+        hidden = np.array([w.shape[0] for w in self.W[:3]], np.int32)
+        Wp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(w) for w in self.W])
+        bp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(x) for x in self.b])
+        self._h = ctypes.c_void_p()
+        check(lib().rt_dqn_create(ctx.handle, _fp(self.nn_vertices), self.n_in, _ip(hidden),
+                                  int(self.W[3].shape[0]), Wp, bp, ctypes.byref(self._h)))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def forward(self, loc: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(loc, np.float32).reshape(-1, 3)
+        q = np.zeros((x.shape[0], ACTIONS), np.float32)
+        check(lib().rt_dqn_forward(self.ctx.handle, self._h, _fp(x), x.shape[0], _fp(q)))
+        return q
+
+    def close(self):
+        if self._h:
+            lib().rt_dqn_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def sample(ctx: Context, scene: Scene, seed: int, q: np.ndarray, loc: np.ndarray, tri: np.ndarray,
+           pix: np.ndarray, sample_idx: int, bounce: int, tp: np.ndarray):
+    """Importance-sample directions from Q (rt_dqn_sample).  Returns (q*cos, tp, dir, action)."""
+    q = np.ascontiguousarray(q, np.float32).copy()
+    loc = np.ascontiguousarray(loc, np.float32)
+    tri = np.ascontiguousarray(tri, np.int32)
+    pix = np.ascontiguousarray(pix, np.uint32)
+    tp = np.ascontiguousarray(tp, np.float32).copy()
+    n = q.shape[0]
+    d = np.zeros((n, 3), np.float32)
+    a = np.zeros(n, np.int32)
+    check(lib().rt_dqn_sample(ctx.handle, scene.handle, seed, _fp(q), _fp(loc), _ip(tri),
+                              pix.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), n, sample_idx,
+                              bounce, _fp(tp), _fp(d), _ip(a)))
+    return q, tp, d, a
+
+
+def render(ctx: Context, scene: Scene, dqn: Dqn, cam, params, rect=None):
+    x0, y0, w, h = rect if rect is not None else (0, 0, params.width, params.height)
+    out = np.zeros((h, w, 3), np.float32)
+    casts = ctypes.c_uint64(0)
+    check(lib().rt_render_dqn(ctx.handle, scene.handle, dqn.handle, ctypes.byref(cam),
+                              ctypes.byref(params), x0, y0, w, h, _fp(out), ctypes.byref(casts)))
+    return out, int(casts.value)
+
+
+def render_tiles_device(ctx: Context, scene: Scene, dqn: Dqn, cam, params, tiles: np.ndarray,
+                        tile_size: int, out_ptr: int, casts_ptr: int, stream: int) -> None:
+    t = np.ascontiguousarray(tiles, np.int32).reshape(-1, 2)
+    check(lib().rt_render_dqn_tiles_device(ctx.handle, scene.handle, dqn.handle, ctypes.byref(cam),
+                                           ctypes.byref(params), _ip(t), t.shape[0], tile_size,
+                                           ctypes.c_void_p(out_ptr), ctypes.c_void_p(casts_ptr),
+                                           ctypes.c_void_p(stream)))

@@ -1,0 +1,162 @@
+"""DQN Q-value path (BASELINE config 4): DyNet reader, forward pass, Q-weighted
+sampling, wavefront render.
+
+Parity levels:
+  * reader, sampler: bit-exact with the oracle (same Q in -> same direction, pdf, action)
+  * forward: bf16 MFMA vs the oracle's bf16-emulating forward (same operand and
+    activation rounding, exact accumulation): max |dq| <= 2e-2 * max|q|, mean <= 2e-3 * mean|q|;
+    vs the fp32 forward (the reference's DyNet arithmetic): mean <= 3e-2 * mean|q|
+  * render: statistical (a Q perturbation can flip one sampled cell and change a path):
+    MAPE(gpu, oracle) must not exceed the oracle's own seed-to-seed MAPE.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS
+
+DOOR_MODEL = os.path.join(MODELS, "door_room_12_12.model")
+
+
+def door(rtmi_mod):
+    return rtmi_mod.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+
+
+def trained(rtmi_mod):
+    return rtmi_mod.dqn.split_layers(rtmi_mod.dqn.read_dynet(DOOR_MODEL))
+
+
+def room_points(geom, n, seed):
+    """random points on the room's surfaces (where Q is evaluated) + their triangles"""
+    rng = np.random.default_rng(seed)
+    tri = rng.integers(0, geom.n_surf, n)
+    v = geom.tri.reshape(-1, 3, 3)[tri]
+    a, b = rng.random((2, n, 1), dtype=np.float32)
+    flip = (a + b) > 1
+    a[flip], b[flip] = 1 - a[flip], 1 - b[flip]
+    p = v[:, 0] + a * (v[:, 1] - v[:, 0]) + b * (v[:, 2] - v[:, 0])
+    return p.astype(np.float32), tri.astype(np.int32)
+
+
+# ---------------------------------------------------------------- CPU ----------
+
+def test_dynet_reader_product_equals_oracle(rtmi_mod, oracle_mod):
+    a = rtmi_mod.dqn.read_dynet(DOOR_MODEL)
+    b = oracle_mod.read_dynet(DOOR_MODEL)
+    assert [x.shape for x in a] == [(200, 342), (200,), (300, 200), (300,), (200, 300), (200,),
+                                    (144, 200), (144,)]
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_oracle_forward_trained_door_room(rtmi_mod, oracle_mod):
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    p, _ = room_points(g, 64, 1)
+    q = oracle_mod.dqn_forward(W, b, g.nn_vertices, p)
+    assert q.shape == (64, 144) and np.all(q >= 0)           # ReLU output layer
+    assert np.mean(q.sum(axis=1) > 0) > 0.9                  # non-degenerate distributions
+    qb = oracle_mod.dqn_forward(W, b, g.nn_vertices, p, bf16=True)
+    assert np.mean(np.abs(qb - q)) <= 3e-2 * np.mean(np.abs(q))
+
+
+def test_oracle_sampler_properties(rtmi_mod, oracle_mod):
+    g = door(rtmi_mod)
+    n = 512
+    p, tri = room_points(g, n, 2)
+    q = np.zeros((n, 144), np.float32)
+    q[:, 37] = 1.0  # all mass in one cell
+    pix = np.arange(n, dtype=np.uint32)
+    qc, tp, d, act = oracle_mod.dqn_sample(g.all_triangles(), q, p, tri, pix, 0, 1, 1984,
+                                           np.ones((n, 3), np.float32))
+    assert np.all(act == 37)
+    assert np.allclose(np.linalg.norm(d, axis=1), 1.0, atol=1e-5)
+    nrm = oracle_mod.normals(g.all_triangles())[tri]
+    cos = np.sum(nrm * d, axis=1)
+    assert np.all(cos > -1e-6)
+    # pdf = (1/2pi) * 144 for a one-cell distribution: tp = cos / pdf
+    assert np.allclose(tp[:, 0], cos * (2 * np.pi) / 144, rtol=1e-5, atol=1e-7)
+    # all-zero Q: no cell, direction zero, throughput untouched (the reference's miss)
+    _, tp0, d0, act0 = oracle_mod.dqn_sample(g.all_triangles(), np.zeros((4, 144), np.float32), p[:4],
+                                             tri[:4], pix[:4], 0, 1, 1984, np.ones((4, 3), np.float32))
+    assert np.all(act0 == -1) and np.all(d0 == 0) and np.all(tp0 == 1)
+
+
+# ---------------------------------------------------------------- GPU ----------
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["door_room", "archway"])
+def test_forward_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx, kind):
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, f"{kind}.obj"), kind)
+    W, b = trained(rtmi_mod) if kind == "door_room" else rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    pts, _ = room_points(g, 777, 3)  # not a multiple of the 64-row tile
+    with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        q = net.forward(pts)
+    qe = oracle_mod.dqn_forward(W, b, g.nn_vertices, pts, bf16=True)
+    qf = oracle_mod.dqn_forward(W, b, g.nn_vertices, pts, bf16=False)
+    err = np.abs(q - qe)
+    assert err.max() <= 2e-2 * np.abs(qe).max() + 1e-6, err.max()
+    assert err.mean() <= 2e-3 * np.abs(qe).mean() + 1e-7, err.mean()
+    assert np.abs(q - qf).mean() <= 3e-2 * np.abs(qf).mean()
+
+
+@pytest.mark.gpu
+def test_sampler_bit_exact(rtmi_mod, oracle_mod, gpu_ctx):
+    g = door(rtmi_mod)
+    n = 2000
+    pts, tri = room_points(g, n, 4)
+    rng = np.random.default_rng(5)
+    q = rng.random((n, 144), dtype=np.float32) * (rng.random((n, 144)) < 0.3)
+    q[:3] = 0.0  # no cell selectable
+    pix = rng.integers(0, 1 << 20, n).astype(np.uint32)
+    tp = rng.random((n, 3), dtype=np.float32)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        gq, gtp, gd, ga = rtmi_mod.dqn.sample(gpu_ctx, sc, 1984, q, pts, tri, pix, 3, 2, tp)
+    oq, otp, od, oa = oracle_mod.dqn_sample(g.all_triangles(), q, pts, tri, pix, 3, 2, 1984, tp)
+    assert np.array_equal(ga, oa)
+    assert np.array_equal(gq.view(np.uint32), oq.view(np.uint32))
+    assert np.array_equal(gd.view(np.uint32), od.view(np.uint32))
+    assert np.array_equal(gtp.view(np.uint32), otp.view(np.uint32))
+    assert np.all(ga[:3] == -1)
+
+
+@pytest.mark.gpu
+def test_dqn_render_statistical(rtmi_mod, oracle_mod, gpu_ctx):
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16, max_bounces=20)
+    rect = (48, 48, 32, 32)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        img, casts = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+        img2, casts2 = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+    assert np.array_equal(img, img2) and casts == casts2  # deterministic
+    ocam = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    ref, rc = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p), rect, bf16=True)
+    p2 = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16, max_bounces=20, seed=7)
+    alt, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p2), rect, bf16=True)
+    noise = rtmi_mod.metrics.mape_f(ref, alt)
+    m = rtmi_mod.metrics.mape_f(ref, img)
+    assert m <= noise, (m, noise)
+    assert abs(casts - rc) <= 0.05 * rc
+    assert img.mean() > 0
+
+
+@pytest.mark.gpu
+def test_dqn_tiles_equal_rect(rtmi_mod, gpu_ctx):
+    torch = pytest.importorskip("torch")
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=4, max_bounces=12)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        full, _ = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p)
+        tiles = rtmi_mod.tiles.tile_origins(64, 64, 32)
+        out = torch.zeros((len(tiles), 32, 32, 3), dtype=torch.float32, device="cuda")
+        casts = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rtmi_mod.dqn.render_tiles_device(gpu_ctx, sc, net, cam, p, tiles, 32, out.data_ptr(),
+                                         casts.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+    img = rtmi_mod.tiles.assemble(out.cpu().numpy()[None], 64, 64, 32, 1)
+    assert np.array_equal(img, full)
