@@ -171,6 +171,9 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
 int rt_dqn_destroy(rt_dqn* dqn);
 /* DQNetwork::network_inference on n ray positions (host arrays): q = n x 144. */
 int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc /* n x 3 */, int n, float* q);
+/* Same on device buffers, asynchronous on `stream`. */
+int rt_dqn_forward_device(rt_ctx* ctx, const rt_dqn* dqn, const float* d_loc, int n, float* d_q,
+                          void* stream);
 /* importance_sample_direction (nn_rendering_helpers.cu:391-489) for n rays given their Q
  * values (host arrays; q is overwritten with Q*cos as in the reference).  tri: surface the
  * ray sits on; pix: global pixel id (RNG key); tp updated in place; action -1 = none. */

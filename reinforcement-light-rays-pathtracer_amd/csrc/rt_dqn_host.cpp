@@ -213,6 +213,15 @@ int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc, int n, floa
     return RT_OK;
 }
 
+int rt_dqn_forward_device(rt_ctx* ctx, const rt_dqn* dqn, const float* d_loc, int n, float* d_q,
+                          void* stream) {
+    if (!ctx || !dqn || (n > 0 && (!d_loc || !d_q))) return err(RT_E_INVALID, "NULL argument");
+    if (n < 0) return err(RT_E_INVALID, "n < 0");
+    RT_HIPE(hipSetDevice(rt::ctx_device(ctx)));
+    RT_HIPE(rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, (hipStream_t)stream));
+    return RT_OK;
+}
+
 int rt_dqn_sample(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float* q, const float* loc,
                   const int32_t* tri, const uint32_t* pix, int n, int sample, int bounce, float* tp,
                   float* dir_out, int32_t* action) {

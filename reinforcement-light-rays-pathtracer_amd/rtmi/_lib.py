@@ -36,7 +36,8 @@ EXPORTS = (
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
     "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
     "rt_pack_argb", "rt_save_bmp", "rt_selftest",
-    "rt_dynet_read", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_sample",
+    "rt_dynet_read", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_forward_device",
+    "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
 )
 
@@ -100,6 +101,7 @@ def _declare(lib):
                               ctypes.POINTER(_P)]),
         "rt_dqn_destroy": (i, [_P]),
         "rt_dqn_forward": (i, [_P, _P, _FP, i, _FP]),
+        "rt_dqn_forward_device": (i, [_P, _P, _P, i, _P, _P]),
         "rt_dqn_sample": (i, [_P, _P, ctypes.c_uint64, _FP, _FP, _IP, _UP, i, i, i, _FP, _FP, _IP]),
         "rt_render_dqn": (i, [_P, _P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i,
                               i, i, _FP, _U64P]),
@@ -107,6 +109,8 @@ def _declare(lib):
                                            ctypes.POINTER(RtParams), _IP, i, i, _P, _P, _P]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name):  # an older A/B variant build; EXPORTS is checked by tests
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

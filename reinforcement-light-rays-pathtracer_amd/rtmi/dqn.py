@@ -88,6 +88,14 @@ class Dqn:
         check(lib().rt_dqn_forward(self.ctx.handle, self._h, _fp(x), x.shape[0], _fp(q)))
         return q
 
+    def forward_device(self, loc_ptr: int, n: int, q_ptr: int, stream: int = 0) -> None:
+        check(lib().rt_dqn_forward_device(self.ctx.handle, self._h, ctypes.c_void_p(loc_ptr), n,
+                                          ctypes.c_void_p(q_ptr), ctypes.c_void_p(stream)))
+
+    def flops_per_ray(self) -> int:
+        """2 * sum(in*out) of the four layers (unpadded)"""
+        return int(2 * sum(w.shape[0] * w.shape[1] for w in self.W))
+
     def close(self):
         if self._h:
             lib().rt_dqn_destroy(self._h)
