@@ -191,6 +191,45 @@ int rt_render_dqn_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_dqn*
                                int n_tiles, int tile_size, float* d_out, uint64_t* d_casts,
                                void* stream);
 
+/* ---- Expected-SARSA radiance volumes (BASELINE config 3) ------------------ */
+typedef struct rt_sarsa rt_sarsa;
+
+/* RadianceMap::RadianceMap (GPU/radiance_volumes/radiance_map.cu:8-55): floor(area/0.001)
+ * radiance volumes per surface, placed by rejection point picking (Philox stream of `seed`
+ * in place of rand()), each with Q = 100/144 per sector, CDF k/144 and the irradiance of
+ * initialise_radiance_grid (radiance_volume.cu:46-89); the KD tree of radiance_tree.cu in
+ * its array form.  The map lives on the context's device. */
+int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa** out);
+int rt_sarsa_destroy(rt_sarsa* sarsa);
+/* sizes: volumes, KD array elements, frames rendered so far (any pointer may be NULL) */
+int rt_sarsa_info(const rt_sarsa* sarsa, int32_t* n_volumes, int32_t* n_nodes, uint32_t* frames);
+/* host copies: pos n x 3, normal n x 3, surface index n, KD array n_nodes x 12 words
+ * {dim, leaf, left, right (int32), data, px, py, pz, nx, ny, nz (float), vol (int32)} */
+int rt_sarsa_volumes(const rt_sarsa* sarsa, float* pos, float* normal, int32_t* surface,
+                     float* kd_nodes);
+/* Q-table (radiance_grid), CDF (radiance_distribution), visits (n x 144, sector x*12+y) and
+ * irradiance_accum (n) after the last applied frame; NULL pointers are skipped. */
+int rt_sarsa_read(const rt_sarsa* sarsa, float* q, float* cdf, uint32_t* visits,
+                  float* irradiance);
+/* RadianceMap::find_closest_radiance_volume_iterative (radiance_map.cu:149-203), n queries. */
+int rt_sarsa_nearest(rt_ctx* ctx, const rt_sarsa* sarsa, const float* pos, const float* normal,
+                     int n, int32_t* out);
+/* draw_reinforcement_path_tracing + update_radiance_volume_distributions per frame
+ * (reinforcement_path_tracing.cu:6-120, GPU/main.cu:296-350), GPU-engine preset: `frames`
+ * frames of params->spp samples, each frame learning from the previous frame's Q-table;
+ * out_rgb = the last frame (W x H x 3), out_ray_casts = casts of all frames. */
+int rt_render_sarsa(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* sarsa, const rt_camera* cam,
+                    const rt_params* params, int frames, float* out_rgb, uint64_t* out_ray_casts);
+/* One frame over a tile list into device memory (stream-ordered).  apply = 0 leaves the
+ * frame's TD sums in the map's accumulators (rt_sarsa_td_device: int64 fixed-point sums,
+ * uint32 counts, n x 144 each) for a cross-GPU sum before rt_sarsa_apply. */
+int rt_render_sarsa_tiles_device(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* sarsa,
+                                 const rt_camera* cam, const rt_params* params,
+                                 const int32_t* tiles, int n_tiles, int tile_size, float* d_out,
+                                 uint64_t* d_casts, int apply, void* stream);
+int rt_sarsa_td_device(rt_sarsa* sarsa, void** d_sum, void** d_count, int64_t* n_entries);
+int rt_sarsa_apply(rt_sarsa* sarsa, void* stream);
+
 /* Device self-tests of numeric building blocks (no reference counterpart).
  * RT_SELFTEST_RCP: the kernels' correctly-rounded reciprocal vs IEEE 1.0f/x over
  * all 2^32 floats; result[0] = mismatches, result[1] = first mismatching bits. */

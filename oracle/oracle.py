@@ -243,3 +243,75 @@ def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False):
                      int(bf16), ctypes.byref(cam), ctypes.byref(params), x0, y0, w, h, _f(out),
                      ctypes.byref(casts))
     return out, int(casts.value)
+
+
+KD_DTYPE = np.dtype([("dim", "<i4"), ("leaf", "<i4"), ("left", "<i4"), ("right", "<i4"), ("data", "<f4"),
+                     ("px", "<f4"), ("py", "<f4"), ("pz", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                     ("vol", "<i4")])
+
+
+class Sarsa:
+    """Expected-SARSA radiance map of the restatement (orc_sarsa_*)."""
+
+    def __init__(self, geom, seed: int):
+        L = lib()
+        VP = ctypes.c_void_p
+        L.orc_sarsa_create.restype = VP
+        L.orc_sarsa_create.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.c_uint64]
+        L.orc_sarsa_destroy.argtypes = [VP]
+        L.orc_sarsa_info.argtypes = [VP, _IP, _IP]
+        L.orc_sarsa_volumes.argtypes = [VP, _FP, _FP, _IP, VP]
+        L.orc_sarsa_read.argtypes = [VP, _FP, _FP, ctypes.POINTER(ctypes.c_uint32), _FP]
+        L.orc_sarsa_nearest.argtypes = [VP, _FP, _FP, ctypes.c_int, _IP]
+        L.orc_render_sarsa.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
+                                       _FP, ctypes.POINTER(ctypes.c_uint64)]
+        get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
+        self._keep = [np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32),
+                      np.ascontiguousarray(get("albedo"), np.float32),
+                      np.ascontiguousarray(get("emission"), np.float32),
+                      np.ascontiguousarray(get("light_group"), np.int32)]
+        tri, alb, em, grp = self._keep
+        self._L = L
+        self._h = L.orc_sarsa_create(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp),
+                                     get("light").shape[0], seed)
+        nv, nk = ctypes.c_int32(0), ctypes.c_int32(0)
+        L.orc_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk))
+        self.n_volumes, self.n_nodes = nv.value, nk.value
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orc_sarsa_destroy(self._h)
+            self._h = None
+
+    def volumes(self):
+        n = self.n_volumes
+        pos = np.zeros((n, 3), np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        surf = np.zeros(n, np.int32)
+        kd = np.zeros(self.n_nodes, KD_DTYPE)
+        self._L.orc_sarsa_volumes(self._h, _f(pos), _f(nrm), _i(surf), kd.ctypes.data_as(ctypes.c_void_p))
+        return pos, nrm, surf, kd
+
+    def read(self):
+        n = self.n_volumes
+        q = np.zeros((n, 144), np.float32)
+        cdf = np.zeros((n, 144), np.float32)
+        vis = np.zeros((n, 144), np.uint32)
+        acc = np.zeros(n, np.float32)
+        self._L.orc_sarsa_read(self._h, _f(q), _f(cdf), vis.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                               _f(acc))
+        return q, cdf, vis, acc
+
+    def nearest(self, pos, nrm):
+        p = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        n_ = np.ascontiguousarray(nrm, np.float32).reshape(-1, 3)
+        out = np.zeros(p.shape[0], np.int32)
+        self._L.orc_sarsa_nearest(self._h, _f(p), _f(n_), p.shape[0], _i(out))
+        return out
+
+    def render(self, cam: OrcCamera, params: OrcParams, frames: int = 1):
+        out = np.zeros((params.height, params.width, 3), np.float32)
+        casts = ctypes.c_uint64(0)
+        self._L.orc_render_sarsa(self._h, ctypes.byref(cam), ctypes.byref(params), frames, _f(out),
+                                 ctypes.byref(casts))
+        return out, int(casts.value)

@@ -850,3 +850,490 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
     if (out_casts) *out_casts = total_casts;
     return 0;
 }
+
+/* ================================================================== */
+/* Expected-SARSA path (BASELINE config 3)                             */
+/* ================================================================== */
+/*
+ * Restates (GPU_Rendering_Engine/Source/):
+ *   radiance volume count / placement  radiance_volumes/radiance_map.cu:57-84,
+ *                                      objects/triangle.cu:17-45 (area; rejection point picking)
+ *   initial Q / CDF / irradiance       radiance_volumes/radiance_volume.cu:46-89
+ *   KD tree + array form               radiance_volumes/radiance_tree.cu:10-246 (std::sort on
+ *                                      position[dim]: oracle/orc_sort.cpp calls the same std::sort)
+ *   nearest volume                     radiance_volumes/radiance_map.cu:149-203
+ *   sector sampling                    radiance_volume.cu:191-244, radiance_map.cu:90-106
+ *   TD target                          radiance_map.cu:110-146, radiance_volume.cu:304-307
+ *   TD update + irradiance             radiance_volume.cu:93-112, 282-301
+ *   CDF rebuild                        radiance_volume.cu:148-188
+ *   render loop                        path_tracing/reinforcement_path_tracing.cu:26-120
+ * Frame-synchronous TD: a frame reads the previous frame's
+ * Q / CDF / irradiance; its TD targets are summed per (volume, sector) in
+ * fixed point (round(target * 2^32), int64) with counts, then folded as the
+ * running mean of alpha = 1/(1 + visits), clamped at 0.8/144.
+ * RNG: volume placement counter (volume, attempt, 0xFFFF0001, 0), u01 of words
+ * 0,1; sampling at bounce i counter (pixel, frame*spp + sample, 1+i, 0): words
+ * 0,1,2 = r (sector), rx, ry (uniform fallback: words 0,1).
+ */
+void orc_kd_sort(int32_t *v, int n, const float *pos4, int dim); /* orc_sort.cpp */
+
+typedef struct {
+    int dim, leaf, left, right;
+    float data, px, py, pz, nx, ny, nz;
+    int vol;
+} orc_kd;
+
+typedef struct {
+    int n_vol, n_kd, kd_cap;
+    float *pos;     /* [n][4] */
+    float *nrm;     /* [n][3] */
+    int32_t *surf;  /* [n] */
+    float *frame;   /* [n][9] N T B */
+    float *brdf;    /* [n] */
+    float *cc, *ck; /* [n*144] cos of cell centre / corner directions */
+    float *Q, *cdf, *accum;
+    uint32_t *visits, *cnt;
+    int64_t *sum;
+    orc_kd *kd;
+    float *tri_lum;
+    uint32_t frames;
+    uint64_t seed;
+    /* scene (copied) */
+    int n_surf, n_light;
+    float *tri, *albedo, *emission, *normal;
+    int32_t *light_group;
+} orc_sarsa;
+
+static float lum3(const float *c) {
+    float mx = c[0] > c[1] ? c[0] : c[1];
+    mx = mx > c[2] ? mx : c[2];
+    float mn = c[0] < c[1] ? c[0] : c[1];
+    mn = mn < c[2] ? mn : c[2];
+    return 0.5f * (mx + mn);
+}
+
+/* Triangle::compute_area: float lengths/cosine, 1 - pow(cos,2) and sqrt in double */
+static float tri_area(const float *v) {
+    v3 a = mk(v[3] - v[0], v[4] - v[1], v[5] - v[2]);
+    v3 b = mk(v[6] - v[0], v[7] - v[1], v[8] - v[2]);
+    float e = sqrtf(dot3(a, a)) * sqrtf(dot3(b, b));
+    float c = dot3(a, b) / e;
+    float s = (float)sqrt(1.0 - (double)c * (double)c);
+    return 0.5f * e * s;
+}
+
+typedef struct { int dim; float median; int vol, left, right; } kd_sub;
+
+static int kd_build(orc_sarsa *m, kd_sub *subs, int *n_subs, int32_t *v, int n, int dim) {
+    int me = (*n_subs)++;
+    subs[me].dim = dim;
+    subs[me].vol = -1;
+    subs[me].left = subs[me].right = -1;
+    if (n == 1) {
+        subs[me].median = m->pos[4 * v[0] + dim];
+        subs[me].vol = v[0];
+        return me;
+    }
+    orc_kd_sort(v, n, m->pos, dim);
+    int mi;
+    if (n % 2 == 0) {
+        mi = n / 2 - 1;
+        subs[me].median = (m->pos[4 * v[mi] + dim] + m->pos[4 * v[mi + 1] + dim]) / 2;
+    } else {
+        mi = n / 2;
+        subs[me].median = m->pos[4 * v[mi] + dim];
+    }
+    int l = kd_build(m, subs, n_subs, v, mi + 1, (dim + 1) % 3);
+    int r = kd_build(m, subs, n_subs, v + mi + 1, n - mi - 1, (dim + 1) % 3);
+    subs[me].left = l;
+    subs[me].right = r;
+    return me;
+}
+
+/* traverse_and_insert: children appended as a pair, left subtree first */
+static void kd_insert(orc_sarsa *m, const kd_sub *subs, int s, int slot) {
+    int last = m->n_kd - 1;
+    const kd_sub *u = &subs[s];
+    if (u->vol >= 0) {
+        orc_kd *e = &m->kd[slot];
+        memset(e, 0, sizeof(*e));
+        e->dim = u->dim; e->leaf = 1; e->data = (float)u->vol; e->vol = u->vol;
+        e->px = m->pos[4 * u->vol]; e->py = m->pos[4 * u->vol + 1]; e->pz = m->pos[4 * u->vol + 2];
+        e->nx = m->nrm[3 * u->vol]; e->ny = m->nrm[3 * u->vol + 1]; e->nz = m->nrm[3 * u->vol + 2];
+        return;
+    }
+    m->kd[slot].left = last + 1;
+    m->kd[slot].right = last + 2;
+    orc_kd c;
+    memset(&c, 0, sizeof(c));
+    c.dim = (u->dim + 1) % 3;
+    c.data = subs[u->left].median;
+    m->kd[m->n_kd++] = c;
+    c.data = subs[u->right].median;
+    m->kd[m->n_kd++] = c;
+    kd_insert(m, subs, u->left, last + 1);
+    kd_insert(m, subs, u->right, last + 2);
+}
+
+ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n_surf, const float *emission,
+                                    const int32_t *light_group, int n_light, uint64_t seed) {
+    orc_sarsa *m = (orc_sarsa *)calloc(1, sizeof(orc_sarsa));
+    int nt = n_surf + n_light;
+    m->n_surf = n_surf; m->n_light = n_light; m->seed = seed;
+    m->tri = (float *)malloc(sizeof(float) * 9 * (size_t)(nt + 1));
+    memcpy(m->tri, tri, sizeof(float) * 9 * (size_t)nt);
+    m->albedo = (float *)malloc(sizeof(float) * 3 * (size_t)(n_surf + 1));
+    memcpy(m->albedo, albedo, sizeof(float) * 3 * (size_t)n_surf);
+    m->emission = (float *)malloc(sizeof(float) * 3 * (size_t)(n_light + 1));
+    memcpy(m->emission, emission, sizeof(float) * 3 * (size_t)n_light);
+    m->light_group = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n_light + 1));
+    memcpy(m->light_group, light_group, sizeof(int32_t) * (size_t)n_light);
+    m->normal = (float *)malloc(sizeof(float) * 3 * (size_t)(nt + 1));
+    orc_triangle_normals(m->tri, nt, m->normal);
+    /* count, then place */
+    int n = 0;
+    for (int j = 0; j < n_surf; j++) n += (int)floorf(tri_area(tri + 9 * j) / 0.001f);
+    m->n_vol = n;
+    m->pos = (float *)malloc(sizeof(float) * 4 * (size_t)(n + 1));
+    m->nrm = (float *)malloc(sizeof(float) * 3 * (size_t)(n + 1));
+    m->surf = (int32_t *)malloc(sizeof(int32_t) * (size_t)(n + 1));
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    int x = 0;
+    for (int j = 0; j < n_surf; j++) {
+        const float *v = tri + 9 * j;
+        int cnt = (int)floorf(tri_area(v) / 0.001f);
+        for (int i = 0; i < cnt; i++, x++) {
+            float a1, a2;
+            uint32_t attempt = 0;
+            do {
+                uint32_t ctr[4] = {(uint32_t)x, attempt++, 0xFFFF0001u, 0u}, o[4];
+                orc_philox4x32_10(ctr, key, o);
+                a1 = u01(o[0]);
+                a2 = u01(o[1]);
+            } while (a1 + a2 > 1.0f);
+            for (int c = 0; c < 3; c++)
+                m->pos[4 * x + c] = (v[c] + a1 * (v[3 + c] - v[c])) + a2 * (v[6 + c] - v[c]);
+            m->pos[4 * x + 3] = 1.0f;
+            for (int c = 0; c < 3; c++) m->nrm[3 * x + c] = m->normal[3 * j + c];
+            m->surf[x] = j;
+        }
+    }
+    size_t nS = (size_t)n * 144 + 1;
+    m->frame = (float *)malloc(sizeof(float) * 9 * (size_t)(n + 1));
+    m->brdf = (float *)malloc(sizeof(float) * (size_t)(n + 1));
+    m->cc = (float *)malloc(sizeof(float) * nS);
+    m->ck = (float *)malloc(sizeof(float) * nS);
+    m->Q = (float *)malloc(sizeof(float) * nS);
+    m->cdf = (float *)malloc(sizeof(float) * nS);
+    m->accum = (float *)malloc(sizeof(float) * (size_t)(n + 1));
+    m->visits = (uint32_t *)calloc(nS, sizeof(uint32_t));
+    m->cnt = (uint32_t *)calloc(nS, sizeof(uint32_t));
+    m->sum = (int64_t *)calloc(nS, sizeof(int64_t));
+    const float Q0 = (1.f / (12.0f * 12.0f)) * 100.f;
+    for (int i = 0; i < n; i++) {
+        v3 N = mk(m->nrm[3 * i], m->nrm[3 * i + 1], m->nrm[3 * i + 2]);
+        v3 P = mk(m->pos[4 * i], m->pos[4 * i + 1], m->pos[4 * i + 2]);
+        v3 T, B;
+        normal_frame(N, &T, &B);
+        float *f = m->frame + 9 * (size_t)i;
+        f[0] = N.x; f[1] = N.y; f[2] = N.z; f[3] = T.x; f[4] = T.y; f[5] = T.z; f[6] = B.x; f[7] = B.y; f[8] = B.z;
+        float lum = lum3(albedo + 3 * m->surf[i]);
+        m->brdf[i] = lum / PI_F;
+        float irr = 0.0f;
+        for (int gx = 0; gx < 12; gx++)
+            for (int gy = 0; gy < 12; gy++) {
+                int k = gx * 12 + gy;
+                size_t at = (size_t)i * 144 + k;
+                m->cc[at] = dot3(grid_dir((float)gx + 0.5f, (float)gy + 0.5f, N, T, B, P), N);
+                m->ck[at] = dot3(grid_dir((float)gx, (float)gy, N, T, B, P), N);
+                m->Q[at] = Q0;
+                m->cdf[at] = (float)k * (1.f / (12.0f * 12.0f));
+                irr = (float)((double)irr + ((double)m->cc[at] * ((double)lum / 3.14159265358979323846)) * (double)Q0);
+            }
+        m->accum[i] = irr;
+    }
+    m->tri_lum = (float *)malloc(sizeof(float) * (size_t)(nt + 1));
+    for (int j = 0; j < n_surf; j++) m->tri_lum[j] = lum3(albedo + 3 * j);
+    for (int j = 0; j < n_light; j++) m->tri_lum[n_surf + j] = lum3(emission + 3 * j);
+    if (n > 0) {
+        int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * (size_t)n);
+        for (int i = 0; i < n; i++) idx[i] = i;
+        kd_sub *subs = (kd_sub *)malloc(sizeof(kd_sub) * (size_t)(2 * n));
+        int n_subs = 0;
+        int root = kd_build(m, subs, &n_subs, idx, n, 0);
+        m->kd = (orc_kd *)calloc((size_t)(2 * n), sizeof(orc_kd));
+        m->kd[0].dim = subs[root].dim;
+        m->kd[0].data = subs[root].median;
+        m->n_kd = 1;
+        kd_insert(m, subs, root, 0);
+        free(subs);
+        free(idx);
+    }
+    return m;
+}
+
+ORC_API void orc_sarsa_destroy(orc_sarsa *m) {
+    if (!m) return;
+    free(m->pos); free(m->nrm); free(m->surf); free(m->frame); free(m->brdf); free(m->cc); free(m->ck);
+    free(m->Q); free(m->cdf); free(m->accum); free(m->visits); free(m->cnt); free(m->sum); free(m->kd);
+    free(m->tri_lum); free(m->tri); free(m->albedo); free(m->emission); free(m->light_group); free(m->normal);
+    free(m);
+}
+
+ORC_API void orc_sarsa_info(const orc_sarsa *m, int32_t *n_vol, int32_t *n_kd) {
+    *n_vol = m->n_vol;
+    *n_kd = m->n_kd;
+}
+
+/* kd_nodes: n_kd x 12 words, the layout of rt_sarsa_volumes */
+ORC_API void orc_sarsa_volumes(const orc_sarsa *m, float *pos, float *nrm, int32_t *surf, void *kd_nodes) {
+    for (int i = 0; i < m->n_vol; i++) {
+        if (pos) memcpy(pos + 3 * i, m->pos + 4 * i, sizeof(float) * 3);
+        if (nrm) memcpy(nrm + 3 * i, m->nrm + 3 * i, sizeof(float) * 3);
+        if (surf) surf[i] = m->surf[i];
+    }
+    if (kd_nodes) memcpy(kd_nodes, m->kd, sizeof(orc_kd) * (size_t)m->n_kd);
+}
+
+ORC_API void orc_sarsa_read(const orc_sarsa *m, float *q, float *cdf, uint32_t *visits, float *accum) {
+    size_t nS = (size_t)m->n_vol * 144;
+    if (q) memcpy(q, m->Q, sizeof(float) * nS);
+    if (cdf) memcpy(cdf, m->cdf, sizeof(float) * nS);
+    if (visits) memcpy(visits, m->visits, sizeof(uint32_t) * nS);
+    if (accum) memcpy(accum, m->accum, sizeof(float) * (size_t)m->n_vol);
+}
+
+static float dist3(float ax, float ay, float az, float bx, float by, float bz) {
+    float x = ax - bx, y = ay - by, z = az - bz;
+    return sqrtf((x * x + y * y) + z * z);
+}
+
+/* find_closest_radiance_volume_iterative */
+static int sarsa_nearest(const orc_sarsa *m, v3 p, v3 nrm) {
+    int best = 0;
+    float best_d = dist3(p.x, p.y, p.z, m->kd[0].px, m->kd[0].py, m->kd[0].pz);
+    int stack[64], sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const orc_kd *e = &m->kd[stack[--sp]];
+        if (e->leaf) {
+            float d = dist3(e->px, e->py, e->pz, p.x, p.y, p.z);
+            if (nrm.x == e->nx && nrm.y == e->ny && nrm.z == e->nz && d < best_d) {
+                best = (int)e->data;
+                best_d = d;
+            }
+        } else {
+            float pc = e->dim == 0 ? p.x : (e->dim == 1 ? p.y : p.z);
+            float delta = pc - e->data;
+            int near_split = (delta * delta) < 0.003f;
+            if (sp + 2 > 64) break;
+            if (delta < 0.0f) {
+                if (near_split) stack[sp++] = e->right;
+                stack[sp++] = e->left;
+            } else {
+                if (near_split) stack[sp++] = e->left;
+                stack[sp++] = e->right;
+            }
+        }
+    }
+    return best;
+}
+
+ORC_API void orc_sarsa_nearest(const orc_sarsa *m, const float *pos, const float *nrm, int n, int32_t *out) {
+    #pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++)
+        out[i] = sarsa_nearest(m, mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]),
+                               mk(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]));
+}
+
+/* sample_direction_from_radiance_distribution: 0 = no sector found */
+static int sarsa_sample(const orc_sarsa *m, int rv, float r, float rx, float ry, int *sector, v3 *dir, float *pdf) {
+    const float *cdf = m->cdf + (size_t)rv * 144;
+    const float RHO = 1.0f / (2.0f * 3.1415926535f);
+    const float GRID_RHO = 1.0f / (12.0f * 12.0f);
+    int found = -1;
+    float dv = 0.0f;
+    if (r <= cdf[0]) {
+        found = 0;
+        dv = cdf[0];
+    } else {
+        int start = 0, end = 143;
+        while (start <= end) {
+            int mid = (end + start) / 2;
+            float mv = cdf[mid], pv = mid > 0 ? cdf[mid - 1] : 0.0f;
+            if (r < mv && pv <= r) { found = mid; dv = mv - pv; break; }
+            else if (mv < r) start = mid + 1;
+            else end = mid - 1;
+        }
+    }
+    if (found < 0) return 0;
+    int sx = found / 12, sy = found - sx * 12;
+    *sector = found;
+    *pdf = RHO * (dv / GRID_RHO);
+    const float *f = m->frame + 9 * (size_t)rv;
+    *dir = grid_dir((float)sx + rx, (float)sy + ry, mk(f[0], f[1], f[2]), mk(f[3], f[4], f[5]), mk(f[6], f[7], f[8]),
+                    mk(m->pos[4 * rv], m->pos[4 * rv + 1], m->pos[4 * rv + 2]));
+    return 1;
+}
+
+static void td_add(orc_sarsa *m, int rv, int sector, float target) {
+    int64_t v = (int64_t)llrintf(target * 4294967296.0f);
+    size_t k = (size_t)rv * 144 + sector;
+    #pragma omp atomic
+    m->sum[k] += v;
+    #pragma omp atomic
+    m->cnt[k] += 1u;
+}
+
+/* path_trace_reinforcement_iterative with the frame-synchronous TD */
+static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t smp, v3 o, v3 d, uint64_t *casts) {
+    orc_scene sc;
+    sc.n_surf = m->n_surf; sc.n_light = m->n_light; sc.tri = m->tri; sc.albedo = m->albedo;
+    sc.emission = m->emission; sc.light_group = m->light_group; sc.normal = m->normal;
+    const float RHO = 1.0f / (2.0f * 3.1415926535f);
+    const float IRR = (2.f * PI_F) / ((float)(12 * 12));
+    v3 tp = mk(1.0f, 1.0f, 1.0f);
+    int cur_rv = -1, cur_sector = -1;
+    float cur_brdf = 0.0f;
+    uint32_t key[2] = {(uint32_t)p->seed, (uint32_t)(p->seed >> 32)};
+    for (int i = 0; i < p->max_bounces; i++) {
+        hit_t h = closest_hit(&sc, o, d, p->t_scale, p->hit_rule);
+        (*casts)++;
+        int is_surf = h.tri >= 0 && h.tri < sc.n_surf;
+        v3 pos = o, nrm = mk(0.0f, 0.0f, 0.0f);
+        if (is_surf) {
+            v3 D = mk(d.x * p->t_scale, d.y * p->t_scale, d.z * p->t_scale);
+            pos = mk(o.x + h.t * D.x, o.y + h.t * D.y, o.z + h.t * D.z);
+            nrm = mk(sc.normal[3 * h.tri], sc.normal[3 * h.tri + 1], sc.normal[3 * h.tri + 2]);
+        }
+        if (i > 0) {
+            if (cur_rv >= 0 && cur_sector >= 0) {
+                float target;
+                int next = -1;
+                if (h.tri < 0) target = cur_brdf * p->env_light;
+                else if (!is_surf) target = cur_brdf * m->tri_lum[h.tri];
+                else {
+                    next = sarsa_nearest(m, pos, nrm);
+                    target = (m->accum[next] * IRR) * cur_brdf;
+                }
+                td_add(m, cur_rv, cur_sector, target);
+                cur_rv = next;
+                cur_sector = -1;
+            }
+        } else if (is_surf) {
+            cur_rv = sarsa_nearest(m, pos, nrm);
+        }
+        if (h.tri < 0) return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
+        if (!is_surf) {
+            const float *e = sc.emission + (size_t)(h.tri - sc.n_surf) * 3;
+            return mk(tp.x * e[0], tp.y * e[1], tp.z * e[2]);
+        }
+        uint32_t ctr[4] = {pix, smp, 1u + (uint32_t)i, 0u}, rn[4];
+        orc_philox4x32_10(ctr, key, rn);
+        v3 sd;
+        float pdf;
+        if (cur_rv < 0) {
+            float ct;
+            sd = sample_dir(nrm, u01(rn[0]), u01(rn[1]), 0, &ct);
+            pdf = RHO;
+        } else if (!sarsa_sample(m, cur_rv, u01(rn[0]), u01(rn[1]), u01(rn[2]), &cur_sector, &sd, &pdf)) {
+            if (i + 1 >= p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
+            (*casts)++; /* the zero direction is traced and misses */
+            return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
+        }
+        const float *al = sc.albedo + (size_t)h.tri * 3;
+        float cos_theta = dot3(nrm, sd);
+        cur_brdf = m->tri_lum[h.tri] / PI_F;
+        tp.x = tp.x * (((al[0] / PI_F) * cos_theta) / pdf);
+        tp.y = tp.y * (((al[1] / PI_F) * cos_theta) / pdf);
+        tp.z = tp.z * (((al[2] / PI_F) * cos_theta) / pdf);
+        o = mk(pos.x + sd.x * 1e-5f, pos.y + sd.y * 1e-5f, pos.z + sd.z * 1e-5f);
+        d = normalize3(sd);
+    }
+    return mk(0.0f, 0.0f, 0.0f);
+}
+
+/* update_radiance_distribution + the frame's TD fold */
+static void sarsa_apply(orc_sarsa *m) {
+    const float thr = (1.f / (12.0f * 12.0f)) * 0.8f;
+    #pragma omp parallel for schedule(static)
+    for (int v = 0; v < m->n_vol; v++) {
+        size_t b = (size_t)v * 144;
+        float brdf = m->brdf[v], accum = m->accum[v];
+        for (int k = 0; k < 144; k++) {
+            uint32_t n = m->cnt[b + k];
+            if (n == 0u) continue;
+            float sum = (float)((double)m->sum[b + k] * 2.3283064365386962890625e-10);
+            uint32_t vis = m->visits[b + k];
+            float q_old = m->Q[b + k];
+            float q_new = (q_old * (float)vis + sum) / (float)(vis + n);
+            q_new = q_new > thr ? q_new : thr;
+            float cc = m->ck[b + k];
+            accum = (accum - ((q_old * cc) * brdf)) + ((q_new * cc) * brdf);
+            m->Q[b + k] = q_new;
+            m->visits[b + k] = vis + n;
+            m->cnt[b + k] = 0u;
+            m->sum[b + k] = 0;
+        }
+        m->accum[v] = accum;
+        float total = 0.0000000001f;
+        for (int k = 0; k < 144; k++) {
+            float t = m->Q[b + k] * m->cc[b + k];
+            t = t > 0.0f ? t : 0.0f;
+            total += t;
+        }
+        float prev = 0.0f;
+        for (int k = 0; k < 144; k++) {
+            float t = m->Q[b + k] * m->cc[b + k];
+            t = t > 0.0f ? t : 0.0f;
+            float rad = t / total + prev;
+            m->cdf[b + k] = rad;
+            prev = rad;
+        }
+    }
+}
+
+/* `frames` frames of the whole width x height image (GPU-engine preset); out_rgb = last frame */
+ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int frames, float *out_rgb,
+                             uint64_t *out_casts) {
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    orc_params pg = *p;
+    pg.preset = 1;
+    uint64_t total = 0;
+    int W = p->width, H = p->height;
+    int S = p->spp_split <= 0 ? 1 : p->spp_split;
+    int per = p->spp / S;
+    for (int f = 0; f < frames; f++) {
+        uint32_t base = m->frames * (uint32_t)p->spp;
+        #pragma omp parallel for schedule(dynamic, 1) reduction(+:total)
+        for (int py = 0; py < H; py++) {
+            for (int px = 0; px < W; px++) {
+                uint32_t pix = (uint32_t)py * (uint32_t)W + (uint32_t)px;
+                v3 acc = mk(0.0f, 0.0f, 0.0f);
+                uint64_t casts = 0;
+                for (int c = 0; c < S; c++) {
+                    v3 part = mk(0.0f, 0.0f, 0.0f);
+                    for (int s = c * per; s < (c + 1) * per; s++) {
+                        float r1, r2;
+                        draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
+                        v3 o, d;
+                        camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                        v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
+                        part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
+                    }
+                    if (c == 0) acc = part;
+                    else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }
+                }
+                float fs = (float)p->spp;
+                float *dst = out_rgb + ((size_t)py * W + px) * 3;
+                dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+                total += casts;
+            }
+        }
+        sarsa_apply(m);
+        m->frames++;
+    }
+    if (out_casts) *out_casts = total;
+    return 0;
+}

@@ -58,12 +58,24 @@ struct rt_scene {
     rt::DeviceScene dev;
     int n_surf = 0, n_light = 0;
     std::vector<float> normals;  // host copy, n_tri x 3
+    std::vector<float> tri;      // host copy, n_tri x 9 (surfaces then lights)
+    std::vector<float> albedo;   // n_surf x 3
+    std::vector<float> emission; // n_light x 3
 };
 
 namespace rt {
 void release_dqn_workspace(const rt_ctx* ctx);
 int ctx_device(const rt_ctx* ctx) { return ctx->device; }
 const DeviceScene& scene_device(const rt_scene* s) { return s->dev; }
+void scene_host(const rt_scene* s, const float** tri, const float** normals, const float** albedo,
+                const float** emission, int* n_surf, int* n_light) {
+    *tri = s->tri.data();
+    *normals = s->normals.data();
+    *albedo = s->albedo.data();
+    *emission = s->emission.data();
+    *n_surf = s->n_surf;
+    *n_light = s->n_light;
+}
 int ensure_blocks_impl(rt_ctx* ctx, const std::vector<BlockDesc>& blocks);
 // Device block list (16x16 pixel blocks) of a tile list, cached per context.
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
@@ -180,6 +192,13 @@ rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const 
 
 }  // namespace
 
+namespace rt {
+// shared with the SARSA host code (rt_sarsa_host.cpp)
+RenderLaunch render_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p) {
+    return make_launch(scene, cam, p);
+}
+}  // namespace rt
+
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
@@ -256,6 +275,15 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     sc->n_surf = n_surf;
     sc->n_light = n_light;
     sc->normals.resize((size_t)n * 3);
+    sc->tri.resize((size_t)n * 9);
+    if (n_surf > 0) {
+        memcpy(sc->tri.data(), tri_v, sizeof(float) * 9 * (size_t)n_surf);
+        sc->albedo.assign(albedo, albedo + 3 * (size_t)n_surf);
+    }
+    if (n_light > 0) {
+        memcpy(sc->tri.data() + 9 * (size_t)n_surf, light_v, sizeof(float) * 9 * (size_t)n_light);
+        sc->emission.assign(emission, emission + 3 * (size_t)n_light);
+    }
     for (int i = 0; i < n; ++i) {
         const bool is_light = i >= n_surf;
         const int j = is_light ? i - n_surf : i;

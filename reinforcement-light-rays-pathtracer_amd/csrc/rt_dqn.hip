@@ -181,59 +181,6 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
     mlp_layer<false, true>(net, 3, bufB, kStrideB, nullptr, 0, locm, q_rows, rows_valid);
 }
 
-// ---------------------------------------------------------------------------
-// Grid cell -> world direction (hemisphere_helpers.cu:95-121 + Chiu's map
-// :123-226), restated in turns: theta from cos = 1 - xx^2,
-// sin = xx*sqrt(2 - xx^2); phi = offset + (yy/xx)/8 turns.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void chiu_map(float x, float y, float* xr, float* yr, float* zr) {
-    x = 2.0f * x - 1.0f;
-    y = 2.0f * y - 1.0f;
-    float xx, yy, off;
-    bool origin = false;
-    if (y > -x) {
-        if (y < x) {
-            xx = x;
-            if (y > 0.0f) { off = 0.0f; yy = y; }
-            else { off = 0.875f; yy = x + y; }
-        } else {
-            xx = y;
-            if (x > 0.0f) { off = 0.125f; yy = y - x; }
-            else { off = 0.25f; yy = -x; }
-        }
-    } else {
-        if (y > x) {
-            xx = -x;
-            if (y > 0.0f) { off = 0.375f; yy = -x - y; }
-            else { off = 0.5f; yy = -y; }
-        } else {
-            xx = -y;
-            if (x > 0.0f) { off = 0.75f; yy = x; }
-            else if (y != 0.0f) { off = 0.625f; yy = x - y; }
-            else { origin = true; xx = 1.0f; yy = 0.0f; off = 0.0f; }
-        }
-    }
-    const float c = 1.0f - xx * xx;
-    const float s = xx * sqrtf(2.0f - xx * xx);
-    const float phi = off + 0.125f * (yy / xx);
-    float sp, cp;
-    sincos_turn(phi, &sp, &cp);
-    *xr = origin ? 0.0f : s * cp;
-    *yr = origin ? 1.0f : c;
-    *zr = origin ? 0.0f : s * sp;
-}
-
-// convert_grid_pos_to_direction_random: map((x+r1)/12, (y+r2)/12), then
-// world = mat4(T, N, B, pos) * (xh, yh, zh, 1) (glm order), dir = normalize(world - pos)
-__device__ __forceinline__ f3 grid_direction(float gx, float gy, f3 N, f3 T, f3 B, f3 pos) {
-    float xh, yh, zh;
-    chiu_map(gx / (float)kDqnGrid, gy / (float)kDqnGrid, &xh, &yh, &zh);
-    const f3 w = make3((T.x * xh + N.x * yh) + (B.x * zh + pos.x * 1.0f),
-                       (T.y * xh + N.y * yh) + (B.y * zh + pos.y * 1.0f),
-                       (T.z * xh + N.z * yh) + (B.z * zh + pos.z * 1.0f));
-    return normalize(make3(w.x - pos.x, w.y - pos.y, w.z - pos.z));
-}
-
 struct SampleOut {
     int action;   // -1: no cell selected (the reference then traces a zero direction: a miss)
     f3 dir;

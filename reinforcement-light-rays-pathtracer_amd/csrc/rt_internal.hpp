@@ -55,6 +55,7 @@ struct RenderLaunch {
     int out_pitch;
     float* out;
     unsigned long long* casts;
+    uint32_t sample_base;  // first RNG sample index (SARSA: frame * spp); 0 elsewhere
 };
 
 // ---- DQN Q-value network (dq_network/fc_layer) and its wavefront renderer ----
@@ -119,6 +120,42 @@ hipError_t launch_dqn_sample_only(const DeviceScene& s, const float* q, const fl
                                   const int32_t* tri, const uint32_t* pix, int n, int sample,
                                   int bounce, uint32_t seed_lo, uint32_t seed_hi, float* tp,
                                   float* dir_out, int32_t* action, hipStream_t stream);
+
+// ---- Expected-SARSA radiance volumes (BASELINE config 3) ----
+// Flattened KD tree of GPU/radiance_volumes/radiance_tree.cuh:19-27 (48 B per node).
+struct KdNode {
+    int dim, leaf, left, right;
+    float data;          // split median (internal) or volume index (leaf, as float like the reference)
+    float px, py, pz;    // leaf position (0 for internal nodes)
+    float nx, ny, nz;    // leaf normal
+    int vol;             // leaf volume index
+};
+
+constexpr int kSarsaSectors = 144;
+
+struct SarsaMap {
+    int n_vol = 0;
+    const float4* vol_pos = nullptr;    // [n] sampled position
+    const float4* vol_frame = nullptr;  // [n*3] N, T, B (create_transformation_matrix)
+    const float* vol_brdf = nullptr;    // [n] luminance/pi of the volume's surface
+    const float* cos_center = nullptr;  // [n*144] cos of the cell-centre directions
+    const float* cos_corner = nullptr;  // [n*144] cos of the cell-corner directions
+    const float* tri_lum = nullptr;     // [n_tri] Material/AreaLight luminance 0.5*(max+min)
+    float* Q = nullptr;                 // [n*144] radiance_grid
+    float* cdf = nullptr;               // [n*144] radiance_distribution
+    uint32_t* visits = nullptr;         // [n*144]
+    float* accum = nullptr;             // [n] irradiance_accum
+    unsigned long long* acc_sum = nullptr;  // [n*144] frame TD targets, fixed point 2^-32
+    uint32_t* acc_cnt = nullptr;            // [n*144] frame TD target count
+    const KdNode* kd = nullptr;
+    int n_kd = 0;
+    float max_dist = 0.003f;            // MAX_DIST (compared with delta^2)
+};
+
+hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
+hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);
+hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float* nrm, int n, int32_t* out,
+                                hipStream_t stream);
 
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, float* out_t, int32_t* out_hit,

@@ -114,5 +114,57 @@ RT_HD void normal_frame(f3 n, f3* T, f3* B) {
 
 constexpr float kPi = 3.14159265358979323846f;  // (float)M_PI
 constexpr float kEps = 1e-5f;                   // EPS / the 0.00001f offsets
+constexpr int kGridRes = 12;                    // GRID_RESOLUTION (GPU/constants/radiance_volumes_settings.h:9)
+
+// Chiu's square -> hemisphere map (GPU/utils/hemisphere_helpers.cu:123-226),
+// restated in turns: cos(theta) = 1 - xx^2, sin(theta) = xx*sqrt(2 - xx^2),
+// phi = offset + (yy/xx)/8 turns (the same angles; no acos/sin/cos of radians).
+RT_HD void chiu_map(float x, float y, float* xr, float* yr, float* zr) {
+    x = 2.0f * x - 1.0f;
+    y = 2.0f * y - 1.0f;
+    float xx, yy, off;
+    bool origin = false;
+    if (y > -x) {
+        if (y < x) {
+            xx = x;
+            if (y > 0.0f) { off = 0.0f; yy = y; }
+            else { off = 0.875f; yy = x + y; }
+        } else {
+            xx = y;
+            if (x > 0.0f) { off = 0.125f; yy = y - x; }
+            else { off = 0.25f; yy = -x; }
+        }
+    } else {
+        if (y > x) {
+            xx = -x;
+            if (y > 0.0f) { off = 0.375f; yy = -x - y; }
+            else { off = 0.5f; yy = -y; }
+        } else {
+            xx = -y;
+            if (x > 0.0f) { off = 0.75f; yy = x; }
+            else if (y != 0.0f) { off = 0.625f; yy = x - y; }
+            else { origin = true; xx = 1.0f; yy = 0.0f; off = 0.0f; }
+        }
+    }
+    const float c = 1.0f - xx * xx;
+    const float s = xx * sqrtf(2.0f - xx * xx);
+    const float phi = off + 0.125f * (yy / xx);
+    float sp, cp;
+    sincos_turn(phi, &sp, &cp);
+    *xr = origin ? 0.0f : s * cp;
+    *yr = origin ? 1.0f : c;
+    *zr = origin ? 0.0f : s * sp;
+}
+
+// convert_grid_pos_to_direction(_random) (hemisphere_helpers.cu:95-121): map(gx/12, gy/12),
+// world = mat4(T, N, B, pos) * (xh, yh, zh, 1) in glm order, direction = normalize(world - pos)
+RT_HD f3 grid_direction(float gx, float gy, f3 N, f3 T, f3 B, f3 pos) {
+    float xh, yh, zh;
+    chiu_map(gx / (float)kGridRes, gy / (float)kGridRes, &xh, &yh, &zh);
+    const f3 w = make3((T.x * xh + N.x * yh) + (B.x * zh + pos.x * 1.0f),
+                       (T.y * xh + N.y * yh) + (B.y * zh + pos.y * 1.0f),
+                       (T.z * xh + N.z * yh) + (B.z * zh + pos.z * 1.0f));
+    return normalize(make3(w.x - pos.x, w.y - pos.y, w.z - pos.z));
+}
 
 }  // namespace rt

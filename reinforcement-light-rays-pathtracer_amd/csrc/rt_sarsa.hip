@@ -1,0 +1,343 @@
+// rt_sarsa.hip — Expected-SARSA radiance-volume path tracer (BASELINE config 3).
+//
+// Reference: GPU/path_tracing/reinforcement_path_tracing.cu:6-120 (render
+// kernel, per-frame distribution update), GPU/radiance_volumes/radiance_map.cu
+// (:90-146 sampling + TD update dispatch, :149-203 nearest volume),
+// GPU/radiance_volumes/radiance_volume.cu (:93-112 expected_sarsa_irradiance,
+// :148-188 update_radiance_distribution, :191-244 CDF sampling,
+// :282-307 temporal_difference_update, irradiance estimate).
+//
+// Determinism: the reference updates the Q-table racily while
+// it renders (non-atomic read-modify-write + atomicExch).  Here a frame reads
+// the Q-table, irradiance and CDFs of the previous frame, and every TD target
+// is added to a per-(volume, sector) fixed-point sum (2^-32 units, integer
+// atomics: order-independent) with a visit count; k_sarsa_apply then folds
+// the frame's targets into Q in closed form — the running mean that
+// alpha = 1/(1 + visits) produces — and rebuilds the CDFs.  Same frames, same
+// seed: bit-identical Q-table and image on any GPU count, and against oracle/.
+#include <float.h>
+
+#include "rt_trace.hpp"
+
+namespace rt {
+
+namespace {
+
+constexpr float kGridRhoS = 1.0f / ((float)kGridRes * (float)kGridRes);             // GRID_RHO
+constexpr float kRadianceThreshold = (1.f / ((float)kGridRes * (float)kGridRes)) * 0.8f;  // RADIANCE_THRESHOLD
+constexpr float kIrrScale = (2.f * kPi) / ((float)(kGridRes * kGridRes));          // get_irradiance_estimate
+
+__device__ __forceinline__ float len3(float x, float y, float z) { return sqrtf((x * x + y * y) + z * z); }
+
+// find_closest_radiance_volume_iterative (radiance_map.cu:149-203): explicit-stack
+// KD descent; a far child is visited when delta^2 < MAX_DIST; leaves need an
+// identical normal; the search starts from volume 0 at the distance of the root
+// element's position (the origin for an internal root).
+__device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm) {
+    const KdNode* __restrict__ kd = m.kd;
+    int best = 0;
+    float best_d = len3(pos.x - kd[0].px, pos.y - kd[0].py, pos.z - kd[0].pz);
+    int stack[64];
+    int sp = 0;
+    stack[sp++] = 0;
+    while (sp > 0) {
+        const KdNode nd = kd[stack[--sp]];
+        if (nd.leaf) {
+            const float d = len3(nd.px - pos.x, nd.py - pos.y, nd.pz - pos.z);
+            if (nrm.x == nd.nx && nrm.y == nd.ny && nrm.z == nd.nz && d < best_d) {
+                best = nd.vol;
+                best_d = d;
+            }
+        } else {
+            const float pc = (nd.dim == 0) ? pos.x : ((nd.dim == 1) ? pos.y : pos.z);
+            const float delta = pc - nd.data;
+            const bool near_split = (delta * delta) < m.max_dist;
+            if (sp + 2 > 64) break;  // the reference's Stack is 30 deep; this one cannot overflow at depth <= 31
+            if (delta < 0.0f) {
+                if (near_split) stack[sp++] = nd.right;
+                stack[sp++] = nd.left;
+            } else {
+                if (near_split) stack[sp++] = nd.left;
+                stack[sp++] = nd.right;
+            }
+        }
+    }
+    return best;
+}
+
+// sample_direction_from_radiance_distribution (radiance_volume.cu:191-244)
+__device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float ry, int* sector, f3* dir,
+                             float* pdf) {
+    const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
+    int found = -1;
+    float mv = 0.0f, pv = 0.0f;
+    if (r <= cdf[0]) {
+        found = 0;
+        mv = cdf[0];
+    } else {
+        int start = 0, end = kSarsaSectors - 1;
+        while (start <= end) {
+            const int mid = (end + start) / 2;
+            const float mval = cdf[mid];
+            const float pval = (mid > 0) ? cdf[mid - 1] : 0.0f;
+            if (r < mval && pval <= r) {
+                found = mid;
+                mv = mval;
+                pv = pval;
+                break;
+            } else if (mval < r) {
+                start = mid + 1;
+            } else {
+                end = mid - 1;
+            }
+        }
+    }
+    if (found < 0) return false;
+    const int sx = found / kGridRes;
+    const int sy = found - sx * kGridRes;
+    *sector = found;
+    *pdf = kRho * ((found == 0 ? mv : (mv - pv)) / kGridRhoS);
+    const float4 p4 = m.vol_pos[rv];
+    const float4 N4 = m.vol_frame[rv * 3 + 0], T4 = m.vol_frame[rv * 3 + 1], B4 = m.vol_frame[rv * 3 + 2];
+    *dir = grid_direction((float)sx + rx, (float)sy + ry, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                          make3(B4.x, B4.y, B4.z), make3(p4.x, p4.y, p4.z));
+    return true;
+}
+
+__device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, float target) {
+    const long long v = __float2ll_rn(target * 4294967296.0f);
+    const size_t k = (size_t)rv * kSarsaSectors + sector;
+    atomicAdd(&m.acc_sum[k], (unsigned long long)v);
+    atomicAdd(&m.acc_cnt[k], 1u);
+}
+
+// path_trace_reinforcement_iterative (reinforcement_path_tracing.cu:50-120), GPU preset
+template <int RULE>
+__global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, const SarsaMap m) {
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    const int part = blockIdx.x & (a.split - 1);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int chunk = threadIdx.x & (a.split - 1);
+    const int lane = threadIdx.x & 63;
+    const int lx = q & 15, ly = q >> 4;
+    const int px = blk.px0 + lx, py = blk.py0 + ly;
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+    const float4* __restrict__ tri = a.scene.isect;
+    const float4* __restrict__ shade = a.scene.shade;
+    const int n_surf = a.scene.n_surf, n_tri = a.scene.n_tri;
+    const int s_end = (chunk + 1) * a.per_chunk;
+
+    int s = valid ? chunk * a.per_chunk : s_end;
+    int depth = 0;
+    int cur_rv = -1, cur_sector = -1;
+    float cur_brdf = 0.0f;
+    f3 o = make3(a.cam_x, a.cam_y, a.cam_z), d = make3(0.f, 0.f, 1.f);
+    f3 tp = make3(1.f, 1.f, 1.f), acc = make3(0.f, 0.f, 0.f);
+    unsigned n_casts = 0;
+    if (s < s_end) {
+        float r1, r2;
+        draw2(pix, a.sample_base + (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        camera_ray<1>(a, px, py, r1, r2, &d);
+    }
+    for (;;) {
+        const bool active = s < s_end;
+        if (__ballot(active) == 0ull) break;
+        if (!active) continue;
+        const Hit h = closest_hit<RULE>(tri, n_tri, o, d, a.t_scale);
+        ++n_casts;
+        const bool is_surf = (h.tri >= 0) && (h.tri < n_surf);
+        f3 pos = o;
+        f3 nrm = make3(0.f, 0.f, 0.f);
+        if (is_surf) {
+            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+            pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+            const float4 N4 = shade[h.tri * kShadeF4 + 0];
+            nrm = make3(N4.x, N4.y, N4.z);
+        }
+        if (depth > 0) {
+            if (cur_rv >= 0 && cur_sector >= 0) {  // temporal_difference_update_radiance_volume_sector
+                float target;
+                int next_rv = -1;
+                if (h.tri < 0) {
+                    target = cur_brdf * a.env_light;
+                } else if (!is_surf) {
+                    target = cur_brdf * m.tri_lum[h.tri];
+                } else {
+                    next_rv = sarsa_nearest(m, pos, nrm);
+                    target = (m.accum[next_rv] * kIrrScale) * cur_brdf;
+                }
+                td_event(m, cur_rv, cur_sector, target);
+                cur_rv = next_rv;
+                cur_sector = -1;
+            }
+        } else if (is_surf) {
+            cur_rv = sarsa_nearest(m, pos, nrm);
+        }
+        bool terminal = false;
+        f3 L = make3(0.f, 0.f, 0.f);
+        if (h.tri < 0) {
+            terminal = true;
+            L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+        } else if (!is_surf) {
+            terminal = true;
+            const float4 e = shade[h.tri * kShadeF4 + 3];
+            L = make3(tp.x * e.x, tp.y * e.y, tp.z * e.z);
+        } else {
+            uint32_t rn[4];
+            philox4x32_10(pix, a.sample_base + (uint32_t)s, 1u + (uint32_t)depth, 0u, a.seed_lo, a.seed_hi, rn);
+            f3 sd;
+            float pdf;
+            bool ok = true;
+            if (cur_rv < 0) {  // no volume: uniform hemisphere, pdf = RHO
+                const float4 T4 = shade[h.tri * kShadeF4 + 1], B4 = shade[h.tri * kShadeF4 + 2];
+                const float c = u01(rn[0]);
+                const float st = sqrtf(1.0f - c * c);
+                float sphi, cphi;
+                sincos_turn(u01(rn[1]), &sphi, &cphi);
+                const float sx = st * cphi, sz = st * sphi;
+                sd = make3((sx * B4.x + c * nrm.x) + sz * T4.x, (sx * B4.y + c * nrm.y) + sz * T4.y,
+                           (sx * B4.z + c * nrm.z) + sz * T4.z);
+                pdf = kRho;
+            } else {
+                ok = sarsa_sample(m, cur_rv, u01(rn[0]), u01(rn[1]), u01(rn[2]), &cur_sector, &sd, &pdf);
+            }
+            if (!ok) {
+                // no sector: the reference traces the zero direction it returns, which
+                // hits nothing (one more cast; its radiance there is NaN, here the miss value)
+                terminal = true;
+                if (depth + 1 < a.max_bounces) {
+                    ++n_casts;
+                    L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+                }
+            } else {
+                const float4 brdf = shade[h.tri * kShadeF4 + 3];
+                const float cos_theta = dot(nrm, sd);
+                cur_brdf = m.tri_lum[h.tri] / kPi;
+                tp.x = tp.x * ((brdf.x * cos_theta) / pdf);
+                tp.y = tp.y * ((brdf.y * cos_theta) / pdf);
+                tp.z = tp.z * ((brdf.z * cos_theta) / pdf);
+                o = make3(pos.x + sd.x * kEps, pos.y + sd.y * kEps, pos.z + sd.z * kEps);
+                d = normalize(sd);
+                ++depth;
+                if (depth == a.max_bounces) terminal = true;
+            }
+        }
+        if (terminal) {
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+            ++s;
+            depth = 0;
+            cur_rv = -1;
+            cur_sector = -1;
+            tp = make3(1.f, 1.f, 1.f);
+            o = make3(a.cam_x, a.cam_y, a.cam_z);
+            if (s < s_end) {
+                float r1, r2;
+                draw2(pix, a.sample_base + (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+                camera_ray<1>(a, px, py, r1, r2, &d);
+            }
+        }
+    }
+    const int base = lane & ~(a.split - 1);
+    f3 tot = acc;
+    for (int k = 1; k < a.split; ++k) {
+        const float vx = __shfl(acc.x, base + k, 64);
+        const float vy = __shfl(acc.y, base + k, 64);
+        const float vz = __shfl(acc.z, base + k, 64);
+        tot.x = tot.x + vx;
+        tot.y = tot.y + vy;
+        tot.z = tot.z + vz;
+    }
+    if (valid && chunk == 0) {
+        const float fs = (float)a.spp;
+        float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+        dst[0] = tot.x / fs;
+        dst[1] = tot.y / fs;
+        dst[2] = tot.z / fs;
+    }
+    if (a.casts != nullptr) {
+        const unsigned total = wave_sum(n_casts);
+        if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
+    }
+}
+
+// End of frame, one lane per volume: fold the frame's TD targets (the running
+// mean of alpha = 1/(1+visits), clamped at RADIANCE_THRESHOLD), update the
+// irradiance with expected_sarsa_irradiance's increments (cell corners), and
+// rebuild the CDF from Q*cos(cell centre) (update_radiance_distribution).
+__global__ __launch_bounds__(256) void k_sarsa_apply(const SarsaMap m) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= m.n_vol) return;
+    const size_t b = (size_t)v * kSarsaSectors;
+    const float brdf = m.vol_brdf[v];
+    float accum = m.accum[v];
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        const uint32_t n = m.acc_cnt[b + k];
+        if (n == 0u) continue;
+        const long long S = (long long)m.acc_sum[b + k];
+        const float sum = (float)((double)S * 2.3283064365386962890625e-10);
+        const uint32_t vis = m.visits[b + k];
+        const float q_old = m.Q[b + k];
+        float q_new = (q_old * (float)vis + sum) / (float)(vis + n);
+        q_new = q_new > kRadianceThreshold ? q_new : kRadianceThreshold;
+        const float cc = m.cos_corner[b + k];
+        accum = (accum - ((q_old * cc) * brdf)) + ((q_new * cc) * brdf);
+        m.Q[b + k] = q_new;
+        m.visits[b + k] = vis + n;
+        m.acc_cnt[b + k] = 0u;
+        m.acc_sum[b + k] = 0ull;
+    }
+    m.accum[v] = accum;
+    float total = 0.0000000001f;
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        float t = m.Q[b + k] * m.cos_center[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        total += t;
+    }
+    float prev = 0.0f;
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        float t = m.Q[b + k] * m.cos_center[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        const float rad = t / total + prev;
+        m.cdf[b + k] = rad;
+        prev = rad;
+    }
+}
+
+// nearest-volume queries alone (KD parity): pos/nrm [n][3]
+__global__ __launch_bounds__(256) void k_sarsa_nearest(const SarsaMap m, const float* __restrict__ pos,
+                                                       const float* __restrict__ nrm, int n, int32_t* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    out[i] = sarsa_nearest(m, make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]),
+                           make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]));
+}
+
+}  // namespace
+
+hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float* nrm, int n, int32_t* out,
+                                hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sarsa_nearest, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, m, pos, nrm, n, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
+    if (a.n_blocks <= 0) return hipSuccess;
+    if (a.hit_rule == 0)
+        hipLaunchKernelGGL(k_sarsa_render<0>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
+    else
+        hipLaunchKernelGGL(k_sarsa_render<1>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
+    return hipGetLastError();
+}
+
+hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream) {
+    if (m.n_vol <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sarsa_apply, dim3((unsigned)((m.n_vol + 255) / 256)), dim3(256), 0, stream, m);
+    return hipGetLastError();
+}
+
+}  // namespace rt

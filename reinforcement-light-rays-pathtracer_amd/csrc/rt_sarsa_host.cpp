@@ -1,0 +1,497 @@
+// rt_sarsa_host.cpp — C ABI of the Expected-SARSA path (BASELINE config 3):
+// radiance-volume placement (RadianceMap::get_radiance_volumes_count /
+// uniformly_sample_radiance_volumes, GPU/radiance_volumes/radiance_map.cu:57-84),
+// the radiance volume's initial state (RadianceVolume::initialise_*,
+// radiance_volume.cu:46-89), the KD tree and its array form (RadianceTree,
+// radiance_tree.cu:10-246), and the frame driver (GPU/main.cu:296-350: render,
+// then update_radiance_volume_distributions).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/rtmi.h"
+#include "rt_internal.hpp"
+
+namespace rt {
+int set_error(int code, const char* msg);
+int ctx_device(const rt_ctx* ctx);
+const DeviceScene& scene_device(const rt_scene* s);
+void scene_host(const rt_scene* s, const float** tri, const float** normals, const float** albedo,
+                const float** emission, int* n_surf, int* n_light);
+int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
+               const BlockDesc** d_blocks, int* n_blocks);
+RenderLaunch render_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p);
+}  // namespace rt
+
+namespace {
+
+int err(int code, const std::string& m) { return rt::set_error(code, m.c_str()); }
+
+#define RT_HIPE(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t e_ = (expr);                                                                \
+        if (e_ != hipSuccess) return err(RT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+constexpr float kAreaPerSample = 0.001f;  // AREA_PER_SAMPLE (radiance_volumes_settings.h:12)
+constexpr float kInitialRadiance = (1.f / ((float)rt::kGridRes * (float)rt::kGridRes)) * 100.f;  // :16
+constexpr uint32_t kPlacementEvent = 0xFFFF0001u;  // RNG counter word 2 of volume placement
+constexpr int kMaxKdDepth = 30;                  // k_sarsa_render's traversal stack holds 64 entries
+
+// Triangle::compute_area (GPU/objects/triangle.cu:17-27): float lengths and
+// cosine; 1 - pow(cos, 2) and its sqrt in double (host pow promotes).
+float triangle_area(const float* v) {
+    using rt::f3;
+    const f3 a = rt::make3(v[3] - v[0], v[4] - v[1], v[5] - v[2]);
+    const f3 b = rt::make3(v[6] - v[0], v[7] - v[1], v[8] - v[2]);
+    const float e01_e02 = sqrtf(rt::dot(a, a)) * sqrtf(rt::dot(b, b));
+    const float c = rt::dot(a, b) / e01_e02;
+    const float s = (float)sqrt(1.0 - (double)c * (double)c);
+    return 0.5f * e01_e02 * s;
+}
+
+// Material::Material / AreaLight luminance (objects/material.cu:13, lights/area_light.cu:22)
+float luminance(const float* rgb) {
+    const float mx = std::max(rgb[0], std::max(rgb[1], rgb[2]));
+    const float mn = std::min(rgb[0], std::min(rgb[1], rgb[2]));
+    return 0.5f * (mx + mn);
+}
+
+struct Tree {
+    const std::vector<float>* pos;  // [n][4]
+    std::vector<rt::KdNode> nodes;
+    int max_depth = 0;
+
+    struct Sub {  // one RadianceTree node before flattening
+        int dim;
+        float median;
+        int vol = -1;  // leaf
+        int left = -1, right = -1;
+    };
+    std::vector<Sub> subs;
+
+    // RadianceTree::RadianceTree (radiance_tree.cu:10-60): std::sort on the split
+    // dimension (the reference's comparator: position[dim] <), left = [0, median_index].
+    int build(std::vector<int>& v, int dim, int depth) {
+        max_depth = std::max(max_depth, depth);
+        const int me = (int)subs.size();
+        subs.push_back(Sub());
+        subs[me].dim = dim;
+        const int n = (int)v.size();
+        const std::vector<float>& P = *pos;
+        if (n == 1) {
+            subs[me].median = P[4 * v[0] + dim];
+            subs[me].vol = v[0];
+            return me;
+        }
+        std::sort(v.begin(), v.end(), [&](int l, int r) { return P[4 * l + dim] < P[4 * r + dim]; });
+        int mi;
+        if (n % 2 == 0) {
+            mi = n / 2 - 1;
+            subs[me].median = (P[4 * v[mi] + dim] + P[4 * v[mi + 1] + dim]) / 2;
+        } else {
+            mi = n / 2;
+            subs[me].median = P[4 * v[mi] + dim];
+        }
+        std::vector<int> L(v.begin(), v.begin() + mi + 1), R(v.begin() + mi + 1, v.end());
+        const int nd = (dim + 1) % 3;
+        const int l = build(L, nd, depth + 1);
+        const int r = build(R, nd, depth + 1);
+        subs[me].left = l;
+        subs[me].right = r;
+        return me;
+    }
+
+    // RadianceTree::convert_to_array / traverse_and_insert (radiance_tree.cu:181-246):
+    // the root first, then each internal node appends its two children and
+    // recurses left before right; a leaf overwrites its own slot.
+    void flatten(int root, const std::vector<float>& nrm) {
+        rt::KdNode r;
+        memset(&r, 0, sizeof(r));
+        r.dim = subs[root].dim;
+        r.data = subs[root].median;
+        nodes.push_back(r);
+        insert(root, 0, nrm);
+    }
+    void insert(int s, int slot, const std::vector<float>& nrm) {
+        const int last = (int)nodes.size() - 1;
+        const Sub& u = subs[s];
+        if (u.vol >= 0) {
+            rt::KdNode& e = nodes[slot];
+            memset(&e, 0, sizeof(e));
+            e.dim = u.dim;
+            e.leaf = 1;
+            e.data = (float)u.vol;
+            e.vol = u.vol;
+            e.px = (*pos)[4 * u.vol];
+            e.py = (*pos)[4 * u.vol + 1];
+            e.pz = (*pos)[4 * u.vol + 2];
+            e.nx = nrm[3 * u.vol];
+            e.ny = nrm[3 * u.vol + 1];
+            e.nz = nrm[3 * u.vol + 2];
+            return;
+        }
+        nodes[slot].left = last + 1;
+        nodes[slot].right = last + 2;
+        rt::KdNode c;
+        memset(&c, 0, sizeof(c));
+        c.dim = (u.dim + 1) % 3;
+        c.data = subs[u.left].median;
+        nodes.push_back(c);
+        c.data = subs[u.right].median;
+        nodes.push_back(c);
+        insert(u.left, last + 1, nrm);
+        insert(u.right, last + 2, nrm);
+    }
+};
+
+}  // namespace
+
+struct rt_sarsa {
+    int device = 0;
+    int n_vol = 0;
+    uint32_t frames = 0;      // frames rendered so far (RNG sample base = frames * spp)
+    uint64_t seed = 0;
+    std::vector<float> pos;   // [n][4]
+    std::vector<float> nrm;   // [n][3]
+    std::vector<int32_t> surf;  // [n] surface index
+    std::vector<rt::KdNode> kd;
+    rt::SarsaMap m;
+    std::vector<void*> allocs;
+    ~rt_sarsa() {
+        (void)hipSetDevice(device);
+        for (void* p : allocs) (void)hipFree(p);
+    }
+    template <class T>
+    hipError_t alloc(T** p, size_t count) {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, sizeof(T) * (count ? count : 1));
+        if (e == hipSuccess) allocs.push_back(q);
+        *p = (T*)q;
+        return e;
+    }
+};
+
+namespace {
+
+int check_sarsa_params(const rt_params* p) {
+    if (!p) return err(RT_E_INVALID, "params is NULL");
+    if (p->width <= 0 || p->height <= 0 || p->spp <= 0) return err(RT_E_INVALID, "bad image size / spp");
+    if (p->max_bounces < 1) return err(RT_E_INVALID, "max_bounces must be >= 1");
+    if (p->preset != RT_PRESET_GPU)
+        return err(RT_E_UNSUPPORTED, "the SARSA renderer implements the GPU-engine preset");
+    if (p->hit_rule != RT_HIT_RULE_CPU && p->hit_rule != RT_HIT_RULE_GPU) return err(RT_E_INVALID, "bad hit_rule");
+    const int split = p->spp_split <= 0 ? 1 : p->spp_split;
+    if (split > 64 || (split & (split - 1)) != 0)
+        return err(RT_E_INVALID, "spp_split must be a power of two <= 64");
+    if (p->spp % split != 0) return err(RT_E_INVALID, "spp_split does not divide spp");
+    if ((int64_t)p->width * (int64_t)p->height > (int64_t)1 << 31) return err(RT_E_INVALID, "image too large");
+    return RT_OK;
+}
+
+int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, const rt_params* p,
+                 const rt::BlockDesc* d_blocks, int n_blocks, int clip_x1, int clip_y1, int out_pitch,
+                 float* d_out, unsigned long long* d_casts, hipStream_t stream, bool apply) {
+    rt::RenderLaunch a = rt::render_launch(scene, cam, p);
+    a.blocks = d_blocks;
+    a.n_blocks = n_blocks;
+    a.clip_x1 = clip_x1;
+    a.clip_y1 = clip_y1;
+    a.out_pitch = out_pitch;
+    a.out = d_out;
+    a.casts = d_casts;
+    a.sample_base = sa->frames * (uint32_t)p->spp;
+    RT_HIPE(rt::launch_sarsa_render(a, sa->m, stream));
+    if (apply) RT_HIPE(rt::launch_sarsa_apply(sa->m, stream));
+    sa->frames += 1;
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa** out) {
+    if (!ctx || !scene || !out) return err(RT_E_INVALID, "NULL argument");
+    *out = nullptr;
+    const float *tri, *normals, *albedo, *emission;
+    int n_surf, n_light;
+    rt::scene_host(scene, &tri, &normals, &albedo, &emission, &n_surf, &n_light);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    rt_sarsa* sa = new rt_sarsa();
+    sa->device = rt::ctx_device(ctx);
+    sa->seed = seed;
+    // get_radiance_volumes_count + uniformly_sample_radiance_volumes: per surface,
+    // floor(area / AREA_PER_SAMPLE) points by rejection (a1 + a2 <= 1), drawn from
+    // Philox counter (volume, attempt, kPlacementEvent, 0) in place of rand().
+    for (int j = 0; j < n_surf; ++j) {
+        const float* v = tri + 9 * j;
+        const int cnt = (int)floorf(triangle_area(v) / kAreaPerSample);
+        for (int i = 0; i < cnt; ++i) {
+            const uint32_t x = (uint32_t)sa->pos.size() / 4;
+            float a1, a2;
+            uint32_t attempt = 0;
+            do {
+                uint32_t r[4];
+                rt::philox4x32_10(x, attempt++, kPlacementEvent, 0u, k0, k1, r);
+                a1 = rt::u01(r[0]);
+                a2 = rt::u01(r[1]);
+            } while (a1 + a2 > 1.f);
+            for (int c = 0; c < 3; ++c) {
+                const float p0 = v[c], p1 = v[3 + c], p2 = v[6 + c];
+                sa->pos.push_back((p0 + a1 * (p1 - p0)) + a2 * (p2 - p0));
+            }
+            sa->pos.push_back(1.f);
+            for (int c = 0; c < 3; ++c) sa->nrm.push_back(normals[3 * j + c]);
+            sa->surf.push_back(j);
+        }
+    }
+    const int n = (int)sa->surf.size();
+    sa->n_vol = n;
+    if (n == 0) {
+        delete sa;
+        return err(RT_E_INVALID, "scene has no radiance volumes (total surface area < AREA_PER_SAMPLE)");
+    }
+    // RadianceVolume frames and per-sector cosines (cell centres for the CDF,
+    // cell corners for expected_sarsa_irradiance), the initial Q / CDF / irradiance.
+    const int S = rt::kSarsaSectors;
+    std::vector<float> frame((size_t)n * 12), brdf(n), cc((size_t)n * S), ck((size_t)n * S), Q((size_t)n * S),
+        cdf((size_t)n * S), accum(n);
+    for (int i = 0; i < n; ++i) {
+        const rt::f3 N = rt::make3(sa->nrm[3 * i], sa->nrm[3 * i + 1], sa->nrm[3 * i + 2]);
+        const rt::f3 P = rt::make3(sa->pos[4 * i], sa->pos[4 * i + 1], sa->pos[4 * i + 2]);
+        rt::f3 T, B;
+        rt::normal_frame(N, &T, &B);
+        const float f[12] = {N.x, N.y, N.z, 0.f, T.x, T.y, T.z, 0.f, B.x, B.y, B.z, 0.f};
+        memcpy(&frame[(size_t)12 * i], f, sizeof(f));
+        const float lum = luminance(albedo + 3 * sa->surf[i]);
+        brdf[i] = lum / rt::kPi;
+        float irr = 0.f;
+        for (int x = 0; x < rt::kGridRes; ++x)
+            for (int y = 0; y < rt::kGridRes; ++y) {
+                const int k = x * rt::kGridRes + y;
+                const rt::f3 dc = rt::grid_direction((float)x + 0.5f, (float)y + 0.5f, N, T, B, P);
+                const rt::f3 dk = rt::grid_direction((float)x, (float)y, N, T, B, P);
+                cc[(size_t)i * S + k] = rt::dot(dc, N);
+                ck[(size_t)i * S + k] = rt::dot(dk, N);
+                Q[(size_t)i * S + k] = kInitialRadiance;
+                cdf[(size_t)i * S + k] = (float)k * (1.f / ((float)rt::kGridRes * (float)rt::kGridRes));
+                // initialise_radiance_grid: cos * (luminance / M_PI) * Q in double, summed in float
+                irr = (float)((double)irr + ((double)cc[(size_t)i * S + k] * ((double)lum / M_PI)) *
+                                                (double)kInitialRadiance);
+            }
+        accum[i] = irr;
+    }
+    std::vector<float> tri_lum(n_surf + n_light);
+    for (int j = 0; j < n_surf; ++j) tri_lum[j] = luminance(albedo + 3 * j);
+    for (int j = 0; j < n_light; ++j) tri_lum[n_surf + j] = luminance(emission + 3 * j);
+    // KD tree over the volume positions
+    Tree t;
+    t.pos = &sa->pos;
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) idx[i] = i;
+    const int root = t.build(idx, 0, 0);
+    if (t.max_depth > kMaxKdDepth) {
+        delete sa;
+        return err(RT_E_UNSUPPORTED, "radiance tree deeper than the traversal stack allows");
+    }
+    t.flatten(root, sa->nrm);
+    sa->kd = t.nodes;
+
+    hipError_t e = hipSetDevice(sa->device);
+    float4 *d_pos = nullptr, *d_frame = nullptr;
+    float *d_brdf = nullptr, *d_cc = nullptr, *d_ck = nullptr, *d_lum = nullptr, *d_Q = nullptr, *d_cdf = nullptr,
+          *d_acc = nullptr;
+    uint32_t *d_vis = nullptr, *d_cnt = nullptr;
+    unsigned long long* d_sum = nullptr;
+    rt::KdNode* d_kd = nullptr;
+    const size_t nS = (size_t)n * S;
+    if (e == hipSuccess) e = sa->alloc(&d_pos, n);
+    if (e == hipSuccess) e = sa->alloc(&d_frame, (size_t)n * 3);
+    if (e == hipSuccess) e = sa->alloc(&d_brdf, n);
+    if (e == hipSuccess) e = sa->alloc(&d_cc, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_ck, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_lum, tri_lum.size());
+    if (e == hipSuccess) e = sa->alloc(&d_Q, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_cdf, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_acc, n);
+    if (e == hipSuccess) e = sa->alloc(&d_vis, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_cnt, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_sum, nS);
+    if (e == hipSuccess) e = sa->alloc(&d_kd, sa->kd.size());
+    auto up = [&](void* d, const void* h, size_t bytes) {
+        if (e == hipSuccess && bytes) e = hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
+    };
+    up(d_pos, sa->pos.data(), sizeof(float) * 4 * n);
+    up(d_frame, frame.data(), sizeof(float) * frame.size());
+    up(d_brdf, brdf.data(), sizeof(float) * n);
+    up(d_cc, cc.data(), sizeof(float) * nS);
+    up(d_ck, ck.data(), sizeof(float) * nS);
+    up(d_lum, tri_lum.data(), sizeof(float) * tri_lum.size());
+    up(d_Q, Q.data(), sizeof(float) * nS);
+    up(d_cdf, cdf.data(), sizeof(float) * nS);
+    up(d_acc, accum.data(), sizeof(float) * n);
+    up(d_kd, sa->kd.data(), sizeof(rt::KdNode) * sa->kd.size());
+    if (e == hipSuccess) e = hipMemset(d_vis, 0, sizeof(uint32_t) * nS);
+    if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(uint32_t) * nS);
+    if (e == hipSuccess) e = hipMemset(d_sum, 0, sizeof(unsigned long long) * nS);
+    if (e != hipSuccess) {
+        delete sa;
+        return err(RT_E_HIP, std::string("rt_sarsa_create: ") + hipGetErrorString(e));
+    }
+    rt::SarsaMap& m = sa->m;
+    m.n_vol = n;
+    m.vol_pos = d_pos;
+    m.vol_frame = d_frame;
+    m.vol_brdf = d_brdf;
+    m.cos_center = d_cc;
+    m.cos_corner = d_ck;
+    m.tri_lum = d_lum;
+    m.Q = d_Q;
+    m.cdf = d_cdf;
+    m.visits = d_vis;
+    m.accum = d_acc;
+    m.acc_sum = d_sum;
+    m.acc_cnt = d_cnt;
+    m.kd = d_kd;
+    m.n_kd = (int)sa->kd.size();
+    *out = sa;
+    return RT_OK;
+}
+
+int rt_sarsa_destroy(rt_sarsa* sarsa) {
+    delete sarsa;
+    return RT_OK;
+}
+
+int rt_sarsa_info(const rt_sarsa* sa, int32_t* n_volumes, int32_t* n_nodes, uint32_t* frames) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (n_volumes) *n_volumes = sa->n_vol;
+    if (n_nodes) *n_nodes = (int32_t)sa->kd.size();
+    if (frames) *frames = sa->frames;
+    return RT_OK;
+}
+
+int rt_sarsa_volumes(const rt_sarsa* sa, float* pos, float* normal, int32_t* surface, float* kd_nodes) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    const int n = sa->n_vol;
+    if (pos)
+        for (int i = 0; i < n; ++i) memcpy(pos + 3 * i, &sa->pos[4 * i], sizeof(float) * 3);
+    if (normal) memcpy(normal, sa->nrm.data(), sizeof(float) * 3 * n);
+    if (surface) memcpy(surface, sa->surf.data(), sizeof(int32_t) * n);
+    if (kd_nodes) memcpy(kd_nodes, sa->kd.data(), sizeof(rt::KdNode) * sa->kd.size());
+    return RT_OK;
+}
+
+int rt_sarsa_read(const rt_sarsa* sa, float* q, float* cdf, uint32_t* visits, float* irradiance) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    RT_HIPE(hipSetDevice(sa->device));
+    const size_t nS = (size_t)sa->n_vol * rt::kSarsaSectors;
+    RT_HIPE(hipDeviceSynchronize());
+    if (q) RT_HIPE(hipMemcpy(q, sa->m.Q, sizeof(float) * nS, hipMemcpyDeviceToHost));
+    if (cdf) RT_HIPE(hipMemcpy(cdf, sa->m.cdf, sizeof(float) * nS, hipMemcpyDeviceToHost));
+    if (visits) RT_HIPE(hipMemcpy(visits, sa->m.visits, sizeof(uint32_t) * nS, hipMemcpyDeviceToHost));
+    if (irradiance) RT_HIPE(hipMemcpy(irradiance, sa->m.accum, sizeof(float) * sa->n_vol, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_sarsa_nearest(rt_ctx* ctx, const rt_sarsa* sa, const float* pos, const float* normal, int n, int32_t* out) {
+    if (!ctx || !sa || (n > 0 && (!pos || !normal || !out))) return err(RT_E_INVALID, "NULL argument");
+    if (n < 0) return err(RT_E_INVALID, "n < 0");
+    if (n == 0) return RT_OK;
+    RT_HIPE(hipSetDevice(sa->device));
+    float *d_p = nullptr, *d_n = nullptr;
+    int32_t* d_o = nullptr;
+    const size_t b3 = sizeof(float) * 3 * (size_t)n;
+    hipError_t e = hipMalloc(&d_p, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_n, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_o, sizeof(int32_t) * n);
+    if (e == hipSuccess) e = hipMemcpy(d_p, pos, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_n, normal, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rt::launch_sarsa_nearest(sa->m, d_p, d_n, n, d_o, 0);
+    if (e == hipSuccess) e = hipMemcpy(out, d_o, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_p);
+    (void)hipFree(d_n);
+    (void)hipFree(d_o);
+    if (e != hipSuccess) return err(RT_E_HIP, std::string("rt_sarsa_nearest: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_render_sarsa(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* sa, const rt_camera* cam,
+                    const rt_params* params, int frames, float* out_rgb, uint64_t* out_ray_casts) {
+    if (!ctx || !scene || !sa || !cam || !out_rgb) return err(RT_E_INVALID, "NULL argument");
+    int rc = check_sarsa_params(params);
+    if (rc != RT_OK) return rc;
+    if (frames < 1) return err(RT_E_INVALID, "frames must be >= 1");
+    if (sa->device != rt::ctx_device(ctx)) return err(RT_E_INVALID, "radiance map belongs to another device");
+    RT_HIPE(hipSetDevice(sa->device));
+    const int W = params->width, H = params->height;
+    std::vector<rt::BlockDesc> blocks;
+    for (int by = 0; by < H; by += 16)
+        for (int bx = 0; bx < W; bx += 16) blocks.push_back({bx, by, bx, by});
+    rt::BlockDesc* d_blocks = nullptr;
+    float* d_out = nullptr;
+    unsigned long long* d_casts = nullptr;
+    const size_t ob = sizeof(float) * 3 * (size_t)W * H;
+    hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
+    if (e == hipSuccess) e = hipMalloc(&d_out, ob);
+    if (e == hipSuccess) e = hipMalloc(&d_casts, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_casts, 0, sizeof(unsigned long long));
+    if (e == hipSuccess)
+        e = hipMemcpy(d_blocks, blocks.data(), sizeof(rt::BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
+    rc = RT_OK;
+    for (int f = 0; e == hipSuccess && rc == RT_OK && f < frames; ++f)
+        rc = render_frame(sa, scene, cam, params, d_blocks, (int)blocks.size(), W, H, W, d_out, d_casts, 0, true);
+    if (rc == RT_OK && e == hipSuccess) e = hipDeviceSynchronize();
+    unsigned long long casts = 0;
+    if (rc == RT_OK && e == hipSuccess) e = hipMemcpy(out_rgb, d_out, ob, hipMemcpyDeviceToHost);
+    if (rc == RT_OK && e == hipSuccess) e = hipMemcpy(&casts, d_casts, sizeof(casts), hipMemcpyDeviceToHost);
+    (void)hipFree(d_blocks);
+    (void)hipFree(d_out);
+    (void)hipFree(d_casts);
+    if (rc != RT_OK) return rc;
+    if (e != hipSuccess) return err(RT_E_HIP, std::string("rt_render_sarsa: ") + hipGetErrorString(e));
+    if (out_ray_casts) *out_ray_casts = casts;
+    return RT_OK;
+}
+
+int rt_render_sarsa_tiles_device(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* sa, const rt_camera* cam,
+                                 const rt_params* params, const int32_t* tiles, int n_tiles, int tile_size,
+                                 float* d_out, uint64_t* d_casts, int apply, void* stream) {
+    if (!ctx || !scene || !sa || !cam) return err(RT_E_INVALID, "NULL argument");
+    int rc = check_sarsa_params(params);
+    if (rc != RT_OK) return rc;
+    if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !d_out))) return err(RT_E_INVALID, "bad tiles/out");
+    if (sa->device != rt::ctx_device(ctx)) return err(RT_E_INVALID, "radiance map belongs to another device");
+    RT_HIPE(hipSetDevice(sa->device));
+    const rt::BlockDesc* d_blocks = nullptr;
+    int n_blocks = 0;
+    if (n_tiles > 0) {
+        rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
+        if (rc != RT_OK) return rc;
+    }
+    return render_frame(sa, scene, cam, params, d_blocks, n_blocks, params->width, params->height, tile_size, d_out,
+                        reinterpret_cast<unsigned long long*>(d_casts), (hipStream_t)stream, apply != 0);
+}
+
+int rt_sarsa_td_device(rt_sarsa* sa, void** d_sum, void** d_count, int64_t* n_entries) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (d_sum) *d_sum = sa->m.acc_sum;
+    if (d_count) *d_count = sa->m.acc_cnt;
+    if (n_entries) *n_entries = (int64_t)sa->n_vol * rt::kSarsaSectors;
+    return RT_OK;
+}
+
+int rt_sarsa_apply(rt_sarsa* sa, void* stream) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    RT_HIPE(hipSetDevice(sa->device));
+    RT_HIPE(rt::launch_sarsa_apply(sa->m, (hipStream_t)stream));
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -34,7 +34,7 @@ struct Hit {
 //                  exact IEEE test runs only for lanes it cannot reject
 //   RT_UNROLL   unroll factor of the triangle loop
 #ifndef RT_HIT_MODE
-#define RT_HIT_MODE 0
+#define RT_HIT_MODE 2  // 7% faster than 0 on Cornell 512^2/256 spp, same image (profiles/r1_ab3.json)
 #endif
 #ifndef RT_UNROLL
 #define RT_UNROLL 1
@@ -42,7 +42,7 @@ struct Hit {
 //   RT_FAST_RCP 1: 1/detA by rcp_rn (v_rcp_f32 + Newton, exhaustively verified)
 //   RT_RCP_STEPS Newton steps of rcp_rn
 #ifndef RT_FAST_RCP
-#define RT_FAST_RCP 0
+#define RT_FAST_RCP 1
 #endif
 #ifndef RT_RCP_STEPS
 #define RT_RCP_STEPS 1
@@ -220,6 +220,38 @@ __device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, u
     philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
     *a = u01(o[0]);
     *b = u01(o[1]);
+}
+
+// Camera ray through (px+r1, py+r2): default_path_tracing.cpp:25-34, Ray::Ray
+// (ray.cpp:7-11), rotate_ray (ray.cpp:47-52; GPU/rays/ray.cu:161-172), with
+// glm's mat4*vec4 order (m0*v0 + m1*v1) + (m2*v2 + m3*v3).
+template <int PRESET>
+__device__ __forceinline__ void camera_ray(const RenderLaunch& a, int px, int py, float r1, float r2,
+                                           f3* d_out) {
+    const float x = (float)px + r1;
+    const float y = (float)py + r2;
+    f3 dir = make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height);
+    dir = normalize(dir);
+    const float w = 1.0f;
+    f3 r;
+    r.x = (a.cos_y * dir.x + 0.0f * dir.y) + (-a.sin_y * dir.z + 0.0f * w);
+    r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
+    r.z = (a.sin_y * dir.x + 0.0f * dir.y) + (a.cos_y * dir.z + 0.0f * w);
+    if (PRESET == 1) {
+        const float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
+        f3 q;
+        q.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
+        q.y = (0.0f * r.x + a.cos_x * r.y) + (a.sin_x * r.z + 0.0f * rw);
+        q.z = (0.0f * r.x + -a.sin_x * r.y) + (a.cos_x * r.z + 0.0f * rw);
+        r = q;
+    }
+    *d_out = r;
+}
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
 }
 
 }  // namespace rt

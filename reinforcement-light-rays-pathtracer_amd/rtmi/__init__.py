@@ -10,7 +10,7 @@ from ._lib import (LIB_PATH, RT_HIT_NONE, RT_HIT_RULE_CPU, RT_HIT_RULE_GPU, RT_H
 from .api import (CAMERAS, OBJ_KINDS, Context, Geometry, Scene, camera, cornell_geometry,
                   default_params, intersect, intersect_device, obj_geometry, pack_argb, render,
                   render_tiles_device, save_bmp)
-from . import dist, dqn, metrics, tiles
+from . import dist, dqn, metrics, sarsa, tiles
 
 __all__ = [
     "LIB_PATH", "RT_HIT_NONE", "RT_HIT_RULE_CPU", "RT_HIT_RULE_GPU", "RT_HIT_TYPE_LIGHT",
@@ -18,5 +18,5 @@ __all__ = [
     "RT_SAMPLER_UNIFORM", "RtCamera", "RtError", "RtParams", "lib", "CAMERAS", "OBJ_KINDS",
     "Context", "Geometry", "Scene", "camera", "cornell_geometry", "default_params", "intersect",
     "intersect_device", "obj_geometry", "pack_argb", "render", "render_tiles_device", "save_bmp",
-    "dist", "dqn", "metrics", "tiles",
+    "dist", "dqn", "metrics", "sarsa", "tiles",
 ]

@@ -39,6 +39,9 @@ EXPORTS = (
     "rt_dynet_read", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
+    "rt_sarsa_create", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
+    "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
+    "rt_sarsa_apply",
 )
 
 
@@ -107,6 +110,18 @@ def _declare(lib):
                               i, i, _FP, _U64P]),
         "rt_render_dqn_tiles_device": (i, [_P, _P, _P, ctypes.POINTER(RtCamera),
                                            ctypes.POINTER(RtParams), _IP, i, i, _P, _P, _P]),
+        "rt_sarsa_create": (i, [_P, _P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+        "rt_sarsa_destroy": (i, [_P]),
+        "rt_sarsa_info": (i, [_P, _IP, _IP, _UP]),
+        "rt_sarsa_volumes": (i, [_P, _FP, _FP, _IP, _P]),
+        "rt_sarsa_read": (i, [_P, _FP, _FP, _UP, _FP]),
+        "rt_sarsa_nearest": (i, [_P, _P, _FP, _FP, i, _IP]),
+        "rt_render_sarsa": (i, [_P, _P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, _FP,
+                                _U64P]),
+        "rt_render_sarsa_tiles_device": (i, [_P, _P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams),
+                                             _IP, i, i, _P, _P, i, _P]),
+        "rt_sarsa_td_device": (i, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
+        "rt_sarsa_apply": (i, [_P, _P]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):  # an older A/B variant build; EXPORTS is checked by tests

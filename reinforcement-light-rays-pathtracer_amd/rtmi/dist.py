@@ -22,3 +22,43 @@ def gather_tiles(out: torch.Tensor, gathered: torch.Tensor) -> torch.Tensor:
         return gathered
     dist.all_gather_into_tensor(gathered.view(world * out.shape[0], *out.shape[1:]), out)
     return gathered
+
+
+def sum_td(td_sum: torch.Tensor, td_count: torch.Tensor) -> None:
+    """Expected-SARSA frame exchange: sum every rank's TD accumulators in place
+    (int64 fixed-point target sums and int32 visit counts, [n_volumes*144]).
+    Integer sums are exact and order-free, so the Q-table every rank applies is
+    bit-identical to the single-GPU one for any world size."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(td_sum, op=dist.ReduceOp.SUM)
+        dist.all_reduce(td_count, op=dist.ReduceOp.SUM)
+
+
+class _DevArray:
+    """__cuda_array_interface__ view of a device buffer owned by librtmi."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def td_tensors(radiance_map, device: torch.device):
+    """torch views (no copy) of a RadianceMap's device TD accumulators."""
+    s, c, n = radiance_map.td_device()
+    ts = torch.as_tensor(_DevArray(s, n, "<i8"), device=device)
+    tc = torch.as_tensor(_DevArray(c, n, "<i4"), device=device)
+    return ts, tc
+
+
+def sarsa_frame(radiance_map, cam, params, tiles, tile_size: int, out: torch.Tensor, casts: torch.Tensor,
+                td=None) -> None:
+    """One multi-GPU SARSA frame: render this rank's tiles (TD sums left in the map),
+    all-reduce the TD sums over ranks, apply the shared update on every rank."""
+    stream = torch.cuda.current_stream(out.device).cuda_stream
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    radiance_map.render_tiles_device(cam, params, tiles, tile_size, out.data_ptr(), casts.data_ptr(),
+                                     apply=(world == 1), stream=stream)
+    if world > 1:
+        ts, tc = td if td is not None else td_tensors(radiance_map, out.device)
+        sum_td(ts, tc)
+        radiance_map.apply(stream)

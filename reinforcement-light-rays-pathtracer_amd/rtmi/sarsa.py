@@ -1,0 +1,106 @@
+"""Expected-SARSA radiance volumes (BASELINE config 3) on top of the C ABI.
+
+  RadianceMap(ctx, scene, seed)   rt_sarsa_create: volumes, Q-table, KD tree on the device
+  .render(cam, params, frames)    draw_reinforcement_path_tracing + update_radiance_volume_
+                                  distributions per frame (rt_render_sarsa)
+  .render_tiles_device(...)       one frame over a tile list; apply=False leaves the frame's TD
+                                  sums for a cross-GPU sum (rtmi.dist.sarsa_frame)
+  .read() / .volumes() / .nearest(pos, nrm)   Q-table, placement, KD queries (parity)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from ._lib import check, lib
+from .api import Context, Scene, _fp, _ip
+
+SECTORS = 144  # GRID_RESOLUTION^2
+
+KD_DTYPE = np.dtype([("dim", "<i4"), ("leaf", "<i4"), ("left", "<i4"), ("right", "<i4"), ("data", "<f4"),
+                     ("px", "<f4"), ("py", "<f4"), ("pz", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
+                     ("vol", "<i4")])
+
+
+class RadianceMap:
+    def __init__(self, ctx: Context, scene: Scene, seed: int = 1984):
+        self.ctx = ctx
+        self.scene = scene
+        self._h = ctypes.c_void_p()
+        check(lib().rt_sarsa_create(ctx.handle, scene.handle, seed, ctypes.byref(self._h)))
+        nv, nk, fr = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_uint32(0)
+        check(lib().rt_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk), ctypes.byref(fr)))
+        self.n_volumes, self.n_nodes = nv.value, nk.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def frames(self) -> int:
+        fr = ctypes.c_uint32(0)
+        check(lib().rt_sarsa_info(self._h, None, None, ctypes.byref(fr)))
+        return int(fr.value)
+
+    def volumes(self):
+        n = self.n_volumes
+        pos = np.zeros((n, 3), np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        surf = np.zeros(n, np.int32)
+        kd = np.zeros(self.n_nodes, KD_DTYPE)
+        check(lib().rt_sarsa_volumes(self._h, _fp(pos), _fp(nrm), _ip(surf), kd.ctypes.data_as(ctypes.c_void_p)))
+        return pos, nrm, surf, kd
+
+    def read(self):
+        """(Q, CDF, visits) as n x 144 and the irradiance estimate accumulators (n)."""
+        n = self.n_volumes
+        q = np.zeros((n, SECTORS), np.float32)
+        cdf = np.zeros((n, SECTORS), np.float32)
+        vis = np.zeros((n, SECTORS), np.uint32)
+        acc = np.zeros(n, np.float32)
+        check(lib().rt_sarsa_read(self._h, _fp(q), _fp(cdf), vis.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                  _fp(acc)))
+        return q, cdf, vis, acc
+
+    def nearest(self, pos: np.ndarray, nrm: np.ndarray) -> np.ndarray:
+        p = np.ascontiguousarray(pos, np.float32).reshape(-1, 3)
+        n_ = np.ascontiguousarray(nrm, np.float32).reshape(-1, 3)
+        out = np.zeros(p.shape[0], np.int32)
+        check(lib().rt_sarsa_nearest(self.ctx.handle, self._h, _fp(p), _fp(n_), p.shape[0], _ip(out)))
+        return out
+
+    def render(self, cam, params, frames: int = 1):
+        out = np.zeros((params.height, params.width, 3), np.float32)
+        casts = ctypes.c_uint64(0)
+        check(lib().rt_render_sarsa(self.ctx.handle, self.scene.handle, self._h, ctypes.byref(cam),
+                                    ctypes.byref(params), frames, _fp(out), ctypes.byref(casts)))
+        return out, int(casts.value)
+
+    def render_tiles_device(self, cam, params, tiles: np.ndarray, tile_size: int, out_ptr: int, casts_ptr: int,
+                            apply: bool, stream: int) -> None:
+        t = np.ascontiguousarray(tiles, np.int32).reshape(-1, 2)
+        check(lib().rt_render_sarsa_tiles_device(self.ctx.handle, self.scene.handle, self._h, ctypes.byref(cam),
+                                                 ctypes.byref(params), _ip(t), t.shape[0], tile_size,
+                                                 ctypes.c_void_p(out_ptr), ctypes.c_void_p(casts_ptr),
+                                                 int(bool(apply)), ctypes.c_void_p(stream)))
+
+    def td_device(self):
+        """Device pointers of the frame's TD sums (int64, fixed point 2^-32) and counts (uint32)."""
+        s, c, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_int64(0)
+        check(lib().rt_sarsa_td_device(self._h, ctypes.byref(s), ctypes.byref(c), ctypes.byref(n)))
+        return int(s.value or 0), int(c.value or 0), int(n.value)
+
+    def apply(self, stream: int = 0) -> None:
+        check(lib().rt_sarsa_apply(self._h, ctypes.c_void_p(stream)))
+
+    def close(self):
+        if self._h:
+            lib().rt_sarsa_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

@@ -14,6 +14,10 @@ Fixtures (all data, no reference source):
                          accept tests, as disassembled
   cornell_ref_stats.json block means of Images/cornell/*.png (statistical
                          reference renders of the GPU engine, 720x720)
+  sarsa_ref_stats.json   the reference's Expected-SARSA training statistics
+                         (Radiance_Map_Data/sarsa_*.txt, written per frame by
+                         GPU/main.cu:321-339: average path length, 0.0,
+                         zero-contribution light paths), per scene
 """
 import json
 import os
@@ -58,6 +62,19 @@ def main(ref):
     }
     with open(os.path.join(HERE, "triangle_o_pin.json"), "w") as f:
         json.dump(pin, f, indent=1)
+
+    sarsa = {}
+    for scene, fname in (("door_room", "sarsa_door_scene.txt"), ("archway", "sarsa_archway.txt"),
+                         ("cornell", "sarsa_cornell.txt"),
+                         ("complex_light_room", "sarsa_complex_light_scene.txt")):
+        rows = [line.split() for line in open(os.path.join(ref, "Radiance_Map_Data", fname)) if line.strip()]
+        sarsa[scene] = {"avg_path_length": [float(r[0]) for r in rows],
+                        "zero_contribution_paths": [int(float(r[2])) for r in rows]}
+    sarsa["_note"] = ("GPU engine, SCREEN 720x720 (constants/image_settings.h) and SAMPLES_PER_PIXEL 32 "
+                      "(constants/monte_carlo_settings.h) at HEAD; the settings of the recorded runs are "
+                      "not stated in the repository")
+    with open(os.path.join(HERE, "sarsa_ref_stats.json"), "w") as f:
+        json.dump(sarsa, f)
 
     try:
         import numpy as np

@@ -1,0 +1,297 @@
+"""Expected-SARSA radiance-volume path (BASELINE config 3).
+
+Parity levels:
+  * volume placement, KD array, nearest-volume queries: bit-exact with the oracle
+  * render + Q-table learning: bit-exact with the oracle (frame-synchronous TD with
+    integer fixed-point sums is order-free, so GPU and CPU agree to the last bit:
+    image, casts, Q, CDF, visits, irradiance)
+  * reference pin (statistical): first-frame average path length per scene vs the
+    reference's own training logs (Radiance_Map_Data/sarsa_*.txt -> golden
+    sarsa_ref_stats.json): the reference logs floor(mean over pixels of
+    floor(per-pixel mean)), i.e. about half a bounce below the true mean.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, MODELS
+
+SCENES = ("cornell", "door_room", "archway", "complex_light_room")
+
+
+def geometry(rtmi_mod, scene):
+    if scene == "cornell":
+        return rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    return rtmi_mod.obj_geometry(os.path.join(MODELS, scene + ".obj"), scene)
+
+
+def area_counts(tri):
+    """floor(area / 0.001) per triangle, Triangle::compute_area's arithmetic (numpy float32)"""
+    v = tri.reshape(-1, 3, 3).astype(np.float32)
+    a, b = v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]
+    dot = lambda x, y: (x[:, 0] * y[:, 0] + x[:, 1] * y[:, 1]) + x[:, 2] * y[:, 2]
+    e = np.sqrt(dot(a, a)) * np.sqrt(dot(b, b))
+    c = dot(a, b) / e
+    s = np.sqrt(1.0 - c.astype(np.float64) ** 2).astype(np.float32)
+    area = np.float32(0.5) * e * s
+    return np.floor(area / np.float32(0.001)).astype(np.int64)
+
+
+def leaves_under(kd, i, out):
+    stack = [i]
+    while stack:
+        j = stack.pop()
+        if kd["leaf"][j]:
+            out.append(int(kd["vol"][j]))
+        else:
+            stack += [int(kd["left"][j]), int(kd["right"][j])]
+    return out
+
+
+# ---------------------------------------------------------------- CPU ----------
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_oracle_volume_placement(rtmi_mod, oracle_mod, scene):
+    g = geometry(rtmi_mod, scene)
+    m = oracle_mod.Sarsa(g, 1984)
+    cnt = area_counts(g.tri)
+    assert m.n_volumes == int(cnt.sum()) > 0
+    pos, nrm, surf, kd = m.volumes()
+    assert np.array_equal(np.bincount(surf, minlength=g.n_surf), cnt)
+    assert np.all(np.diff(surf) >= 0)                       # surfaces in order
+    # on their triangle (barycentric a1 + a2 <= 1, both >= 0) with its normal
+    normals = oracle_mod.normals(g.all_triangles())
+    assert np.array_equal(nrm, normals[surf])
+    v = g.tri.reshape(-1, 3, 3)[surf].astype(np.float64)
+    e1, e2, d = v[:, 1] - v[:, 0], v[:, 2] - v[:, 0], pos - v[:, 0]
+    G = np.stack([e1, e2], 2)
+    ab = np.einsum("nij,nj->ni", np.linalg.pinv(G), d)
+    assert np.all(ab > -1e-4) and np.all(ab.sum(1) < 1 + 1e-4)
+
+
+@pytest.mark.parametrize("scene", ("door_room", "archway"))
+def test_oracle_kd_array(rtmi_mod, oracle_mod, scene):
+    """RadianceTree::convert_to_array form: children appended as pairs, every volume one
+    leaf, medians separate the subtrees on their dimension (x, y, z cycling)."""
+    m = oracle_mod.Sarsa(geometry(rtmi_mod, scene), 1984)
+    pos, _, _, kd = m.volumes()
+    n = m.n_volumes
+    assert m.n_nodes == 2 * n - 1
+    leaf = kd["leaf"].astype(bool)
+    assert np.array_equal(np.sort(kd["vol"][leaf]), np.arange(n))
+    assert np.array_equal(kd["data"][leaf], kd["vol"][leaf].astype(np.float32))
+    inner = np.nonzero(~leaf)[0]
+    assert np.all(kd["right"][inner] == kd["left"][inner] + 1)
+    assert np.array_equal(np.sort(kd["left"][inner]), np.arange(1, 2 * n - 1, 2))
+    assert kd["dim"][0] == 0 and kd["px"][0] == 0 and kd["py"][0] == 0 and kd["pz"][0] == 0
+    rng = np.random.default_rng(0)
+    for i in rng.choice(inner, 64, replace=False):
+        d, med = int(kd["dim"][i]), kd["data"][i]
+        L = leaves_under(kd, int(kd["left"][i]), [])
+        R = leaves_under(kd, int(kd["right"][i]), [])
+        assert pos[L, d].max() <= med <= pos[R, d].min()
+        assert 0 <= len(L) - len(R) <= 1                       # left takes the median
+        for c in (int(kd["left"][i]), int(kd["right"][i])):
+            assert kd["dim"][c] == (d + 1) % 3
+
+
+def test_oracle_nearest_self(rtmi_mod, oracle_mod):
+    m = oracle_mod.Sarsa(geometry(rtmi_mod, "door_room"), 1984)
+    pos, nrm, _, _ = m.volumes()
+    idx = np.random.default_rng(1).choice(m.n_volumes, 4000, replace=False)
+    got = m.nearest(pos[idx], nrm[idx])
+    assert np.array_equal(pos[got], pos[idx]) and np.array_equal(nrm[got], nrm[idx])
+
+
+def test_oracle_initial_state(rtmi_mod, oracle_mod):
+    m = oracle_mod.Sarsa(geometry(rtmi_mod, "door_room"), 1984)
+    q, cdf, vis, acc = m.read()
+    assert np.all(q == np.float32(np.float32(1 / np.float32(144)) * np.float32(100)))
+    k = np.arange(144, dtype=np.float32)
+    assert np.array_equal(cdf, np.broadcast_to(k * np.float32(1 / np.float32(144)), cdf.shape))
+    assert not vis.any()
+    assert np.all(acc > 0)
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_oracle_first_frame_path_length_matches_reference(rtmi_mod, oracle_mod, scene):
+    """Statistical pin: frame 0 (initial CDF) average path length vs the reference's log."""
+    ref = json.load(open(os.path.join(GOLDEN, "sarsa_ref_stats.json")))[scene]["avg_path_length"][0]
+    g = geometry(rtmi_mod, scene)
+    m = oracle_mod.Sarsa(g, 1984)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=48, spp=8)
+    _, casts = m.render(oracle_mod.camera(rtmi_mod.CAMERAS[scene]), oracle_mod.params_from(p), 1)
+    mean = casts / (48 * 48 * 8)
+    assert ref - 0.5 <= mean <= ref + 2.5, (scene, mean, ref)
+
+
+def test_oracle_learning_shortens_paths(rtmi_mod, oracle_mod):
+    m = oracle_mod.Sarsa(geometry(rtmi_mod, "door_room"), 1984)
+    p = oracle_mod.params_from(rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=8))
+    cam = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    lens = [m.render(cam, p, 1)[1] / (64 * 64 * 8) for _ in range(4)]
+    assert lens[3] < lens[0] * 0.8, lens
+    q, cdf, vis, _ = m.read()
+    assert vis.sum() > 0 and np.all(q >= np.float32(1 / np.float32(144)) * np.float32(0.8))
+    assert np.all(np.diff(cdf, axis=1) >= 0) and np.all(np.abs(cdf[:, -1] - 1) < 1e-4)
+
+
+def test_oracle_threads_and_split_do_not_change_learning(rtmi_mod, oracle_mod):
+    """Integer TD sums: the Q-table is independent of thread count and spp_split."""
+    g = geometry(rtmi_mod, "door_room")
+    cam = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    res = []
+    n0 = oracle_mod.num_threads()
+    try:
+        for threads, split in ((1, 1), (n0, 1), (n0, 4)):
+            oracle_mod.set_threads(threads)
+            m = oracle_mod.Sarsa(g, 1984)
+            p = oracle_mod.params_from(rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=24, height=24,
+                                                               spp=8, spp_split=split))
+            img, casts = m.render(cam, p, 2)
+            res.append((img, casts) + m.read())
+    finally:
+        oracle_mod.set_threads(n0)
+    for r in res[1:]:
+        assert r[1] == res[0][1]
+        for a, b in zip(r[2:], res[0][2:]):
+            assert np.array_equal(a, b)
+    assert np.array_equal(res[1][0], res[0][0])
+
+
+# ---------------------------------------------------------------- GPU ----------
+
+def _both(rtmi_mod, oracle_mod, gpu_ctx, scene, seed=1984):
+    g = geometry(rtmi_mod, scene)
+    sc = rtmi_mod.Scene(gpu_ctx, g)
+    return g, sc, rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, seed), oracle_mod.Sarsa(g, seed)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", SCENES)
+def test_gpu_map_build_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene):
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    try:
+        assert (rm.n_volumes, rm.n_nodes) == (om.n_volumes, om.n_nodes)
+        for a, b in zip(rm.volumes(), om.volumes()):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+        for a, b in zip(rm.read(), om.read()):
+            assert np.array_equal(a, b)
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ("door_room", "complex_light_room"))
+def test_gpu_nearest_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene):
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    try:
+        pos, nrm, _, _ = om.volumes()
+        rng = np.random.default_rng(5)
+        n = 200_000
+        i = rng.integers(0, om.n_volumes, n)
+        q = pos[i] + rng.normal(0, 0.02, (n, 3)).astype(np.float32)   # near the surfaces
+        qn = nrm[i].copy()
+        qn[: n // 10] = nrm[rng.integers(0, om.n_volumes, n // 10)]   # mismatched normals
+        a = rm.nearest(q, qn)
+        b = om.nearest(q, qn)
+        assert np.array_equal(a, b)
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,split,hit_rule", [("door_room", 1, 1), ("door_room", 4, 1), ("cornell", 2, 1),
+                                                   ("archway", 1, 0)])
+def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, split, hit_rule):
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    try:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=40, spp=8, spp_split=split,
+                                    hit_rule=hit_rule)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+        for frames in (1, 2):
+            img_g, casts_g = rm.render(cam, p, frames)
+            img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS[scene]), oracle_mod.params_from(p),
+                                       frames)
+            assert casts_g == casts_o
+            assert np.array_equal(img_g, img_o)
+            for a, b in zip(rm.read(), om.read()):
+                assert np.array_equal(a, b)
+        assert rm.frames == 3
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_tiles_and_td_exchange_equal_single_map(rtmi_mod, gpu_ctx):
+    """Two maps rendering disjoint tile sets, TD sums added on the device, then applied on
+    both == one map rendering the whole frame (the multi-GPU exchange, in one process)."""
+    import torch
+    from rtmi import dist as rdist, tiles as rtiles
+    g = geometry(rtmi_mod, "door_room")
+    sc = rtmi_mod.Scene(gpu_ctx, g)
+    W = H = 64
+    T = 32
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=W, height=H, spp=8, spp_split=2)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    maps = [rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) for _ in range(3)]
+    dev = torch.device("cuda", 0)
+    try:
+        origins = rtiles.tile_origins(W, H, T)
+        full = torch.zeros(len(origins), T, T, 3, device=dev)
+        casts = torch.zeros(1, dtype=torch.int64, device=dev)
+        maps[0].render_tiles_device(cam, p, origins, T, full.data_ptr(), casts.data_ptr(), True, 0)
+        parts = []
+        for r in (0, 1):
+            mine = rtiles.rank_tiles(len(origins), 2, r)
+            out = torch.zeros(len(mine), T, T, 3, device=dev)
+            maps[1 + r].render_tiles_device(cam, p, origins[mine], T, out.data_ptr(), casts.data_ptr(), False, 0)
+            parts.append((mine, out))
+        (s1, c1), (s2, c2) = [rdist.td_tensors(m, dev) for m in maps[1:]]
+        tot_s, tot_c = s1 + s2, c1 + c2
+        s1.copy_(tot_s), c1.copy_(tot_c), s2.copy_(tot_s), c2.copy_(tot_c)
+        maps[1].apply(0)
+        maps[2].apply(0)
+        torch.cuda.synchronize()
+        ref = maps[0].read()
+        for m in maps[1:]:
+            for a, b in zip(m.read(), ref):
+                assert np.array_equal(a, b)
+        for mine, out in parts:
+            assert torch.equal(out, full[mine])
+    finally:
+        for m in maps:
+            m.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_full_size_door_room_properties(rtmi_mod, gpu_ctx):
+    """BASELINE config 3 size (512^2, 256 spp per frame): finite image, reference-like
+    first-frame path length, learning shortens paths, Q/CDF invariants."""
+    ref = json.load(open(os.path.join(GOLDEN, "sarsa_ref_stats.json")))["door_room"]["avg_path_length"]
+    g = geometry(rtmi_mod, "door_room")
+    sc = rtmi_mod.Scene(gpu_ctx, g)
+    rm = rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984)
+    try:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=512, height=512, spp=256, spp_split=8)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+        lens = []
+        for _ in range(3):
+            img, casts = rm.render(cam, p, 1)
+            lens.append(casts / (512 * 512 * 256))
+            assert np.isfinite(img).all() and (img >= 0).all()
+        assert ref[0] - 0.5 <= lens[0] <= ref[0] + 2.5
+        assert lens[2] < lens[0] * 0.6, lens
+        q, cdf, vis, acc = rm.read()
+        assert np.all(q >= np.float32(1 / np.float32(144)) * np.float32(0.8))
+        assert np.all(np.diff(cdf, axis=1) >= 0) and np.all(np.abs(cdf[:, -1] - 1) < 1e-4)
+        assert np.isfinite(acc).all()
+    finally:
+        rm.close()
+        sc.close()
