@@ -88,6 +88,9 @@ ORC_API void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2
 
 /* uniform float in [0,1): top 24 bits */
 static float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+/* (0, 1], curand_uniform's range: the SARSA sector draws (r = 0 would pick sector 0 of a
+ * zero-mass CDF prefix, which the reference's curand cannot) */
+static float u01_oc(uint32_t x) { return (float)((x >> 8) + 1u) * 0x1p-24f; }
 
 /* two uniforms for (pixel, sample, event) */
 static void draw2(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t event, float *a, float *b) {
@@ -873,7 +876,7 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
  * running mean of alpha = 1/(1 + visits), clamped at 0.8/144.
  * RNG: volume placement counter (volume, attempt, 0xFFFF0001, 0), u01 of words
  * 0,1; sampling at bounce i counter (pixel, frame*spp + sample, 1+i, 0): words
- * 0,1,2 = r (sector), rx, ry (uniform fallback: words 0,1).
+ * 0,1,2 = r (sector), rx, ry in (0,1] like curand_uniform (uniform fallback: words 0,1).
  */
 void orc_kd_sort(int32_t *v, int n, const float *pos4, int dim); /* orc_sort.cpp */
 
@@ -1236,7 +1239,7 @@ static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t 
             float ct;
             sd = sample_dir(nrm, u01(rn[0]), u01(rn[1]), 0, &ct);
             pdf = RHO;
-        } else if (!sarsa_sample(m, cur_rv, u01(rn[0]), u01(rn[1]), u01(rn[2]), &cur_sector, &sd, &pdf)) {
+        } else if (!sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf)) {
             if (i + 1 >= p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
             (*casts)++; /* the zero direction is traced and misses */
             return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);

@@ -122,7 +122,12 @@ hipError_t launch_dqn_sample_only(const DeviceScene& s, const float* q, const fl
                                   float* dir_out, int32_t* action, hipStream_t stream);
 
 // ---- Expected-SARSA radiance volumes (BASELINE config 3) ----
-// Flattened KD tree of GPU/radiance_volumes/radiance_tree.cuh:19-27 (48 B per node).
+// Flattened KD tree of GPU/radiance_volumes/radiance_tree.cuh:19-27 (48 B per node):
+// the host/export form.  The device form is 16 B per node in the same order (kd4), so
+// a subtree's nodes, leaf positions included, are contiguous (the reference's layout
+// appends a node's two children together, then the left subtree, then the right):
+//   internal: {median bits, left child (right = left + 1), split dimension, 0xFFFFFFFF}
+//   leaf:     {x, y, z (float bits), volume index}; its normal is vol_frame[3 * volume].
 struct KdNode {
     int dim, leaf, left, right;
     float data;          // split median (internal) or volume index (leaf, as float like the reference)
@@ -147,10 +152,12 @@ struct SarsaMap {
     float* accum = nullptr;             // [n] irradiance_accum
     unsigned long long* acc_sum = nullptr;  // [n*144] frame TD targets, fixed point 2^-32
     uint32_t* acc_cnt = nullptr;            // [n*144] frame TD target count
-    const KdNode* kd = nullptr;
+    const uint4* kd4 = nullptr;         // [n_kd] device KD array (above)
     int n_kd = 0;
+    float root_x = 0.f, root_y = 0.f, root_z = 0.f;  // position of KD element 0 (0 if internal)
     float max_dist = 0.003f;            // MAX_DIST (compared with delta^2)
 };
+constexpr int kKdStack = 32;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
 
 hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);

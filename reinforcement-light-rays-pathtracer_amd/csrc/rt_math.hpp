@@ -69,6 +69,9 @@ RT_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
 
 // 24-bit uniform in [0, 1)
 RT_HD float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+// 24-bit uniform in (0, 1], the range of curand_uniform (the SARSA sector draws: r = 0
+// would select sector 0 of an all-zero-mass CDF prefix, which curand cannot)
+RT_HD float u01_oc(uint32_t x) { return (float)((x >> 8) + 1u) * 0x1p-24f; }
 
 // sin(2*pi*r), cos(2*pi*r) by quarter-turn reduction (exact) and Taylor
 // polynomials of sin(pi/2 f), cos(pi/2 f) on f in [-1/2, 1/2] (Horner, no FMA).

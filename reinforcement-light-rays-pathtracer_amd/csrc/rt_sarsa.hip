@@ -19,6 +19,15 @@
 
 #include "rt_trace.hpp"
 
+// A/B knobs (timing only; both change results): RT_SARSA_NO_TD drops the TD atomics,
+// RT_SARSA_NO_KD replaces the nearest-volume search by volume 0
+#ifndef RT_SARSA_NO_TD
+#define RT_SARSA_NO_TD 0
+#endif
+#ifndef RT_SARSA_NO_KD
+#define RT_SARSA_NO_KD 0
+#endif
+
 namespace rt {
 
 namespace {
@@ -31,35 +40,37 @@ __device__ __forceinline__ float len3(float x, float y, float z) { return sqrtf(
 
 // find_closest_radiance_volume_iterative (radiance_map.cu:149-203): explicit-stack
 // KD descent; a far child is visited when delta^2 < MAX_DIST; leaves need an
-// identical normal; the search starts from volume 0 at the distance of the root
-// element's position (the origin for an internal root).
-__device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm) {
-    const KdNode* __restrict__ kd = m.kd;
+// identical normal; the search starts from volume 0 at the distance of element 0's
+// position (the origin for an internal root).  The stack lives in LDS, one column per
+// lane (st[k * 256]); its depth is bounded by the tree depth (host-checked).
+__device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
+    if (RT_SARSA_NO_KD) return 0;
+    const uint4* __restrict__ kd = m.kd4;
     int best = 0;
-    float best_d = len3(pos.x - kd[0].px, pos.y - kd[0].py, pos.z - kd[0].pz);
-    int stack[64];
-    int sp = 0;
-    stack[sp++] = 0;
+    float best_d = len3(pos.x - m.root_x, pos.y - m.root_y, pos.z - m.root_z);
+    st[0] = 0;
+    int sp = 1;
     while (sp > 0) {
-        const KdNode nd = kd[stack[--sp]];
-        if (nd.leaf) {
-            const float d = len3(nd.px - pos.x, nd.py - pos.y, nd.pz - pos.z);
-            if (nrm.x == nd.nx && nrm.y == nd.ny && nrm.z == nd.nz && d < best_d) {
-                best = nd.vol;
-                best_d = d;
+        --sp;
+        const uint4 nd = kd[st[sp * 256]];
+        if (nd.w != 0xFFFFFFFFu) {  // leaf
+            const float d = len3(__uint_as_float(nd.x) - pos.x, __uint_as_float(nd.y) - pos.y,
+                                 __uint_as_float(nd.z) - pos.z);
+            if (d < best_d) {
+                const float4 n4 = m.vol_frame[nd.w * 3];
+                if (nrm.x == n4.x && nrm.y == n4.y && nrm.z == n4.z) {
+                    best = (int)nd.w;
+                    best_d = d;
+                }
             }
         } else {
-            const float pc = (nd.dim == 0) ? pos.x : ((nd.dim == 1) ? pos.y : pos.z);
-            const float delta = pc - nd.data;
+            const float pc = (nd.z == 0u) ? pos.x : ((nd.z == 1u) ? pos.y : pos.z);
+            const float delta = pc - __uint_as_float(nd.x);
             const bool near_split = (delta * delta) < m.max_dist;
-            if (sp + 2 > 64) break;  // the reference's Stack is 30 deep; this one cannot overflow at depth <= 31
-            if (delta < 0.0f) {
-                if (near_split) stack[sp++] = nd.right;
-                stack[sp++] = nd.left;
-            } else {
-                if (near_split) stack[sp++] = nd.left;
-                stack[sp++] = nd.right;
-            }
+            const int left = (int)nd.y;
+            const int nearc = delta < 0.0f ? left : left + 1;
+            if (near_split) st[(sp++) * 256] = (left + left + 1) - nearc;
+            st[(sp++) * 256] = nearc;
         }
     }
     return best;
@@ -105,6 +116,7 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
 }
 
 __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, float target) {
+    if (RT_SARSA_NO_TD) return;
     const long long v = __float2ll_rn(target * 4294967296.0f);
     const size_t k = (size_t)rv * kSarsaSectors + sector;
     atomicAdd(&m.acc_sum[k], (unsigned long long)v);
@@ -128,6 +140,8 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     const float4* __restrict__ shade = a.scene.shade;
     const int n_surf = a.scene.n_surf, n_tri = a.scene.n_tri;
     const int s_end = (chunk + 1) * a.per_chunk;
+    __shared__ int kd_stack[kKdStack * 256];
+    int* const st = kd_stack + threadIdx.x;
 
     int s = valid ? chunk * a.per_chunk : s_end;
     int depth = 0;
@@ -165,7 +179,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
                 } else if (!is_surf) {
                     target = cur_brdf * m.tri_lum[h.tri];
                 } else {
-                    next_rv = sarsa_nearest(m, pos, nrm);
+                    next_rv = sarsa_nearest(m, pos, nrm, st);
                     target = (m.accum[next_rv] * kIrrScale) * cur_brdf;
                 }
                 td_event(m, cur_rv, cur_sector, target);
@@ -173,7 +187,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
                 cur_sector = -1;
             }
         } else if (is_surf) {
-            cur_rv = sarsa_nearest(m, pos, nrm);
+            cur_rv = sarsa_nearest(m, pos, nrm, st);
         }
         bool terminal = false;
         f3 L = make3(0.f, 0.f, 0.f);
@@ -201,7 +215,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
                            (sx * B4.z + c * nrm.z) + sz * T4.z);
                 pdf = kRho;
             } else {
-                ok = sarsa_sample(m, cur_rv, u01(rn[0]), u01(rn[1]), u01(rn[2]), &cur_sector, &sd, &pdf);
+                ok = sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
             }
             if (!ok) {
                 // no sector: the reference traces the zero direction it returns, which
@@ -310,10 +324,11 @@ __global__ __launch_bounds__(256) void k_sarsa_apply(const SarsaMap m) {
 // nearest-volume queries alone (KD parity): pos/nrm [n][3]
 __global__ __launch_bounds__(256) void k_sarsa_nearest(const SarsaMap m, const float* __restrict__ pos,
                                                        const float* __restrict__ nrm, int n, int32_t* out) {
+    __shared__ int kd_stack[kKdStack * 256];
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     out[i] = sarsa_nearest(m, make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]),
-                           make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]));
+                           make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]), kd_stack + threadIdx.x);
 }
 
 }  // namespace

@@ -41,7 +41,7 @@ int err(int code, const std::string& m) { return rt::set_error(code, m.c_str());
 constexpr float kAreaPerSample = 0.001f;  // AREA_PER_SAMPLE (radiance_volumes_settings.h:12)
 constexpr float kInitialRadiance = (1.f / ((float)rt::kGridRes * (float)rt::kGridRes)) * 100.f;  // :16
 constexpr uint32_t kPlacementEvent = 0xFFFF0001u;  // RNG counter word 2 of volume placement
-constexpr int kMaxKdDepth = 30;                  // k_sarsa_render's traversal stack holds 64 entries
+constexpr int kMaxKdDepth = rt::kKdStack - 1;    // the traversal stack holds depth + 1 entries
 
 // Triangle::compute_area (GPU/objects/triangle.cu:17-27): float lengths and
 // cosine; 1 - pow(cos, 2) and its sqrt in double (host pow promotes).
@@ -309,7 +309,22 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
           *d_acc = nullptr;
     uint32_t *d_vis = nullptr, *d_cnt = nullptr;
     unsigned long long* d_sum = nullptr;
-    rt::KdNode* d_kd = nullptr;
+    uint4* d_kd = nullptr;
+    std::vector<uint4> kd4(sa->kd.size());
+    for (size_t i = 0; i < sa->kd.size(); ++i) {
+        const rt::KdNode& k = sa->kd[i];
+        if (k.leaf) {
+            memcpy(&kd4[i].x, &k.px, 4);
+            memcpy(&kd4[i].y, &k.py, 4);
+            memcpy(&kd4[i].z, &k.pz, 4);
+            kd4[i].w = (uint32_t)k.vol;
+        } else {
+            memcpy(&kd4[i].x, &k.data, 4);
+            kd4[i].y = (uint32_t)k.left;
+            kd4[i].z = (uint32_t)k.dim;
+            kd4[i].w = 0xFFFFFFFFu;
+        }
+    }
     const size_t nS = (size_t)n * S;
     if (e == hipSuccess) e = sa->alloc(&d_pos, n);
     if (e == hipSuccess) e = sa->alloc(&d_frame, (size_t)n * 3);
@@ -336,7 +351,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     up(d_Q, Q.data(), sizeof(float) * nS);
     up(d_cdf, cdf.data(), sizeof(float) * nS);
     up(d_acc, accum.data(), sizeof(float) * n);
-    up(d_kd, sa->kd.data(), sizeof(rt::KdNode) * sa->kd.size());
+    up(d_kd, kd4.data(), sizeof(uint4) * kd4.size());
     if (e == hipSuccess) e = hipMemset(d_vis, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_sum, 0, sizeof(unsigned long long) * nS);
@@ -358,8 +373,11 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     m.accum = d_acc;
     m.acc_sum = d_sum;
     m.acc_cnt = d_cnt;
-    m.kd = d_kd;
+    m.kd4 = d_kd;
     m.n_kd = (int)sa->kd.size();
+    m.root_x = sa->kd[0].px;
+    m.root_y = sa->kd[0].py;
+    m.root_z = sa->kd[0].pz;
     *out = sa;
     return RT_OK;
 }

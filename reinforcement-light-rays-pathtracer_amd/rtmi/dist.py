@@ -50,13 +50,14 @@ def td_tensors(radiance_map, device: torch.device):
     return ts, tc
 
 
-def sarsa_frame(radiance_map, cam, params, tiles, tile_size: int, out: torch.Tensor, casts: torch.Tensor,
-                td=None) -> None:
-    """One multi-GPU SARSA frame: render this rank's tiles (TD sums left in the map),
-    all-reduce the TD sums over ranks, apply the shared update on every rank."""
+def sarsa_frame(radiance_map, cam, params, tiles, n_real: int, tile_size: int, out: torch.Tensor,
+                casts: torch.Tensor, td=None) -> None:
+    """One multi-GPU SARSA frame: render this rank's n_real real tiles (the padding slots
+    of `tiles` are left untouched so no pixel is learned from twice; TD sums stay in the
+    map), all-reduce the TD sums over ranks, apply the shared update on every rank."""
     stream = torch.cuda.current_stream(out.device).cuda_stream
     world = dist.get_world_size() if dist.is_initialized() else 1
-    radiance_map.render_tiles_device(cam, params, tiles, tile_size, out.data_ptr(), casts.data_ptr(),
+    radiance_map.render_tiles_device(cam, params, tiles[:n_real], tile_size, out.data_ptr(), casts.data_ptr(),
                                      apply=(world == 1), stream=stream)
     if world > 1:
         ts, tc = td if td is not None else td_tensors(radiance_map, out.device)

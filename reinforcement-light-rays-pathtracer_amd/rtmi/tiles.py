@@ -33,6 +33,13 @@ def rank_tiles(width: int, height: int, tile: int, rank: int, world: int) -> np.
     return np.ascontiguousarray(mine, np.int32)
 
 
+def rank_tile_count(width: int, height: int, tile: int, rank: int, world: int) -> int:
+    """Number of real (non-padding) tiles among rank_tiles(...): padding repeats a tile,
+    which is harmless for a pure render but must not be rendered twice by a learning
+    renderer (Expected SARSA would count its TD targets twice)."""
+    return len(tile_origins(width, height, tile)[rank::world])
+
+
 def assemble(gathered: np.ndarray, width: int, height: int, tile: int, world: int) -> np.ndarray:
     """gathered: (world, k, tile, tile, 3) per-rank tile buffers -> (height, width, 3)."""
     allt = tile_origins(width, height, tile)

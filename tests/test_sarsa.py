@@ -248,10 +248,11 @@ def test_gpu_tiles_and_td_exchange_equal_single_map(rtmi_mod, gpu_ctx):
         maps[0].render_tiles_device(cam, p, origins, T, full.data_ptr(), casts.data_ptr(), True, 0)
         parts = []
         for r in (0, 1):
-            mine = rtiles.rank_tiles(len(origins), 2, r)
+            mine = np.arange(r, len(origins), 2)
+            assert np.array_equal(rtiles.rank_tiles(W, H, T, r, 2), origins[mine])
             out = torch.zeros(len(mine), T, T, 3, device=dev)
             maps[1 + r].render_tiles_device(cam, p, origins[mine], T, out.data_ptr(), casts.data_ptr(), False, 0)
-            parts.append((mine, out))
+            parts.append((torch.from_numpy(mine).to(dev), out))
         (s1, c1), (s2, c2) = [rdist.td_tensors(m, dev) for m in maps[1:]]
         tot_s, tot_c = s1 + s2, c1 + c2
         s1.copy_(tot_s), c1.copy_(tot_c), s2.copy_(tot_s), c2.copy_(tot_c)

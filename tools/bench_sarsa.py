@@ -28,7 +28,10 @@ def main():
     ap.add_argument("--split", type=int, default=8)
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--lib", default=None, help="librtmi.so variant directory (A/B timing)")
     args = ap.parse_args()
+    if args.lib:
+        rtmi._lib.LIB_PATH = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", args.lib, "librtmi.so")
     if args.scene == "cornell":
         g = rtmi.cornell_geometry(rtmi.RT_PRESET_GPU)
     else:
@@ -59,7 +62,7 @@ def main():
                        "image_mean": round(float(out.mean().item()), 5)})
         print(json.dumps(frames[-1]), file=sys.stderr, flush=True)
     q, cdf, vis, acc = rm.read()
-    res = {"scene": args.scene, "width": args.width, "spp": args.spp, "volumes": rm.n_volumes,
+    res = {"lib": args.lib or "build", "scene": args.scene, "width": args.width, "spp": args.spp, "volumes": rm.n_volumes,
            "frames": frames, "visits": int(vis.sum()), "q_max": float(q.max()),
            "finite": bool(np.isfinite(out.cpu().numpy()).all())}
     print(json.dumps(res))

@@ -12,5 +12,6 @@ run() {  # name limit cmd...
   return 0
 }
 run smoke 150 python -c "import __graft_entry__ as g; g.smoke()"
-run pytest_gpu 480 python -m pytest tests -x -q -m gpu
+run pytest_gpu 600 python -m pytest tests -q -m gpu
 run bench 240 python bench.py --steps 10 --warmup 2
+run bench_sarsa 240 python tools/bench_sarsa.py --frames 4
