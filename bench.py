@@ -38,6 +38,10 @@ import rtmi  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
 TILE = 32
+# HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
+# (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
+PMC_PROFILE = os.path.join("profiles", "r1v3_pmc.json")
+DEFAULT_WORKLOAD = (512, 512, 256, 8)
 
 
 def parse():
@@ -53,6 +57,20 @@ def parse():
                     help="target CPU-baseline sample duration (0 disables)")
     ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
+
+
+def pmc_traffic(params):
+    """(bytes per launch, source) of the committed PMC profile for the default workload."""
+    if (params.width, params.height, params.spp, params.spp_split) != DEFAULT_WORKLOAD:
+        return None, None
+    try:
+        prof = json.load(open(os.path.join(ROOT, PMC_PROFILE)))
+    except (OSError, ValueError):
+        return None, None
+    for name, e in prof.get("selected", {}).items():
+        if "k_render<0, 0, 0>" in name and "traffic_bytes_per_launch" in e:
+            return int(e["traffic_bytes_per_launch"]), PMC_PROFILE
+    return None, None
 
 
 def cpu_baseline(geom, params, cam_pos, seconds):
@@ -170,6 +188,7 @@ def main():
         casts_per_launch = rank_casts / args.steps
         achieved_gbs = casts_per_launch * b_cast / (kernel_ms * 1e-3) / 1e9
         valu_tflops = casts_per_launch * n_tri * 71 / (kernel_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(params)
         line = {
             "metric": "Mrays/sec (Cornell 512^2 256spp ray casts)",
             "value": round(total_casts / elapsed / 1e6, 2),
@@ -197,7 +216,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "k_render<0,0,0>",
                 "kernel_ms": round(kernel_ms, 4),
                 "bytes_per_cast": b_cast,
