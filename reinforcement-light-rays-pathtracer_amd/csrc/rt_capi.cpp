@@ -4,6 +4,8 @@
 
 #include <math.h>
 #include <stdarg.h>
+
+#include <cmath>
 #include <stdio.h>
 #include <string.h>
 
@@ -187,7 +189,64 @@ rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const 
     a.sin_y = (float)sin((double)cam->yaw_y);
     a.cos_x = (float)cos((double)cam->yaw_x);
     a.sin_x = (float)sin((double)cam->yaw_x);
+    a.use_filter = rt::filter_usable(a.scene, a.cam_x, a.cam_y, a.cam_z, a.t_scale);
     return a;
+}
+
+// float >= x (x finite, >= 0)
+float round_up(double x) {
+    const float f = (float)x;
+    return ((double)f >= x) ? f : nextafterf(f, INFINITY);
+}
+
+// Filter record of one triangle for closest_hit_filtered (rt_trace.hpp; layout in
+// rt_internal.hpp).  The filter may reject a (ray, triangle) pair only if the exact
+// test must fail, so its margins bound the difference between the two evaluations of
+// each quantity, for |d_i| <= 2, |o_i| <= obound, t_scale <= kFiltMaxTScale.  With
+// u = 2^-24, both the exact float Cramer evaluation (GLM order, incl. the rounding of
+// b = o - v0 and of -t_scale*d) and the FMA evaluation on the double-rounded records
+// are within 16u of the sum of the absolute values of the products involved:
+//   A = d.N:           S_A = 2 M,            M = sum_i |e1_j e2_k| + |e1_k e2_j|
+//   T = w0 - o.N:      S_T = B M,            B = obound + max_i |v0_i|
+//   U = e2.R - d.G2:   S_U = 2 * 2 B |e2|_1  (R = d x o)
+//   V = -e1.R + d.G1:  S_V = 2 * 2 B |e1|_1
+// (all scaled by 1/t_scale where the exact evaluation carries t_scale).  The margins
+// use c = 2^-16 = 256u, 16x that, plus an absolute floor F = 2^-90 that keeps a
+// rejected u, v, t away from the underflow to -0 (which would pass ">= 0"):
+//   eA = c S_A + F                          sign of A certain when |A~| > eA
+//   EW = 2 (c S_U + c S_V + eA) + F         u < 0, v < 0 or u + v > 1 certain
+//   ET = c S_T + 2 eps kFiltMaxTScale eA + F  t <= eps (RULE 0) / t < 0 certain
+// Returns false outside the ranges where F stays negligible (huge coordinates).
+bool build_filter(const float4& P0, const float4& P1, const float4& P2, double obound, float4* out) {
+    const double v0[3] = {P0.x, P0.y, P0.z};
+    const double a[3] = {P1.x, P1.y, P1.z};  // e1
+    const double b[3] = {P2.x, P2.y, P2.z};  // e2
+    double N[3], G1[3], G2[3], M = 0.0, vmax = 0.0, n1 = 0.0, n2 = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        N[i] = a[j] * b[k] - a[k] * b[j];
+        M += fabs(a[j] * b[k]) + fabs(a[k] * b[j]);
+        G1[i] = v0[j] * a[k] - v0[k] * a[j];
+        G2[i] = v0[j] * b[k] - v0[k] * b[j];
+        vmax = fmax(vmax, fabs(v0[i]));
+        n1 += fabs(a[i]);
+        n2 += fabs(b[i]);
+    }
+    const float Nf[3] = {(float)N[0], (float)N[1], (float)N[2]};
+    const double w0 = v0[0] * Nf[0] + v0[1] * Nf[1] + v0[2] * Nf[2];
+    const double B = obound + vmax;
+    const double c = ldexp(1.0, -16), F = ldexp(1.0, -90), dinf = 2.0;
+    const double eA = c * dinf * M + F;
+    const double EW = 2.0 * (c * 2.0 * dinf * B * n2 + c * 2.0 * dinf * B * n1 + eA) + F;
+    const double ET = c * B * M + 2.0 * 1e-5 * (double)rt::kFiltMaxTScale * eA + F;
+    if (!(M < ldexp(1.0, 36)) || !(B < ldexp(1.0, 20)) || !std::isfinite(EW) || !std::isfinite(ET))
+        return false;
+    out[0] = make_float4(Nf[0], Nf[1], Nf[2], (float)w0);
+    out[1] = make_float4(P2.x, P2.y, P2.z, round_up(eA));
+    out[2] = make_float4((float)-G2[0], (float)-G2[1], (float)-G2[2], round_up(EW));
+    out[3] = make_float4(-P1.x, -P1.y, -P1.z, round_up(ET));
+    out[4] = make_float4((float)G1[0], (float)G1[1], (float)G1[2], 0.0f);
+    return true;
 }
 
 }  // namespace
@@ -320,11 +379,23 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
             code_cpu[i] = code_gpu[i] = (int32_t)((RT_HIT_TYPE_SURFACE << 30) | (uint32_t)j);
         }
     }
+    // Filter records (two-phase hit test).  Origin bound: every surface point, plus room
+    // for a camera outside the scene (a camera beyond it gets the single-phase scan).
+    double vmax = 0.0;
+    for (float v : sc->tri) vmax = fmax(vmax, fabs((double)v));
+    const double obound = fmax(8.0, 2.0 * vmax + 1.0);
+    std::vector<float4> filt((size_t)n * rt::kFiltF4);
+    bool filt_ok = true;
+    for (int i = 0; i < n && filt_ok; ++i)
+        filt_ok = build_filter(isect[(size_t)i * 3 + 0], isect[(size_t)i * 3 + 1], isect[(size_t)i * 3 + 2],
+                               obound, &filt[(size_t)i * rt::kFiltF4]);
     sc->dev.n_surf = n_surf;
     sc->dev.n_tri = n;
+    sc->dev.origin_bound = (float)obound;
     auto cleanup = [&]() {
         if (sc->dev.isect) (void)hipFree(sc->dev.isect);
         if (sc->dev.shade) (void)hipFree(sc->dev.shade);
+        if (sc->dev.filt) (void)hipFree(sc->dev.filt);
         if (sc->dev.code_cpu) (void)hipFree(sc->dev.code_cpu);
         if (sc->dev.code_gpu) (void)hipFree(sc->dev.code_gpu);
         delete sc;
@@ -337,6 +408,11 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     if (e == hipSuccess) e = hipMemcpy(sc->dev.shade, shade.data(), sizeof(float4) * shade.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(sc->dev.code_cpu, code_cpu.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(sc->dev.code_gpu, code_gpu.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && filt_ok) {
+        e = hipMalloc(&sc->dev.filt, sizeof(float4) * filt.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->dev.filt, filt.data(), sizeof(float4) * filt.size(), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         cleanup();
         return fail(RT_E_HIP, "scene upload failed: %s", hipGetErrorString(e));
@@ -352,6 +428,7 @@ int rt_scene_destroy(rt_scene* scene) {
     (void)hipFree(scene->dev.shade);
     (void)hipFree(scene->dev.code_cpu);
     (void)hipFree(scene->dev.code_gpu);
+    if (scene->dev.filt) (void)hipFree(scene->dev.filt);
     delete scene;
     return RT_OK;
 }
@@ -370,7 +447,8 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
     if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
-    RT_HIP(rt::launch_intersect(scene->dev, d_orig, d_dir, n, t_scale, hit_rule, d_t, d_hit,
+    // device rays of unknown range: the single-phase scan (no filter bounds to rely on)
+    RT_HIP(rt::launch_intersect(scene->dev, d_orig, d_dir, n, t_scale, hit_rule, 0, d_t, d_hit,
                                 (hipStream_t)stream));
     return RT_OK;
 }
@@ -393,7 +471,15 @@ int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig, const fl
     if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(int32_t) * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_o, orig, b3, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_d, dir, b3, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, d_t, d_h, 0);
+    // the two-phase hit test when every ray is inside the filter's bounds
+    float omax = 0.0f, dmax = 0.0f;
+    for (size_t k = 0; k < 3 * (size_t)n; ++k) {
+        omax = fmaxf(omax, fabsf(orig[k]));  // NaN: fmaxf keeps omax; NaN rays never reject
+        dmax = fmaxf(dmax, fabsf(dir[k]));
+    }
+    const int use_filter = (dmax <= 2.0f) ? rt::filter_usable(scene->dev, omax, 0.0f, 0.0f, t_scale) : 0;
+    if (e == hipSuccess)
+        e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, use_filter, d_t, d_h, 0);
     if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
     (void)hipFree(d_o);

@@ -246,7 +246,7 @@ __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, f3
                                           f3* tp) {
     const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
     const f3 d = normalize(dir);
-    const Hit h = closest_hit<1>(a.scene.isect, a.scene.n_tri, o, d, a.t_scale);
+    const Hit h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
     if (h.tri < 0) {
         *tp = make3(tp->x * a.env_light, tp->y * a.env_light, tp->z * a.env_light);
         return false;

@@ -340,6 +340,7 @@ int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_came
     a.clip_y1 = clip_y1;
     a.out_pitch = out_pitch;
     a.out = d_out;
+    a.use_filter = rt::filter_usable(a.scene, a.cam_x, a.cam_y, a.cam_z, a.t_scale);
     int32_t* h_count = nullptr;
     RT_HIPE(hipHostMalloc((void**)&h_count, sizeof(int32_t), hipHostMallocDefault));
     hipError_t e = rt::launch_dqn_frame_begin(a, stream);

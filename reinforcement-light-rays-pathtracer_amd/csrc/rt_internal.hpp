@@ -25,9 +25,25 @@ constexpr int kIsectF4 = 3;
 //   [4] = albedo (surfaces)
 constexpr int kShadeF4 = 5;
 
+// Device layout of one triangle for the candidate filter of the two-phase hit
+// test (rt_trace.hpp, closest_hit_filtered): 5 x float4 = 80 B, built in double
+// on the host (rt_capi.cpp, build_filter) with N = e1 x e2, G1 = v0 x e1,
+// G2 = v0 x e2:
+//   [0] = {N, w0 = v0.N}
+//   [1] = {e2, eA}    eA: error bound of the determinant A = d.N
+//   [2] = {-G2, EW}   EW: error bound of the barycentric tests
+//   [3] = {-e1, ET}   ET: error bound of the t test
+//   [4] = {G1, 0}
+// The bounds hold for |d_i| <= 2, |o_i| <= DeviceScene::origin_bound and
+// t_scale <= kFiltMaxTScale (the host checks the last two per launch).
+constexpr int kFiltF4 = 5;
+constexpr float kFiltMaxTScale = 16384.0f;
+
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
     float4* shade = nullptr;   // n_tri * kShadeF4
+    float4* filt = nullptr;    // n_tri * kFiltF4 (nullptr: no filter records for this scene)
+    float origin_bound = 0.0f; // |o_i| bound the filter records were built for
     int32_t* code_cpu = nullptr;  // n_tri packed hit codes under hit rule CPU
     int32_t* code_gpu = nullptr;  // ... under hit rule GPU
     int n_surf = 0;
@@ -56,7 +72,16 @@ struct RenderLaunch {
     float* out;
     unsigned long long* casts;
     uint32_t sample_base;  // first RNG sample index (SARSA: frame * spp); 0 elsewhere
+    int use_filter;        // 1: two-phase closest hit (filter records valid for this launch)
 };
+
+// 1 if the filter records of `s` hold for rays from a camera at (cx, cy, cz) (and
+// from surface points) at this t_scale.  Host side, once per launch.
+inline int filter_usable(const DeviceScene& s, float cx, float cy, float cz, float t_scale) {
+    if (s.filt == nullptr) return 0;
+    const float m = fmaxf(fabsf(cx), fmaxf(fabsf(cy), fabsf(cz)));
+    return (m <= s.origin_bound && t_scale > 0.0f && t_scale <= kFiltMaxTScale) ? 1 : 0;
+}
 
 // ---- DQN Q-value network (dq_network/fc_layer) and its wavefront renderer ----
 // Four ReLU layers n_in -> h1 -> h2 -> h3 -> n_out (NN_Builders/dq_network.cu:8-33).
@@ -106,6 +131,7 @@ struct DqnLaunch {
     int clip_x1, clip_y1;
     int out_pitch;
     float* out;
+    int use_filter;  // as RenderLaunch::use_filter
 };
 
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
@@ -165,8 +191,8 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
                                 hipStream_t stream);
 
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
-                            float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
-                            hipStream_t stream);
+                            float t_scale, int hit_rule, int use_filter, float* out_t,
+                            int32_t* out_hit, hipStream_t stream);
 
 // exhaustive rcp_rn == 1.0f/x check over all 2^32 floats (4096 x 256 threads x 4096)
 hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream);

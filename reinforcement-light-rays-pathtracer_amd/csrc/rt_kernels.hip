@@ -35,7 +35,7 @@ namespace rt {
 namespace {
 
 template <int RULE>
-__global__ __launch_bounds__(256) void k_intersect(const float4* __restrict__ tri, int n_tri,
+__global__ __launch_bounds__(256) void k_intersect(const DeviceScene s, int use_filter,
                                                    const int32_t* __restrict__ code,
                                                    const float* __restrict__ orig,
                                                    const float* __restrict__ dir, int n,
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void k_intersect(const float4* __restrict__ tr
     if (r >= n) return;
     const f3 o = make3(orig[3 * r + 0], orig[3 * r + 1], orig[3 * r + 2]);
     const f3 d = make3(dir[3 * r + 0], dir[3 * r + 1], dir[3 * r + 2]);
-    const Hit h = closest_hit<RULE>(tri, n_tri, o, d, t_scale);
+    const Hit h = closest_hit_sel<RULE>(s, use_filter, o, d, t_scale);
     out_t[r] = (h.tri >= 0) ? h.t : __builtin_inff();
     out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
 }
@@ -74,10 +74,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
     const int py = blk.py0 + ly;
     const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
     const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
-    const float4* __restrict__ tri = a.scene.isect;
     const float4* __restrict__ shade = a.scene.shade;
     const int n_surf = a.scene.n_surf;
-    const int n_tri = a.scene.n_tri;
     const int s_end = (chunk + 1) * a.per_chunk;
 
     int s = valid ? chunk * a.per_chunk : s_end;  // current sample
@@ -101,7 +99,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
 
-        const Hit h = closest_hit<RULE>(tri, n_tri, o, d, a.t_scale);
+        const Hit h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
         ++n_casts;
 
         bool terminal = false;
@@ -255,17 +253,17 @@ hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStr
 }
 
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
-                            float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
-                            hipStream_t stream) {
+                            float t_scale, int hit_rule, int use_filter, float* out_t,
+                            int32_t* out_hit, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     const dim3 block(256);
     const dim3 grid((unsigned)((n + 255) / 256));
     if (hit_rule == 0) {
-        hipLaunchKernelGGL(k_intersect<0>, grid, block, 0, stream, s.isect, s.n_tri, s.code_cpu,
-                           orig, dir, n, t_scale, out_t, out_hit);
+        hipLaunchKernelGGL(k_intersect<0>, grid, block, 0, stream, s, use_filter, s.code_cpu, orig, dir,
+                           n, t_scale, out_t, out_hit);
     } else {
-        hipLaunchKernelGGL(k_intersect<1>, grid, block, 0, stream, s.isect, s.n_tri, s.code_gpu,
-                           orig, dir, n, t_scale, out_t, out_hit);
+        hipLaunchKernelGGL(k_intersect<1>, grid, block, 0, stream, s, use_filter, s.code_gpu, orig, dir,
+                           n, t_scale, out_t, out_hit);
     }
     return hipGetLastError();
 }

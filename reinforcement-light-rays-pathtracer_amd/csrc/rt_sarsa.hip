@@ -136,9 +136,8 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     const int px = blk.px0 + lx, py = blk.py0 + ly;
     const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
     const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
-    const float4* __restrict__ tri = a.scene.isect;
     const float4* __restrict__ shade = a.scene.shade;
-    const int n_surf = a.scene.n_surf, n_tri = a.scene.n_tri;
+    const int n_surf = a.scene.n_surf;
     const int s_end = (chunk + 1) * a.per_chunk;
     __shared__ int kd_stack[kKdStack * 256];
     int* const st = kd_stack + threadIdx.x;
@@ -159,7 +158,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
         const bool active = s < s_end;
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
-        const Hit h = closest_hit<RULE>(tri, n_tri, o, d, a.t_scale);
+        const Hit h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
         ++n_casts;
         const bool is_surf = (h.tri >= 0) && (h.tri < n_surf);
         f3 pos = o;

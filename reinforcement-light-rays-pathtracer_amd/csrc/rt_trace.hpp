@@ -213,6 +213,106 @@ __device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n
     return h;
 }
 
+// Exact test of triangle i, record loaded by this lane: the operations of
+// closest_hit (same operands, same order), so the same bits.
+template <int RULE>
+__device__ __forceinline__ void exact_one(const float4* __restrict__ tri, int i, f3 o, float nDx,
+                                          float nDy, float nDz, Hit& h) {
+    const float4 A = tri[i * kIsectF4 + 0];
+    const float4 E1 = tri[i * kIsectF4 + 1];
+    const float4 E2 = tri[i * kIsectF4 + 2];
+    const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
+    const float s1 = nDy * E2.z - E2.y * nDz;
+    const float s2 = nDy * E1.z - E1.y * nDz;
+    const float detA = (nDx * A.w - E1.x * s1) + E2.x * s2;
+    const float s3 = by * E2.z - E2.y * bz;
+    const float s4 = by * E1.z - E1.y * bz;
+    const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
+    const float s5 = nDy * bz - by * nDz;
+    const float s6 = E1.y * bz - by * E1.z;
+    const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+    const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+    exact_test<RULE>(detA, det_t, det_u, det_v, i, h);
+}
+
+// Two-phase closest hit: the same Hit as closest_hit, bit for bit.
+//
+// The reference's predicate is the exact float Cramer test of every triangle in
+// index order, each accepted hit narrowing the t window of the next.  Its result
+// depends only on the triangles that pass the geometric part of the test
+// (detA != 0, u >= 0, v >= 0, u + v <= 1, t > eps [RULE 0] / t >= 0 [RULE 1]),
+// taken in index order.  Phase 1 (wave-uniform loop, records in SGPRs) evaluates
+// the same quantities with 18 FMAs instead of 43 unfused operations, scaled by
+// 1/t_scale and with the sign of the determinant folded in:
+//   Ad = d.N,  T = w0 - o.N,  U = e2.R - d.G2,  V = -e1.R + d.G1   (R = d x o)
+//   u = U/Ad,  v = V/Ad,  t = T/(t_scale Ad)
+// and rejects a pair only when it is farther from the decision boundary than the
+// combined rounding error of both evaluations (the per-triangle bounds eA, EW, ET
+// of build_filter, rt_capi.cpp); the survivors set a bit of the lane's candidate
+// mask.  Phase 2 runs the exact test (exact_one) on the candidates in index order.
+// NaN/inf inputs never reject (the comparisons fail), and a zero direction leaves
+// |Ad| <= eA, which never rejects either.
+template <int RULE>
+__device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ filt,
+                                                    const float4* __restrict__ tri, int n_tri, f3 o,
+                                                    f3 d, float t_scale) {
+    const float nDx = -(d.x * t_scale);
+    const float nDy = -(d.y * t_scale);
+    const float nDz = -(d.z * t_scale);
+    const float Rx = fmaf(d.y, o.z, -(d.z * o.y));
+    const float Ry = fmaf(d.z, o.x, -(d.x * o.z));
+    const float Rz = fmaf(d.x, o.y, -(d.y * o.x));
+    const float ets = kEps * t_scale;
+    Hit h;
+    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+    h.tri = -1;
+    for (int base = 0; base < n_tri; base += 32) {
+        const int cnt = min(32, n_tri - base);
+        const float4* __restrict__ f = filt + (size_t)base * kFiltF4;
+        uint32_t mask = 0u;
+#pragma unroll 2
+        for (int j = 0; j < cnt; ++j) {
+            const float4 F0 = f[j * kFiltF4 + 0], F1 = f[j * kFiltF4 + 1], F2 = f[j * kFiltF4 + 2];
+            const float4 F3 = f[j * kFiltF4 + 3], F4 = f[j * kFiltF4 + 4];
+            const float ad = fmaf(d.x, F0.x, fmaf(d.y, F0.y, d.z * F0.z));
+            const float tt = fmaf(-o.x, F0.x, fmaf(-o.y, F0.y, fmaf(-o.z, F0.z, F0.w)));
+            const float uu = fmaf(F1.x, Rx, fmaf(F1.y, Ry, fmaf(F1.z, Rz,
+                             fmaf(d.x, F2.x, fmaf(d.y, F2.y, d.z * F2.z)))));
+            const float vv = fmaf(F3.x, Rx, fmaf(F3.y, Ry, fmaf(F3.z, Rz,
+                             fmaf(d.x, F4.x, fmaf(d.y, F4.y, d.z * F4.z)))));
+            const uint32_t sg = __float_as_uint(ad) & 0x80000000u;
+            const float su = __uint_as_float(__float_as_uint(uu) ^ sg);
+            const float sv = __uint_as_float(__float_as_uint(vv) ^ sg);
+            const float st = __uint_as_float(__float_as_uint(tt) ^ sg);
+            const float aa = fabsf(ad);
+            const float w = (aa - su) - sv;
+            const float m = fminf(fminf(su, sv), w);
+            const float tm = (RULE == 0) ? fmaf(-ets, aa, st) : st;
+            const bool reject = (aa > F1.w) && ((m < -F2.w) || (tm < -F3.w));
+            mask |= reject ? 0u : (1u << j);
+        }
+        while (mask != 0u) {
+            const int j = __builtin_ctz(mask);
+            mask &= mask - 1u;
+            exact_one<RULE>(tri, base + j, o, nDx, nDy, nDz, h);
+        }
+    }
+    return h;
+}
+
+#ifndef RT_FILTER
+#define RT_FILTER 1  // 0: always the single-phase scan (A/B builds)
+#endif
+
+template <int RULE>
+__device__ __forceinline__ Hit closest_hit_sel(const DeviceScene& s, int use_filter, f3 o, f3 d,
+                                               float t_scale) {
+#if RT_FILTER
+    if (use_filter) return closest_hit_filtered<RULE>(s.filt, s.isect, s.n_tri, o, d, t_scale);
+#endif
+    return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
+}
+
 // two uniforms of event `ev` of sample `smp` of pixel `pix`
 __device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, uint32_t k0,
                                       uint32_t k1, float* a, float* b) {
