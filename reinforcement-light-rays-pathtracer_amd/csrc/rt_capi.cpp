@@ -384,7 +384,8 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     double vmax = 0.0;
     for (float v : sc->tri) vmax = fmax(vmax, fabs((double)v));
     const double obound = fmax(8.0, 2.0 * vmax + 1.0);
-    std::vector<float4> filt((size_t)n * rt::kFiltF4);
+    // padded to an even triangle count (phase 1 runs in pairs; the pad is masked off)
+    std::vector<float4> filt((size_t)((n + 1) & ~1) * rt::kFiltF4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     bool filt_ok = true;
     for (int i = 0; i < n && filt_ok; ++i)
         filt_ok = build_filter(isect[(size_t)i * 3 + 0], isect[(size_t)i * 3 + 1], isect[(size_t)i * 3 + 2],

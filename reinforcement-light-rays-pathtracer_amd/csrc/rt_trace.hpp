@@ -252,6 +252,79 @@ __device__ __forceinline__ void exact_one(const float4* __restrict__ tri, int i,
 // mask.  Phase 2 runs the exact test (exact_one) on the candidates in index order.
 // NaN/inf inputs never reject (the comparisons fail), and a zero direction leaves
 // |Ad| <= eA, which never rejects either.
+// Phase-1 quantities of one (ray, triangle) pair against filter record `f`,
+// returned as three floats whose sign bits say "certain to fail":
+//   x1 = eA - |Ad|        < 0  <=>  |Ad| > eA   (the sign of Ad is certain)
+//   x2 = min(u,v,w) + EW  < 0  <=>  a barycentric test certainly fails
+//   x3 = tm + ET          < 0  <=>  the t test certainly fails
+// The exact test certainly fails iff x1 < 0 and (x2 < 0 or x3 < 0).  The sums are
+// exact in sign (a nonzero exact sum never rounds to zero under gradual underflow,
+// and an exact zero is +0), so each sign bit equals the comparison it stands for.
+// Finite inputs only (the caller keeps every triangle of a non-finite ray).
+template <int RULE>
+__device__ __forceinline__ void filter_eval(const float4* __restrict__ f, f3 o, f3 d, float Rx,
+                                            float Ry, float Rz, float ets, float* x1, float* x2,
+                                            float* x3) {
+    const float4 F0 = f[0], F1 = f[1], F2 = f[2], F3 = f[3], F4 = f[4];
+    const float ad = fmaf(d.x, F0.x, fmaf(d.y, F0.y, d.z * F0.z));
+    const float tt = fmaf(-o.x, F0.x, fmaf(-o.y, F0.y, fmaf(-o.z, F0.z, F0.w)));
+    const float uu = fmaf(F1.x, Rx, fmaf(F1.y, Ry, fmaf(F1.z, Rz,
+                     fmaf(d.x, F2.x, fmaf(d.y, F2.y, d.z * F2.z)))));
+    const float vv = fmaf(F3.x, Rx, fmaf(F3.y, Ry, fmaf(F3.z, Rz,
+                     fmaf(d.x, F4.x, fmaf(d.y, F4.y, d.z * F4.z)))));
+    const uint32_t sg = __float_as_uint(ad) & 0x80000000u;
+    const float su = __uint_as_float(__float_as_uint(uu) ^ sg);
+    const float sv = __uint_as_float(__float_as_uint(vv) ^ sg);
+    const float st = __uint_as_float(__float_as_uint(tt) ^ sg);
+    const float aa = fabsf(ad);
+    const float w = (aa - su) - sv;
+    const float m = fminf(fminf(su, sv), w);
+    const float tm = (RULE == 0) ? fmaf(-ets, aa, st) : st;
+    *x1 = F1.w - aa;
+    *x2 = m + F2.w;
+    *x3 = tm + F3.w;
+}
+
+// keep bit (bit 31) of one pair: NOT (x1 & (x2 | x3)) on the sign bits
+__device__ __forceinline__ uint32_t keep_bit(float x1, float x2, float x3) {
+    return ~(__float_as_uint(x1) & (__float_as_uint(x2) | __float_as_uint(x3)));
+}
+
+// Phase 1 over triangles [0, cnt) of one 32-triangle block `f`, in pairs (records
+// padded to an even count), branch-free and all-VALU: each keep bit is shifted in
+// at bit 0 (v_alignbit), so triangle j ends at bit cnt-1-j (the pad falls off the
+// bottom).  `finite`: false for a ray with a non-finite component (keep all).
+template <int RULE>
+__device__ __forceinline__ uint32_t filter_block(const float4* __restrict__ f, int cnt, bool finite,
+                                                 f3 o, f3 d, float Rx, float Ry, float Rz,
+                                                 float ets) {
+    uint32_t mask = 0u;
+    const int cnt2 = (cnt + 1) & ~1;
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (int j = 0; j < cnt2; j += 2) {
+        float a1, a2, a3, b1, b2, b3;
+        filter_eval<RULE>(f + j * kFiltF4, o, d, Rx, Ry, Rz, ets, &a1, &a2, &a3);
+        filter_eval<RULE>(f + (j + 1) * kFiltF4, o, d, Rx, Ry, Rz, ets, &b1, &b2, &b3);
+        mask = __builtin_amdgcn_alignbit(mask, keep_bit(a1, a2, a3), 31);
+        mask = __builtin_amdgcn_alignbit(mask, keep_bit(b1, b2, b3), 31);
+    }
+    mask >>= (cnt2 - cnt);
+    const uint32_t all = (cnt >= 32) ? 0xffffffffu : ((1u << cnt) - 1u);
+    return finite ? mask : all;
+}
+
+// exact tests of a block's candidates in index order (triangle base + j at bit cnt-1-j)
+template <int RULE>
+__device__ __forceinline__ void exact_block(const float4* __restrict__ tri, int base, int cnt,
+                                            uint32_t mask, f3 o, float nDx, float nDy, float nDz,
+                                            Hit& h) {
+    while (mask != 0u) {
+        const int b = 31 - __builtin_clz(mask);
+        mask ^= 1u << b;
+        exact_one<RULE>(tri, base + cnt - 1 - b, o, nDx, nDy, nDz, h);
+    }
+}
+
 template <int RULE>
 __device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ filt,
                                                     const float4* __restrict__ tri, int n_tri, f3 o,
@@ -263,39 +336,23 @@ __device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ f
     const float Ry = fmaf(d.z, o.x, -(d.x * o.z));
     const float Rz = fmaf(d.x, o.y, -(d.y * o.x));
     const float ets = kEps * t_scale;
+    const bool finite = __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
+                        __builtin_isfinite(d.x) & __builtin_isfinite(d.y) & __builtin_isfinite(d.z);
     Hit h;
     h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
     h.tri = -1;
-    for (int base = 0; base < n_tri; base += 32) {
-        const int cnt = min(32, n_tri - base);
-        const float4* __restrict__ f = filt + (size_t)base * kFiltF4;
-        uint32_t mask = 0u;
-#pragma unroll 2
-        for (int j = 0; j < cnt; ++j) {
-            const float4 F0 = f[j * kFiltF4 + 0], F1 = f[j * kFiltF4 + 1], F2 = f[j * kFiltF4 + 2];
-            const float4 F3 = f[j * kFiltF4 + 3], F4 = f[j * kFiltF4 + 4];
-            const float ad = fmaf(d.x, F0.x, fmaf(d.y, F0.y, d.z * F0.z));
-            const float tt = fmaf(-o.x, F0.x, fmaf(-o.y, F0.y, fmaf(-o.z, F0.z, F0.w)));
-            const float uu = fmaf(F1.x, Rx, fmaf(F1.y, Ry, fmaf(F1.z, Rz,
-                             fmaf(d.x, F2.x, fmaf(d.y, F2.y, d.z * F2.z)))));
-            const float vv = fmaf(F3.x, Rx, fmaf(F3.y, Ry, fmaf(F3.z, Rz,
-                             fmaf(d.x, F4.x, fmaf(d.y, F4.y, d.z * F4.z)))));
-            const uint32_t sg = __float_as_uint(ad) & 0x80000000u;
-            const float su = __uint_as_float(__float_as_uint(uu) ^ sg);
-            const float sv = __uint_as_float(__float_as_uint(vv) ^ sg);
-            const float st = __uint_as_float(__float_as_uint(tt) ^ sg);
-            const float aa = fabsf(ad);
-            const float w = (aa - su) - sv;
-            const float m = fminf(fminf(su, sv), w);
-            const float tm = (RULE == 0) ? fmaf(-ets, aa, st) : st;
-            const bool reject = (aa > F1.w) && ((m < -F2.w) || (tm < -F3.w));
-            mask |= reject ? 0u : (1u << j);
-        }
-        while (mask != 0u) {
-            const int j = __builtin_ctz(mask);
-            mask &= mask - 1u;
-            exact_one<RULE>(tri, base + j, o, nDx, nDy, nDz, h);
-        }
+    // 64 triangles per round: both masks first, then one divergent phase 2
+    for (int base = 0; base < n_tri; base += 64) {
+        const int c0 = min(32, n_tri - base);
+        const int c1 = min(32, n_tri - base - 32);
+        const uint32_t m0 =
+            filter_block<RULE>(filt + (size_t)base * kFiltF4, c0, finite, o, d, Rx, Ry, Rz, ets);
+        uint32_t m1 = 0u;
+        if (c1 > 0)
+            m1 = filter_block<RULE>(filt + (size_t)(base + 32) * kFiltF4, c1, finite, o, d, Rx, Ry,
+                                    Rz, ets);
+        exact_block<RULE>(tri, base, c0, m0, o, nDx, nDy, nDz, h);
+        if (c1 > 0) exact_block<RULE>(tri, base + 32, c1, m1, o, nDx, nDy, nDz, h);
     }
     return h;
 }
