@@ -607,8 +607,12 @@ ORC_API void orc_set_threads(int n) {
  *   render_frame / initialise_ray / trace_ray  GPU/deep_learning/pre_trained_pathtracer.cu:188-491
  * RNG: event 1+b of bounce b >= 1: Philox counter word 3 = 0 gives rv,
  * = 1 + a/2 the jitter of cells a (pairs), = 73 the final jitter.
- * The forward pass accumulates in double (bf16 = 0) or emulates the kernel's bf16
- * operand / activation rounding with double accumulation (bf16 = 1).
+ * The forward pass accumulates in double (bf16 = 0: the reference's fp32 network,
+ * DyNet) or follows the kernel's arithmetic (bf16 = 1): layer 0 folded to the affine
+ * map h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x))) of the ray position (c0 = W1 v + b1,
+ * S = W1's column sums per coordinate, both summed in double in index order and
+ * rounded to float, as rt_dqn_create does), bf16-rounded; layers 1-3 with bf16
+ * operands and activations, double accumulation.
  */
 typedef struct {
     int n_in, h1, h2, h3, n_out;
@@ -629,11 +633,25 @@ static float bf16_round(float f) {
 static void dqn_forward_one(const orc_dqn *net, const float *loc, int bf16, float *q_out, float *scratch) {
     int dims[5] = {net->n_in, net->h1, net->h2, net->h3, net->n_out};
     float *in = scratch, *out = scratch + 1024;
-    for (int k = 0; k < net->n_in; k++) {
-        float x = net->verts[k] - loc[k % 3];
-        in[k] = bf16 ? bf16_round(x) : x;
+    int l0 = 0;
+    if (bf16) {
+        for (int o = 0; o < net->h1; o++) {
+            const float *w = net->W[0] + (size_t)o * net->n_in;
+            double c0 = (double)net->b[0][o], S[3] = {0.0, 0.0, 0.0};
+            for (int i = 0; i < net->n_in; i++) {
+                c0 += (double)w[i] * (double)net->verts[i];
+                S[i % 3] += (double)w[i];
+            }
+            const float cf = (float)c0, s0 = (float)S[0], s1 = (float)S[1], s2 = (float)S[2];
+            float h = cf - fmaf(s2, loc[2], fmaf(s1, loc[1], s0 * loc[0]));
+            h = h > 0.0f ? h : 0.0f;
+            in[o] = bf16_round(h);
+        }
+        l0 = 1;
+    } else {
+        for (int k = 0; k < net->n_in; k++) in[k] = net->verts[k] - loc[k % 3];
     }
-    for (int l = 0; l < 4; l++) {
+    for (int l = l0; l < 4; l++) {
         const float *W = net->W[l], *b = net->b[l];
         for (int o = 0; o < dims[l + 1]; o++) {
             double acc = 0.0;

@@ -35,7 +35,13 @@ namespace {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
-constexpr int kTileM = 64;        // rays per MLP workgroup
+#ifndef RT_MLP_MT
+#define RT_MLP_MT 4  // 16-row M-tiles per MLP workgroup
+#endif
+constexpr int kTileM = RT_MLP_MT * 16;  // rays per MLP workgroup
+// MT = 8 (one 142 KB workgroup per CU) is 1.4x slower; a single flattened weight
+// stream over layers 1-3 with a 2-4 deep register ring was 2x slower (round-1 A/B,
+// DESIGN.md §4).
 constexpr int kStrideA = 320 + 8; // LDS row strides in bf16 elements (+16 B pad)
 constexpr int kStrideB = 224 + 8;
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
@@ -63,13 +69,39 @@ __device__ __forceinline__ void list_append(bool keep, int32_t rid, int32_t* lis
 }
 
 // ---------------------------------------------------------------------------
-// MLP: one layer of 64 rows on 4 waves.  A from LDS (bf16) or, for layer 0,
-// built from the scene features and the ray positions.
+// Layer 0, folded to an affine map of the ray position (rt_internal.hpp DqnNet):
+// fp32 on the VALU, one lane per (row, 8 consecutive outputs), ReLU, bf16 into LDS.
 // ---------------------------------------------------------------------------
-template <bool FIRST, bool LAST>
+template <int MT>
+__device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __restrict__ loc_lds,
+                                           __bf16* out_lds, int out_stride) {
+    const int groups = net.N[0] >> 3;
+    const int items = MT * 16 * groups;
+    for (int it = threadIdx.x; it < items; it += 256) {
+        const int row = it / groups;
+        const int g = it - row * groups;
+        const float x = loc_lds[row * 3 + 0], y = loc_lds[row * 3 + 1], z = loc_lds[row * 3 + 2];
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float4 c = net.l0[g * 8 + e];
+            float h = c.w - fmaf(c.z, z, fmaf(c.y, y, c.x * x));
+            h = h > 0.0f ? h : 0.0f;
+            v[e] = (__bf16)h;
+        }
+        *reinterpret_cast<bf16x8*>(out_lds + row * out_stride + g * 8) = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MLP layers 1-3: MT*16 rows on 4 waves, A (bf16) from LDS.  Each wave owns every
+// M-tile and the N-tiles chunk, chunk+4, chunk+8, chunk+12 of each 16-tile chunk,
+// so a weight fragment (one contiguous 1 KB load) feeds MT MFMAs; the fragments of
+// K step k+32 are in flight while the MFMAs of step k run.
+// ---------------------------------------------------------------------------
+template <bool LAST, int MT>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
-                                          __bf16* out_lds, int out_stride, const float (&locm)[4][3],
-                                          float* q_rows, int rows_valid) {
+                                          __bf16* out_lds, int out_stride, float* q_rows, int rows_valid) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int K = net.K[L];
@@ -82,47 +114,41 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         // this wave's n-tiles in the chunk: chunk, chunk+4, chunk+8, chunk+12
         int nt[4];
         bool use[4];
+        const uint16_t* wrow[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             nt[j] = chunk + 4 * j;
             use[j] = nt[j] < n_tiles;
+            wrow[j] = W + ((size_t)(use[j] ? nt[j] : chunk) * (K >> 5) * 64 + lane) * 8;
         }
-        f32x4 acc[4][4];
+        f32x4 acc[MT][4];
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        bf16x8 bw[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8*>(wrow[j]);
         for (int k0 = 0; k0 < K; k0 += 32) {
             const int kb = k0 + kg;
-            bf16x8 a[4];
-            if (FIRST) {
-                const int c = k0 / net.vblock;  // coordinate of this K step (uniform)
-                const float4 f0 = *reinterpret_cast<const float4*>(net.feat + kb);
-                const float4 f1 = *reinterpret_cast<const float4*>(net.feat + kb + 4);
-                const float fv[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            // prefetch the next K step's weight fragments (unused tiles re-read a used one)
+            const int kn = (k0 + 32 < K) ? k0 + 32 : k0;
+            bf16x8 bn[4];
 #pragma unroll
-                for (int m = 0; m < 4; ++m) {
-                    const float lc = (c == 0) ? locm[m][0] : ((c == 1) ? locm[m][1] : locm[m][2]);
+            for (int j = 0; j < 4; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kn * 16);
+            bf16x8 a[MT];
 #pragma unroll
-                    for (int j = 0; j < 8; ++j) a[m][j] = (__bf16)(fv[j] - lc);
-                }
-            } else {
-#pragma unroll
-                for (int m = 0; m < 4; ++m)
-                    a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + kb);
-            }
-            bf16x8 bw[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (use[j])
-                    bw[j] = *reinterpret_cast<const bf16x8*>(W + (size_t)(nt[j] * 16 + r16) * K + kb);
+            for (int m = 0; m < MT; ++m)
+                a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + kb);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
                 if (use[j]) {
 #pragma unroll
-                    for (int m = 0; m < 4; ++m)
+                    for (int m = 0; m < MT; ++m)
                         acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], bw[j], acc[m][j], 0, 0, 0);
                 }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bw[j] = bn[j];
         }
         // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
 #pragma unroll
@@ -131,7 +157,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
             const int col = nt[j] * 16 + r16;
             const float bj = bias[col];
 #pragma unroll
-            for (int m = 0; m < 4; ++m)
+            for (int m = 0; m < MT; ++m)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = m * 16 + (lane >> 4) * 4 + r;
@@ -147,38 +173,42 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
 }
 
+// One workgroup = MT*16 rays (LDS: MT=4 -> 71 KB, two workgroups per CU).
+template <int MT>
 __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
                                                  float* __restrict__ q) {
-    __shared__ __attribute__((aligned(16))) __bf16 bufA[kTileM * kStrideA];
-    __shared__ __attribute__((aligned(16))) __bf16 bufB[kTileM * kStrideB];
+    constexpr int kRows = MT * 16;
+    __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrideA];
+    __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrideB];
+    __shared__ float locs[kRows * 3];
     const int n_rows = (count != nullptr) ? min(*count, max_rows) : max_rows;
-    const int row0 = blockIdx.x * kTileM;
+    const int row0 = blockIdx.x * kRows;
     if (row0 >= n_rows) return;
-    const int rows_valid = min(kTileM, n_rows - row0);
-    const int lane = threadIdx.x & 63;
-    float locm[4][3];
-#pragma unroll
-    for (int m = 0; m < 4; ++m) {
-        const int row = m * 16 + (lane & 15);
+    const int rows_valid = min(kRows, n_rows - row0);
+    if (threadIdx.x < kRows) {
+        const int row = threadIdx.x;
+        float x = 0.0f, y = 0.0f, z = 0.0f;
         if (row < rows_valid) {
             const int rid = (list != nullptr) ? list[row0 + row] : (row0 + row);
-            locm[m][0] = loc[(size_t)rid * 3 + 0];
-            locm[m][1] = loc[(size_t)rid * 3 + 1];
-            locm[m][2] = loc[(size_t)rid * 3 + 2];
-        } else {
-            locm[m][0] = locm[m][1] = locm[m][2] = 0.0f;
+            x = loc[(size_t)rid * 3 + 0];
+            y = loc[(size_t)rid * 3 + 1];
+            z = loc[(size_t)rid * 3 + 2];
         }
+        locs[row * 3 + 0] = x;
+        locs[row * 3 + 1] = y;
+        locs[row * 3 + 2] = z;
     }
+    __syncthreads();
     float* q_rows = q + (size_t)row0 * kDqnActions;
-    mlp_layer<true, false>(net, 0, nullptr, 0, bufB, kStrideB, locm, nullptr, rows_valid);
+    mlp_layer0<MT>(net, locs, bufB, kStrideB);
     __syncthreads();
-    mlp_layer<false, false>(net, 1, bufB, kStrideB, bufA, kStrideA, locm, nullptr, rows_valid);
+    mlp_layer<false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA, q_rows, rows_valid);
     __syncthreads();
-    mlp_layer<false, false>(net, 2, bufA, kStrideA, bufB, kStrideB, locm, nullptr, rows_valid);
+    mlp_layer<false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB, q_rows, rows_valid);
     __syncthreads();
-    mlp_layer<false, true>(net, 3, bufB, kStrideB, nullptr, 0, locm, q_rows, rows_valid);
+    mlp_layer<true, MT>(net, 3, bufB, kStrideB, nullptr, 0, q_rows, rows_valid);
 }
 
 struct SampleOut {
@@ -420,7 +450,7 @@ hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* li
                           int max_rows, float* q, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
     const int blocks = (max_rows + kTileM - 1) / kTileM;
-    hipLaunchKernelGGL(k_dqn_mlp, dim3((unsigned)blocks), dim3(256), 0, stream, net, loc, list, count,
+    hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(256), 0, stream, net, loc, list, count,
                        max_rows, q);
     return hipGetLastError();
 }

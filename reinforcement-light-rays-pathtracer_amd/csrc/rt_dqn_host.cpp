@@ -136,11 +136,7 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
     d->n_in = n_in;
     d->n_out = n_out;
     for (int l = 0; l < 3; ++l) d->h[l] = hidden[l];
-    const int n_vert = n_in / 3;
-    const int vblock = pad32(n_vert);
-    d->net.n_vert = n_vert;
-    d->net.vblock = vblock;
-    d->net.K[0] = 3 * vblock;
+    d->net.K[0] = n_in;
     d->net.N[0] = pad32(dims[1]);
     d->net.K[1] = d->net.N[0];
     d->net.N[1] = pad32(dims[2]);
@@ -148,10 +144,6 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
     d->net.N[2] = pad32(dims[3]);
     d->net.K[3] = d->net.N[2];
     d->net.N[3] = n_out;
-    // permuted features: index c*vblock + v  <-  nn_vertices[v*3 + c]
-    std::vector<float> feat((size_t)d->net.K[0], 0.0f);
-    for (int v = 0; v < n_vert; ++v)
-        for (int c = 0; c < 3; ++c) feat[(size_t)c * vblock + v] = nn_vertices[(size_t)v * 3 + c];
     auto upload = [&](const void* src, size_t bytes, void** dst) -> int {
         void* p = nullptr;
         hipError_t e = hipMalloc(&p, bytes);
@@ -164,23 +156,39 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
         *dst = p;
         return RT_OK;
     };
+    // layer 0 folded (rt_internal.hpp): c0 = W1 v + b1, S[.][c] = column sums of W1 per coordinate
+    std::vector<float4> l0((size_t)d->net.N[0], make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (int o = 0; o < dims[1]; ++o) {
+        const float* w = W[0] + (size_t)o * n_in;
+        double c0 = (double)b[0][o], S[3] = {0.0, 0.0, 0.0};
+        for (int i = 0; i < n_in; ++i) {
+            c0 += (double)w[i] * (double)nn_vertices[i];
+            S[i % 3] += (double)w[i];
+        }
+        l0[o] = make_float4((float)S[0], (float)S[1], (float)S[2], (float)c0);
+    }
     void* p = nullptr;
-    int rc = upload(feat.data(), feat.size() * sizeof(float), &p);
+    int rc = upload(l0.data(), l0.size() * sizeof(float4), &p);
     if (rc != RT_OK) { delete d; return rc; }
-    d->net.feat = (const float*)p;
-    for (int l = 0; l < 4; ++l) {
+    d->net.l0 = (const float4*)p;
+    for (int l = 1; l < 4; ++l) {
         const int Kp = d->net.K[l], Np = d->net.N[l], in = dims[l], outd = dims[l + 1];
         std::vector<uint16_t> w((size_t)Np * Kp, 0);
         std::vector<float> bias((size_t)Np, 0.0f);
         for (int o = 0; o < outd; ++o) {
-            for (int i = 0; i < in; ++i) {
-                int col = i;
-                if (l == 0) col = (i % 3) * vblock + i / 3;  // coordinate-major permutation
-                w[(size_t)o * Kp + col] = to_bf16(W[l][(size_t)o * in + i]);
-            }
+            for (int i = 0; i < in; ++i) w[(size_t)o * Kp + i] = to_bf16(W[l][(size_t)o * in + i]);
             bias[o] = b[l][o];
         }
-        rc = upload(w.data(), w.size() * sizeof(uint16_t), &p);
+        // fragment order (rt_internal.hpp DqnNet::W): one 16x32 B-fragment = 1 KB contiguous
+        std::vector<uint16_t> wf((size_t)Np * Kp, 0);
+        const int KS = Kp / 32;
+        for (int nt = 0; nt < Np / 16; ++nt)
+            for (int ks = 0; ks < KS; ++ks)
+                for (int ln = 0; ln < 64; ++ln)
+                    for (int e = 0; e < 8; ++e)
+                        wf[(((size_t)nt * KS + ks) * 64 + ln) * 8 + e] =
+                            w[(size_t)(nt * 16 + (ln & 15)) * Kp + ks * 32 + (ln >> 4) * 8 + e];
+        rc = upload(wf.data(), wf.size() * sizeof(uint16_t), &p);
         if (rc != RT_OK) { delete d; return rc; }
         d->net.W[l] = (const uint16_t*)p;
         rc = upload(bias.data(), bias.size() * sizeof(float), &p);

@@ -85,21 +85,25 @@ inline int filter_usable(const DeviceScene& s, float cx, float cy, float cz, flo
 
 // ---- DQN Q-value network (dq_network/fc_layer) and its wavefront renderer ----
 // Four ReLU layers n_in -> h1 -> h2 -> h3 -> n_out (NN_Builders/dq_network.cu:8-33).
-// Device weights: bf16, row-major [out_padded][in_padded], zero padded; the input
-// features are permuted coordinate-major (all x, then all y, then all z, each
-// block padded to a multiple of 32) so a 32-wide K step needs one coordinate of
-// the ray location; W1's columns are permuted to match.
+// Layer 0's input is x = Scene::vertices - p, the vertices relative to the ray
+// position p (nn_rendering_helpers.cu:280-298), so W1 x + b1 = (W1 v + b1) - S p
+// with S[o][c] = sum over the vertices of W1[o][3v + c]: an affine map of the 3
+// coordinates of p.  The host folds it once per network in double
+// (rt_dqn_create); the kernel evaluates it in fp32 on the VALU (the reference's
+// own precision) instead of a K = n_in bf16 contraction.  Layers 1-3 run on MFMA:
+// device weights bf16, zero padded, stored in MFMA B-fragment order.
 constexpr int kDqnActions = 144;  // GRID_RESOLUTION^2 (GPU/constants/radiance_volumes_settings.h:9)
 constexpr int kDqnGrid = 12;
 
 struct DqnNet {
-    const uint16_t* W[4] = {nullptr, nullptr, nullptr, nullptr};  // bf16 bits
-    const float* b[4] = {nullptr, nullptr, nullptr, nullptr};      // fp32, padded
-    const float* feat = nullptr;  // permuted scene vertex coordinates [K[0]] (0 in padding)
-    int K[4] = {0, 0, 0, 0};      // padded input width of each layer (multiple of 32)
+    // layer 0 folded: [N[0]] x {S0, S1, S2, c0}; h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x)))
+    const float4* l0 = nullptr;
+    // layers 1-3: bf16 bits in fragment order [N/16][K/32][lane 64][8], lane = kq*16 + r
+    // holding W[nt*16 + r][ks*32 + kq*8 .. +7] -- a wave's fragment load is one contiguous 1 KB
+    const uint16_t* W[4] = {nullptr, nullptr, nullptr, nullptr};
+    const float* b[4] = {nullptr, nullptr, nullptr, nullptr};      // fp32, padded (b[0] unused)
+    int K[4] = {0, 0, 0, 0};      // padded input width of each layer (K[0] = n_in, unpadded)
     int N[4] = {0, 0, 0, 0};      // padded output width of each layer (multiple of 32; last = 144)
-    int n_vert = 0;               // vertices (n_in / 3)
-    int vblock = 0;               // padded per-coordinate block (multiple of 32)
 };
 
 // Ray state of the DQN wavefront renderer (SoA over the rays of a frame part).

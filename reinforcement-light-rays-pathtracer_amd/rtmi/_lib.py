@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG_DIR, "build", "librtmi.so")
+# RTMI_LIB: another build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("RTMI_LIB", os.path.join(_PKG_DIR, "build", "librtmi.so"))
 
 RT_OK = 0
 RT_E_INVALID = -1

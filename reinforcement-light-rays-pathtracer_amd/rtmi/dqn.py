@@ -96,6 +96,11 @@ class Dqn:
         """2 * sum(in*out) of the four layers (unpadded)"""
         return int(2 * sum(w.shape[0] * w.shape[1] for w in self.W))
 
+    def mfma_flops_per_ray(self) -> int:
+        """2 * sum(in*out) of layers 1-3, the ones executed on MFMA (unpadded); layer 0 is
+        folded to a 3-input affine map on the VALU (rt_internal.hpp DqnNet)"""
+        return int(2 * sum(w.shape[0] * w.shape[1] for w in self.W[1:]))
+
     def close(self):
         if self._h:
             lib().rt_dqn_destroy(self._h)

@@ -3,9 +3,11 @@ sampling, wavefront render.
 
 Parity levels:
   * reader, sampler: bit-exact with the oracle (same Q in -> same direction, pdf, action)
-  * forward: bf16 MFMA vs the oracle's bf16-emulating forward (same operand and
-    activation rounding, exact accumulation): max |dq| <= 2e-2 * max|q|, mean <= 2e-3 * mean|q|;
-    vs the fp32 forward (the reference's DyNet arithmetic): mean <= 3e-2 * mean|q|
+  * forward: layer 0 folded to an fp32 affine map of the ray position + bf16 MFMA
+    layers 1-3, vs the oracle's forward with the same arithmetic (same fold, same
+    operand and activation rounding, exact accumulation): max |dq| <= 2e-2 * max|q|,
+    mean <= 2e-3 * mean|q|; vs the fp32 forward (the reference's DyNet arithmetic):
+    mean <= 1e-2 * mean|q|
   * render: statistical (a Q perturbation can flip one sampled cell and change a path):
     MAPE(gpu, oracle) must not exceed the oracle's own seed-to-seed MAPE.
 """
@@ -58,7 +60,7 @@ def test_oracle_forward_trained_door_room(rtmi_mod, oracle_mod):
     assert q.shape == (64, 144) and np.all(q >= 0)           # ReLU output layer
     assert np.mean(q.sum(axis=1) > 0) > 0.9                  # non-degenerate distributions
     qb = oracle_mod.dqn_forward(W, b, g.nn_vertices, p, bf16=True)
-    assert np.mean(np.abs(qb - q)) <= 3e-2 * np.mean(np.abs(q))
+    assert np.mean(np.abs(qb - q)) <= 1e-2 * np.mean(np.abs(q))
 
 
 def test_oracle_sampler_properties(rtmi_mod, oracle_mod):
@@ -98,7 +100,7 @@ def test_forward_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx, kind):
     err = np.abs(q - qe)
     assert err.max() <= 2e-2 * np.abs(qe).max() + 1e-6, err.max()
     assert err.mean() <= 2e-3 * np.abs(qe).mean() + 1e-7, err.mean()
-    assert np.abs(q - qf).mean() <= 3e-2 * np.abs(qf).mean()
+    assert np.abs(q - qf).mean() <= 1e-2 * np.abs(qf).mean()
 
 
 @pytest.mark.gpu

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--spp", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-bounces", type=int, default=80)
+    ap.add_argument("--no-render", action="store_true", help="forward pass only (profiling)")
     args = ap.parse_args()
     g = rtmi.obj_geometry(os.path.join(ROOT, "assets", "models", args.scene + ".obj"), args.scene)
     if args.scene == "door_room":
@@ -65,8 +66,15 @@ def main():
     tflops = net.flops_per_ray() * args.rays / (ms * 1e-3) / 1e12
     res["mlp"] = {"rays": args.rays, "ms": round(ms, 4), "tflops": round(tflops, 2),
                   "frac_bf16_peak": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-                  "flops_per_ray": net.flops_per_ray(), "q_mean": float(q.mean().item())}
+                  "flops_per_ray": net.flops_per_ray(),
+                  # what the MFMA units actually execute (layers 1-3; layer 0 is folded)
+                  "mfma_flops_per_ray": net.mfma_flops_per_ray(),
+                  "mfma_tflops": round(net.mfma_flops_per_ray() * args.rays / (ms * 1e-3) / 1e12, 2),
+                  "q_mean": float(q.mean().item())}
 
+    if args.no_render:
+        print(json.dumps(res), flush=True)
+        return
     # --- full render: one frame of `spp` samples per step
     p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=args.width, height=args.width, spp=args.spp,
                             max_bounces=args.max_bounces)
