@@ -41,7 +41,7 @@ TILE = 32
 # HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
 # (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
 PMC_PROFILE = os.path.join("profiles", "r1v4_pmc.json")
-DEFAULT_WORKLOAD = (512, 512, 256, 8)
+DEFAULT_WORKLOAD = (512, 512, 256, 32)
 
 
 def parse():
@@ -52,7 +52,7 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--spp-split", type=int, default=8)
+    ap.add_argument("--spp-split", type=int, default=32)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU-baseline sample duration (0 disables)")
     ap.add_argument("--no-parity", action="store_true")

@@ -1,8 +1,8 @@
-"""Multi-GPU frame assembly: one process per GPU, image tiles round-robin
-over ranks (rtmi.tiles), one all-gather of the equal-sized per-rank tile
+"""Multi-GPU frame assembly: one process per GPU, image tiles dealt to the
+ranks by diagonals (rtmi.tiles: tile (tx, ty) -> rank (tx + ty) mod P), one all-gather of the equal-sized per-rank tile
 buffers over RCCL (backend "nccl" on ROCm; "gloo" for CPU tests).
 
-Data path per frame: rank r renders tiles k = r, r+P, ...
+Data path per frame: rank r renders its tiles
 into out[k_r, T, T, 3] -> all_gather_into_tensor -> gathered[P, k_r, T, T, 3]
 -> rtmi.tiles.assemble on the consumer.  Message per rank = k_r*T*T*12 B
 (512^2 frame on 8 GPUs: 393 KB per rank).

@@ -248,7 +248,7 @@ def test_gpu_tiles_and_td_exchange_equal_single_map(rtmi_mod, gpu_ctx):
         maps[0].render_tiles_device(cam, p, origins, T, full.data_ptr(), casts.data_ptr(), True, 0)
         parts = []
         for r in (0, 1):
-            mine = np.arange(r, len(origins), 2)
+            mine = rtiles.rank_tile_indices(W, H, T, r, 2)
             assert np.array_equal(rtiles.rank_tiles(W, H, T, r, 2), origins[mine])
             out = torch.zeros(len(mine), T, T, 3, device=dev)
             maps[1 + r].render_tiles_device(cam, p, origins[mine], T, out.data_ptr(), casts.data_ptr(), False, 0)

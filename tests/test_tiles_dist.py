@@ -16,8 +16,10 @@ def test_tile_partition_covers_image_once(rtmi_mod):
         seen = []
         for r in range(world):
             mine = T.rank_tiles(w, h, tile, r, world)
-            assert mine.shape == (T.tiles_per_rank(len(allt), world), 2)
-            seen += [tuple(x) for x in allt[r::world]]
+            assert mine.shape == (T.tiles_per_rank(w, h, tile, world), 2)
+            real = allt[T.rank_tile_indices(w, h, tile, r, world)]
+            assert np.array_equal(mine[:len(real)], real)
+            seen += [tuple(x) for x in real]
         assert sorted(seen) == sorted(tuple(x) for x in allt)
 
 

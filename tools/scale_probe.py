@@ -1,0 +1,75 @@
+#!/usr/bin/env python3
+"""Predict bench.py's tile-parallel scaling on ONE GPU: render the tile set of every
+rank r of a P-rank job (rtmi.tiles.rank_tiles) alone and time it with HIP events.
+max over r of that time is the kernel part of a P-GPU step; t(1) / max_r t(P, r) is
+the kernel-only speedup the 8-GPU driver run can reach (the all-gather comes on top).
+
+    python tools/scale_probe.py [--spp-split 8] [--worlds 1 2 4 8]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd"))
+import torch  # noqa: E402
+
+import rtmi  # noqa: E402
+
+TILE = 32
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spp-split", type=int, default=8)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--width", type=int, default=512)
+    ap.add_argument("--worlds", type=int, nargs="+", default=[1, 2, 4, 8])
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    ctx = rtmi.Context(0)
+    geom = rtmi.cornell_geometry(rtmi.RT_PRESET_CPU)
+    scene = rtmi.Scene(ctx, geom)
+    p = rtmi.default_params(rtmi.RT_PRESET_CPU, width=args.width, height=args.width, spp=args.spp,
+                            spp_split=args.spp_split)
+    cam = rtmi.camera(rtmi.CAMERAS["cornell"])
+    stream = torch.cuda.current_stream(dev)
+    res = {"spp_split": args.spp_split, "width": args.width, "spp": args.spp, "worlds": {}}
+    t1 = None
+    for world in args.worlds:
+        per_rank = []
+        for rank in range(world):
+            tiles = rtmi.tiles.rank_tiles(p.width, p.height, TILE, rank, world)
+            out = torch.zeros((tiles.shape[0], TILE, TILE, 3), dtype=torch.float32, device=dev)
+            casts = torch.zeros(1, dtype=torch.int64, device=dev)
+
+            def run():
+                rtmi.render_tiles_device(ctx, scene, cam, p, tiles, TILE, out.data_ptr(),
+                                         casts.data_ptr(), stream.cuda_stream)
+            run()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(args.reps):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                run()
+                e1.record(stream)
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            per_rank.append(float(np.median(ts)))
+        tmax = max(per_rank)
+        if world == 1:
+            t1 = tmax
+        res["worlds"][world] = {"ms_per_rank": [round(t, 4) for t in per_rank], "ms_max": round(tmax, 4),
+                                "kernel_speedup": round(t1 / tmax, 3) if t1 else None}
+    print(json.dumps(res), flush=True)
+    scene.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
