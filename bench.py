@@ -6,10 +6,12 @@
 
 A step renders one full 512x512 / 256-spp frame of the reference's Cornell
 box (CPU-engine preset: cap 2 bounces, hit rule of the prebuilt CPU object,
-uniform hemisphere sampling).  The frame is cut into 32x32 tiles dealt
-round-robin to the ranks (one process per GPU); each rank renders its tiles
-with the HIP megakernel, and the per-rank tile buffers are all-gathered over
-RCCL into the full image.  The frame is fixed as N grows: strong scaling.
+uniform hemisphere sampling).  The frame is cut into 32x32 tiles dealt to the
+ranks by diagonals (rtmi.tiles; one process per GPU); each rank renders its
+tiles with the HIP megakernel, and the per-rank tile buffers are all-gathered
+over RCCL into the full image -- asynchronously, into one of two buffers, so
+frame i+1 renders while frame i is exchanged.  The frame is fixed as N grows:
+strong scaling.
 
 value = total ray casts (all ranks) / max-over-ranks wall time of the K
 timed steps, in Mrays/s.  rank 0 prints one JSON line with the roofline of
@@ -128,22 +130,35 @@ def main():
 
     tiles = rtmi.tiles.rank_tiles(params.width, params.height, TILE, rank, world)
     k = tiles.shape[0]
-    out = torch.zeros((k, TILE, TILE, 3), dtype=torch.float32, device=dev)
+    # two frame buffers: frame i+1 renders while frame i is all-gathered over RCCL
+    outs = [torch.zeros((k, TILE, TILE, 3), dtype=torch.float32, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world, k, TILE, TILE, 3), dtype=torch.float32, device=dev)
+                for _ in range(2)]
     casts = torch.zeros(1, dtype=torch.int64, device=dev)
-    gathered = torch.empty((world, k, TILE, TILE, 3), dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
+    pending = [None, None]
 
-    def render():
-        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(),
+    def render(b):
+        if pending[b] is not None:  # the gather still reading this buffer
+            pending[b].wait()
+            pending[b] = None
+        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, outs[b].data_ptr(),
                                  casts.data_ptr(), stream.cuda_stream)
 
-    def step():
-        render()
+    def gather(b):
         if world > 1:
-            rtmi.dist.gather_tiles(out, gathered)
+            pending[b] = rtmi.dist.gather_tiles(outs[b], gathered[b], async_op=True)
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        for b in range(2):
+            if pending[b] is not None:
+                pending[b].wait()
+                pending[b] = None
+
+    for i in range(args.warmup):
+        render(i % 2)
+        gather(i % 2)
+    drain()
     torch.cuda.synchronize()
     casts.zero_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -153,15 +168,20 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        b = i % 2
+        if pending[b] is not None:
+            pending[b].wait()
+            pending[b] = None
         ev[i][0].record(stream)
-        render()
+        render(b)
         ev[i][1].record(stream)
-        if world > 1:
-            rtmi.dist.gather_tiles(out, gathered)
+        gather(b)
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    last = (args.steps - 1) % 2
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_casts = int(casts.item())
@@ -176,11 +196,10 @@ def main():
     else:
         total_casts = rank_casts
 
-    if world == 1:
-        gathered = out[None]
+    frame = outs[last][None] if world == 1 else gathered[last]
     image = None
     if rank == 0:
-        image = rtmi.tiles.assemble(gathered.cpu().numpy(), params.width, params.height, TILE, world)
+        image = rtmi.tiles.assemble(frame.cpu().numpy(), params.width, params.height, TILE, world)
 
     if rank == 0:
         n_tri = geom.n_tri

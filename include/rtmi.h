@@ -203,6 +203,17 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
 int rt_sarsa_destroy(rt_sarsa* sarsa);
 /* sizes: volumes, KD array elements, frames rendered so far (any pointer may be NULL) */
 int rt_sarsa_info(const rt_sarsa* sarsa, int32_t* n_volumes, int32_t* n_nodes, uint32_t* frames);
+/* Nearest-volume search of find_closest_radiance_volume_iterative
+ * (GPU/radiance_volumes/radiance_map.cu:149-203).  Both modes return the same volume
+ * for every query: RT_SARSA_SEARCH_KD walks the reference's KD array;
+ * RT_SARSA_SEARCH_GRID (default) answers from a per-normal uniform grid when the
+ * nearest same-normal volume is provably a leaf the KD walk visits and is unique,
+ * and walks the KD array otherwise (counted in kd_fallbacks). */
+#define RT_SARSA_SEARCH_KD 0
+#define RT_SARSA_SEARCH_GRID 1
+int rt_sarsa_set_search(rt_sarsa* sarsa, int mode);
+int rt_sarsa_search_stats(const rt_sarsa* sarsa, int32_t* mode, int32_t* n_classes, int64_t* grid_cells,
+                          uint64_t* kd_fallbacks);
 /* host copies: pos n x 3, normal n x 3, surface index n, KD array n_nodes x 12 words
  * {dim, leaf, left, right (int32), data, px, py, pz, nx, ny, nz (float), vol (int32)} */
 int rt_sarsa_volumes(const rt_sarsa* sarsa, float* pos, float* normal, int32_t* surface,

@@ -186,6 +186,20 @@ struct SarsaMap {
     int n_kd = 0;
     float root_x = 0.f, root_y = 0.f, root_z = 0.f;  // position of KD element 0 (0 if internal)
     float max_dist = 0.003f;            // MAX_DIST (compared with delta^2)
+    // Exact fast path of the nearest-volume search (rt_sarsa.hip sarsa_nearest_fast):
+    // per normal class (volumes whose normals compare equal), a uniform grid of cell
+    // size >= grid_h over the class's volume positions.
+    int use_grid = 0;
+    int n_class = 0;
+    const int32_t* tri_class = nullptr;    // [n_surf] class of each surface's normal, -1: none
+    const float4* class_org = nullptr;     // [n_class] grid origin, w = first cell (int bits)
+    const int4* class_dim = nullptr;       // [n_class] cells per axis
+    const float4* class_nrm = nullptr;     // [n_class] the class normal
+    const uint32_t* cell_start = nullptr;  // [cells + 1] first grid_leaf of each cell
+    const float4* grid_leaf = nullptr;     // [n] volume positions by (class, cell), w = volume (int bits)
+    float grid_inv_cs = 0.f;               // 1 / cell size
+    float grid_h = 0.f;                    // accept radius: sqrt(MAX_DIST) * 0.999
+    unsigned long long* grid_fallbacks = nullptr;  // optional count of KD fallbacks
 };
 constexpr int kKdStack = 32;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
 

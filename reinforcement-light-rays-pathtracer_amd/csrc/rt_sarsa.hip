@@ -76,16 +76,138 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
     return best;
 }
 
+// The same volume as sarsa_nearest, from the per-normal grid when that is provably
+// equal (rt_sarsa_host.cpp NearestGrid): the nearest same-normal volume among the
+// 3x3x3 cells around pos, if its distance is below grid_h (so the KD walk visits it)
+// and no other candidate has the same float distance (the KD walk's order would
+// break the tie).  cls: normal class of the hit surface (-1: no volume has its
+// normal, the KD walk keeps volume 0).
+__device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, int* st) {
+    if (RT_SARSA_NO_KD) return 0;
+    if (m.use_grid) {
+        if (cls < 0) return 0;
+        const float4 G = m.class_org[cls];
+        const int4 D = m.class_dim[cls];
+        const float ic = m.grid_inv_cs;
+        const int ix = (int)floorf(fminf(fmaxf((pos.x - G.x) * ic, -1.0f), (float)D.x));
+        const int iy = (int)floorf(fminf(fmaxf((pos.y - G.y) * ic, -1.0f), (float)D.y));
+        const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, -1.0f), (float)D.z));
+        // axis D.w is stored fastest (rt_sarsa_host.cpp grid_cell_id): a row of up to 3
+        // cells along it is one contiguous range; 3 x 3 rows around the query
+        const int a0 = D.w;
+        const int n0 = (a0 == 0) ? D.x : ((a0 == 1) ? D.y : D.z);
+        const int i0 = (a0 == 0) ? ix : ((a0 == 1) ? iy : iz);
+        const int n1 = (a0 == 0) ? D.y : D.x, i1 = (a0 == 0) ? iy : ix;
+        const int n2 = (a0 == 2) ? D.y : D.z, i2 = (a0 == 2) ? iy : iz;
+        const int lo0 = max(i0 - 1, 0), hi0 = min(i0 + 1, n0 - 1);
+        const uint32_t base = __float_as_uint(G.w);
+        // all 9 row ranges first (independent loads), then the candidates 4 at a time
+        uint32_t rb[9], re[9];
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const int b = i1 + (r % 3) - 1, c = i2 + (r / 3) - 1;
+            const bool ok = (b >= 0) && (b < n1) && (c >= 0) && (c < n2);
+            const uint32_t row = base + (uint32_t)(n0 * (b + n1 * c));
+            rb[r] = ok ? m.cell_start[row + lo0] : 0u;
+            re[r] = ok ? m.cell_start[row + hi0 + 1] : 0u;
+        }
+        float b1 = INFINITY, b2 = INFINITY;
+        int bv = -1;
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            const uint32_t e = re[r];
+            for (uint32_t k = rb[r]; k < e; k += 4) {
+                float4 L[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) L[u] = m.grid_leaf[min(k + (uint32_t)u, e - 1u)];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float dx = L[u].x - pos.x, dy = L[u].y - pos.y, dz = L[u].z - pos.z;
+                    const float s = (dx * dx + dy * dy) + dz * dz;  // len3's sum
+                    if (k + (uint32_t)u < e) {
+                        if (s < b1) {
+                            b2 = b1;
+                            b1 = s;
+                            bv = __float_as_int(L[u].w);
+                        } else if (s < b2) {
+                            b2 = s;
+                        }
+                    }
+                }
+            }
+        }
+        const float d = sqrtf(b1);
+        if (bv >= 0 && d < m.grid_h && sqrtf(b2) != d) {
+            const float d0 = len3(pos.x - m.root_x, pos.y - m.root_y, pos.z - m.root_z);
+            return d < d0 ? bv : 0;
+        }
+        if (m.grid_fallbacks != nullptr) atomicAdd(m.grid_fallbacks, 1ull);
+    }
+    return sarsa_nearest(m, pos, nrm, st);
+}
+
+// normal class of a query normal (queries without a surface index)
+__device__ int sarsa_class_of(const SarsaMap& m, f3 nrm) {
+    for (int c = 0; c < m.n_class; ++c) {
+        const float4 n4 = m.class_nrm[c];
+        if (nrm.x == n4.x && nrm.y == n4.y && nrm.z == n4.z) return c;
+    }
+    return -1;
+}
+
 // sample_direction_from_radiance_distribution (radiance_volume.cu:191-244)
 __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float ry, int* sector, f3* dir,
                              float* pdf) {
     const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
     int found = -1;
     float mv = 0.0f, pv = 0.0f;
-    if (r <= cdf[0]) {
+    // The CDF is non-decreasing, so the reference's binary search returns i0, the first
+    // sector with cdf > r, unless one of its probes meets cdf[k] == r (it then turns
+    // left of i0 and fails), which requires cdf[i0 - 1] == r.  i0 from two rounds of
+    // independent loads (the 12 row ends, then one 12-sector row) instead of 8
+    // dependent probes; the rare equal / NaN cases run the search itself.
+    bool exact = false;
+    const float c0 = cdf[0];
+    if (r <= c0) {
         found = 0;
-        mv = cdf[0];
+        mv = c0;
     } else {
+        float top[kGridRes];
+#pragma unroll
+        for (int x = 0; x < kGridRes; ++x) top[x] = cdf[x * kGridRes + kGridRes - 1];
+        int row = 0;
+        bool nan = false;
+#pragma unroll
+        for (int x = 0; x < kGridRes; ++x) {
+            row += (top[x] <= r) ? 1 : 0;
+            nan |= (top[x] != top[x]);
+        }
+        if (row < kGridRes && !nan) {
+            const float4* rp = reinterpret_cast<const float4*>(cdf + row * kGridRes);
+            const float4 q0 = rp[0], q1 = rp[1], q2 = rp[2];
+            const float v[kGridRes] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            int j = 0;
+            float prev = (row > 0) ? top[row - 1] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < kGridRes; ++k) {
+                const bool le = v[k] <= r;
+                j += le ? 1 : 0;
+                prev = le ? v[k] : prev;
+                nan |= (v[k] != v[k]);
+            }
+            // j < 12: the row's last value is top[row] > r
+            if (nan || prev == r) {
+                exact = true;
+            } else {
+                found = row * kGridRes + j;
+                mv = v[j < kGridRes ? j : kGridRes - 1];
+                pv = prev;
+            }
+        } else {
+            exact = nan;  // row == 12: no sector has cdf > r, the search fails
+        }
+    }
+    if (exact) {
         int start = 0, end = kSarsaSectors - 1;
         while (start <= end) {
             const int mid = (end + start) / 2;
@@ -169,24 +291,27 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
             const float4 N4 = shade[h.tri * kShadeF4 + 0];
             nrm = make3(N4.x, N4.y, N4.z);
         }
-        if (depth > 0) {
-            if (cur_rv >= 0 && cur_sector >= 0) {  // temporal_difference_update_radiance_volume_sector
-                float target;
-                int next_rv = -1;
-                if (h.tri < 0) {
-                    target = cur_brdf * a.env_light;
-                } else if (!is_surf) {
-                    target = cur_brdf * m.tri_lum[h.tri];
-                } else {
-                    next_rv = sarsa_nearest(m, pos, nrm, st);
-                    target = (m.accum[next_rv] * kIrrScale) * cur_brdf;
-                }
-                td_event(m, cur_rv, cur_sector, target);
-                cur_rv = next_rv;
-                cur_sector = -1;
+        // temporal_difference_update_radiance_volume_sector at every bounce after a
+        // sampled sector; the volume at a surface hit serves both the TD target and
+        // the next sampling step (one search call site: the search is divergent)
+        const bool td = depth > 0 && cur_rv >= 0 && cur_sector >= 0;
+        int rv = -1;
+        if (is_surf && (depth == 0 || td))
+            rv = sarsa_nearest_fast(m, m.use_grid ? m.tri_class[h.tri] : -1, pos, nrm, st);
+        if (td) {
+            float target;
+            if (h.tri < 0) {
+                target = cur_brdf * a.env_light;
+            } else if (!is_surf) {
+                target = cur_brdf * m.tri_lum[h.tri];
+            } else {
+                target = (m.accum[rv] * kIrrScale) * cur_brdf;
             }
-        } else if (is_surf) {
-            cur_rv = sarsa_nearest(m, pos, nrm, st);
+            td_event(m, cur_rv, cur_sector, target);
+            cur_rv = rv;
+            cur_sector = -1;
+        } else if (depth == 0 && is_surf) {
+            cur_rv = rv;
         }
         bool terminal = false;
         f3 L = make3(0.f, 0.f, 0.f);
@@ -326,8 +451,9 @@ __global__ __launch_bounds__(256) void k_sarsa_nearest(const SarsaMap m, const f
     __shared__ int kd_stack[kKdStack * 256];
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
-    out[i] = sarsa_nearest(m, make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]),
-                           make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]), kd_stack + threadIdx.x);
+    const f3 p = make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
+    const f3 nr = make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]);
+    out[i] = sarsa_nearest_fast(m, m.use_grid ? sarsa_class_of(m, nr) : -1, p, nr, kd_stack + threadIdx.x);
 }
 
 }  // namespace

@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -150,6 +152,131 @@ struct Tree {
     }
 };
 
+// Exact fast path of find_closest_radiance_volume_iterative (rt_sarsa.hip
+// sarsa_nearest_fast).  The KD search visits a leaf L iff, at every ancestor whose
+// split separates the query q from L, (q_k - split)^2 < MAX_DIST; the split lies
+// between q_k and L_k (left subtrees hold coordinates <= the median, right ones >=),
+// so a leaf whose float distance to q is below h = sqrt(MAX_DIST) * 0.999 is always
+// visited.  Hence when the nearest same-normal volume is closer than h and unique in
+// float distance, it is the search's result (against the initial volume 0 at the
+// distance of element 0); otherwise the kernel runs the KD search itself.  The
+// candidates closer than h lie in the 3x3x3 cells around q in a grid of cell size
+// 1.01 h over the volumes of q's normal class.
+struct NearestGrid {
+    std::vector<int32_t> tri_class;  // [n_surf]
+    std::vector<float4> org, nrm;    // [n_class]
+    std::vector<int4> dim;           // [n_class]
+    std::vector<uint32_t> start;     // [cells + 1]
+    std::vector<float4> leaf;        // [n]
+    float inv_cs = 0.f, h = 0.f;
+};
+
+constexpr size_t kMaxGridCells = (size_t)1 << 26;
+
+inline bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
+
+// class key of a normal under float ==: -0 and +0 compare equal
+std::array<uint32_t, 3> normal_key(const float* v) {
+    std::array<uint32_t, 3> k;
+    for (int c = 0; c < 3; ++c) {
+        const float x = (v[c] == 0.0f) ? 0.0f : v[c];
+        memcpy(&k[c], &x, 4);
+    }
+    return k;
+}
+
+// cell of coordinate p along one axis; the kernel evaluates the same float operations
+inline int grid_cell(float p, float o, float inv_cs) { return (int)floorf((p - o) * inv_cs); }
+
+// cell (x, y, z) -> offset in its class: axis d.w fastest, then the other two in order
+// (rt_sarsa.hip sarsa_nearest_fast)
+inline uint32_t grid_cell_id(int4 d, int x, int y, int z) {
+    const int n[3] = {d.x, d.y, d.z}, i[3] = {x, y, z};
+    const int a0 = d.w, a1 = (a0 == 0) ? 1 : 0, a2 = (a0 == 2) ? 1 : 2;
+    return (uint32_t)(i[a0] + n[a0] * (i[a1] + n[a1] * i[a2]));
+}
+
+bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>& nrm, int n,
+                        const float* normals, int n_surf, float max_dist, NearestGrid* g) {
+    g->h = sqrtf(max_dist) * 0.999f;
+    g->inv_cs = 1.0f / (g->h * 1.01f);
+    std::map<std::array<uint32_t, 3>, int> cls;
+    std::vector<int> vc(n, -1);
+    for (int i = 0; i < n; ++i) {
+        if (!finite3(&nrm[3 * i])) continue;  // never equal to any query normal
+        auto it = cls.emplace(normal_key(&nrm[3 * i]), (int)cls.size()).first;
+        vc[i] = it->second;
+    }
+    const int nc = (int)cls.size();
+    if (nc == 0) return false;
+    g->nrm.assign(nc, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (const auto& kv : cls) {
+        float v[3];
+        memcpy(v, kv.first.data(), 12);
+        g->nrm[kv.second] = make_float4(v[0], v[1], v[2], 0.f);
+    }
+    g->tri_class.assign(n_surf, -1);
+    for (int j = 0; j < n_surf; ++j) {
+        if (!finite3(normals + 3 * j)) continue;
+        auto it = cls.find(normal_key(normals + 3 * j));
+        if (it != cls.end()) g->tri_class[j] = it->second;
+    }
+    std::vector<float> lo((size_t)nc * 3, INFINITY), hi((size_t)nc * 3, -INFINITY);
+    for (int i = 0; i < n; ++i) {
+        if (vc[i] < 0) continue;
+        for (int c = 0; c < 3; ++c) {
+            lo[(size_t)vc[i] * 3 + c] = std::min(lo[(size_t)vc[i] * 3 + c], pos[4 * i + c]);
+            hi[(size_t)vc[i] * 3 + c] = std::max(hi[(size_t)vc[i] * 3 + c], pos[4 * i + c]);
+        }
+    }
+    g->org.resize(nc);
+    g->dim.resize(nc);
+    size_t cells = 0;
+    for (int k = 0; k < nc; ++k) {
+        int d[3];
+        for (int c = 0; c < 3; ++c) {
+            const float l = lo[(size_t)k * 3 + c], h = hi[(size_t)k * 3 + c];
+            if (!std::isfinite(l) || !std::isfinite(h)) return false;
+            const float span = (h - l) * g->inv_cs;
+            if (!(span < 1e6f)) return false;
+            d[c] = grid_cell(h, l, g->inv_cs) + 1;
+        }
+        uint32_t base = (uint32_t)cells;
+        float basef;
+        memcpy(&basef, &base, 4);
+        g->org[k] = make_float4(lo[(size_t)k * 3], lo[(size_t)k * 3 + 1], lo[(size_t)k * 3 + 2], basef);
+        // the longest axis is the fastest (rows of 3 cells along it are contiguous)
+        const int a0 = (d[0] >= d[1] && d[0] >= d[2]) ? 0 : ((d[1] >= d[2]) ? 1 : 2);
+        g->dim[k] = make_int4(d[0], d[1], d[2], a0);
+        cells += (size_t)d[0] * d[1] * d[2];
+        if (cells > kMaxGridCells) return false;
+    }
+    std::vector<uint32_t> cell_of(n, 0xFFFFFFFFu), count(cells + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        if (vc[i] < 0) continue;
+        const float4 o = g->org[vc[i]];
+        const int4 d = g->dim[vc[i]];
+        uint32_t base;
+        memcpy(&base, &o.w, 4);
+        const int x = grid_cell(pos[4 * i], o.x, g->inv_cs), y = grid_cell(pos[4 * i + 1], o.y, g->inv_cs),
+                  z = grid_cell(pos[4 * i + 2], o.z, g->inv_cs);
+        if (x < 0 || y < 0 || z < 0 || x >= d.x || y >= d.y || z >= d.z) return false;
+        cell_of[i] = base + grid_cell_id(d, x, y, z);
+        ++count[cell_of[i] + 1];
+    }
+    g->start.assign(cells + 1, 0);
+    for (size_t c = 0; c < cells; ++c) g->start[c + 1] = g->start[c] + count[c + 1];
+    std::vector<uint32_t> fill(g->start.begin(), g->start.end() - 1);
+    g->leaf.assign(g->start[cells], make_float4(0.f, 0.f, 0.f, 0.f));
+    for (int i = 0; i < n; ++i) {
+        if (cell_of[i] == 0xFFFFFFFFu) continue;
+        float vf;
+        memcpy(&vf, &i, 4);
+        g->leaf[fill[cell_of[i]]++] = make_float4(pos[4 * i], pos[4 * i + 1], pos[4 * i + 2], vf);
+    }
+    return true;
+}
+
 }  // namespace
 
 struct rt_sarsa {
@@ -161,6 +288,7 @@ struct rt_sarsa {
     std::vector<float> nrm;   // [n][3]
     std::vector<int32_t> surf;  // [n] surface index
     std::vector<rt::KdNode> kd;
+    int64_t grid_cells = 0;   // nearest-volume grid (0: none, every search walks the KD tree)
     rt::SarsaMap m;
     std::vector<void*> allocs;
     ~rt_sarsa() {
@@ -302,6 +430,8 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     }
     t.flatten(root, sa->nrm);
     sa->kd = t.nodes;
+    NearestGrid grid;
+    const bool have_grid = build_nearest_grid(sa->pos, sa->nrm, n, normals, n_surf, sa->m.max_dist, &grid);
 
     hipError_t e = hipSetDevice(sa->device);
     float4 *d_pos = nullptr, *d_frame = nullptr;
@@ -339,6 +469,20 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     if (e == hipSuccess) e = sa->alloc(&d_cnt, nS);
     if (e == hipSuccess) e = sa->alloc(&d_sum, nS);
     if (e == hipSuccess) e = sa->alloc(&d_kd, sa->kd.size());
+    int32_t* d_tcls = nullptr;
+    float4 *d_corg = nullptr, *d_cnrm = nullptr, *d_leaf = nullptr;
+    int4* d_cdim = nullptr;
+    uint32_t* d_cstart = nullptr;
+    unsigned long long* d_fb = nullptr;
+    if (e == hipSuccess) e = sa->alloc(&d_fb, 1);
+    if (have_grid) {
+        if (e == hipSuccess) e = sa->alloc(&d_tcls, grid.tri_class.size());
+        if (e == hipSuccess) e = sa->alloc(&d_corg, grid.org.size());
+        if (e == hipSuccess) e = sa->alloc(&d_cnrm, grid.nrm.size());
+        if (e == hipSuccess) e = sa->alloc(&d_cdim, grid.dim.size());
+        if (e == hipSuccess) e = sa->alloc(&d_cstart, grid.start.size());
+        if (e == hipSuccess) e = sa->alloc(&d_leaf, grid.leaf.size());
+    }
     auto up = [&](void* d, const void* h, size_t bytes) {
         if (e == hipSuccess && bytes) e = hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
     };
@@ -352,6 +496,15 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     up(d_cdf, cdf.data(), sizeof(float) * nS);
     up(d_acc, accum.data(), sizeof(float) * n);
     up(d_kd, kd4.data(), sizeof(uint4) * kd4.size());
+    if (have_grid) {
+        up(d_tcls, grid.tri_class.data(), sizeof(int32_t) * grid.tri_class.size());
+        up(d_corg, grid.org.data(), sizeof(float4) * grid.org.size());
+        up(d_cnrm, grid.nrm.data(), sizeof(float4) * grid.nrm.size());
+        up(d_cdim, grid.dim.data(), sizeof(int4) * grid.dim.size());
+        up(d_cstart, grid.start.data(), sizeof(uint32_t) * grid.start.size());
+        up(d_leaf, grid.leaf.data(), sizeof(float4) * grid.leaf.size());
+    }
+    if (e == hipSuccess) e = hipMemset(d_fb, 0, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(d_vis, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_sum, 0, sizeof(unsigned long long) * nS);
@@ -378,6 +531,20 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     m.root_x = sa->kd[0].px;
     m.root_y = sa->kd[0].py;
     m.root_z = sa->kd[0].pz;
+    if (have_grid) {
+        m.use_grid = 1;
+        m.n_class = (int)grid.org.size();
+        m.tri_class = d_tcls;
+        m.class_org = d_corg;
+        m.class_dim = d_cdim;
+        m.class_nrm = d_cnrm;
+        m.cell_start = d_cstart;
+        m.grid_leaf = d_leaf;
+        m.grid_inv_cs = grid.inv_cs;
+        m.grid_h = grid.h;
+        sa->grid_cells = (int64_t)grid.start.size() - 1;
+    }
+    m.grid_fallbacks = d_fb;
     *out = sa;
     return RT_OK;
 }
@@ -392,6 +559,28 @@ int rt_sarsa_info(const rt_sarsa* sa, int32_t* n_volumes, int32_t* n_nodes, uint
     if (n_volumes) *n_volumes = sa->n_vol;
     if (n_nodes) *n_nodes = (int32_t)sa->kd.size();
     if (frames) *frames = sa->frames;
+    return RT_OK;
+}
+
+int rt_sarsa_set_search(rt_sarsa* sa, int mode) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (mode != RT_SARSA_SEARCH_KD && mode != RT_SARSA_SEARCH_GRID) return err(RT_E_INVALID, "bad search mode");
+    sa->m.use_grid = (mode == RT_SARSA_SEARCH_GRID && sa->grid_cells > 0) ? 1 : 0;
+    return RT_OK;
+}
+
+int rt_sarsa_search_stats(const rt_sarsa* sa, int32_t* mode, int32_t* n_classes, int64_t* grid_cells,
+                          uint64_t* kd_fallbacks) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (mode) *mode = sa->m.use_grid ? RT_SARSA_SEARCH_GRID : RT_SARSA_SEARCH_KD;
+    if (n_classes) *n_classes = sa->m.n_class;
+    if (grid_cells) *grid_cells = sa->grid_cells;
+    if (kd_fallbacks) {
+        unsigned long long v = 0;
+        (void)hipSetDevice(sa->device);
+        RT_HIPE(hipMemcpy(&v, sa->m.grid_fallbacks, sizeof(v), hipMemcpyDeviceToHost));
+        *kd_fallbacks = v;
+    }
     return RT_OK;
 }
 

@@ -13,15 +13,19 @@ import torch
 import torch.distributed as dist
 
 
-def gather_tiles(out: torch.Tensor, gathered: torch.Tensor) -> torch.Tensor:
+def gather_tiles(out: torch.Tensor, gathered: torch.Tensor, async_op: bool = False):
     """All-gather the per-rank tile buffers (out: [k, T, T, 3]) into
-    gathered: [world, k, T, T, 3]."""
+    gathered: [world, k, T, T, 3].  async_op: return the collective's work handle
+    (RCCL runs on its own stream after the work already queued on the current one;
+    work.wait() makes the current stream wait for it) so the next frame's render
+    overlaps the exchange; None when there is nothing to wait for."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     if world == 1:
         gathered[0].copy_(out)
-        return gathered
-    dist.all_gather_into_tensor(gathered.view(world * out.shape[0], *out.shape[1:]), out)
-    return gathered
+        return None if async_op else gathered
+    work = dist.all_gather_into_tensor(gathered.view(world * out.shape[0], *out.shape[1:]), out,
+                                       async_op=async_op)
+    return work if async_op else gathered
 
 
 def sum_td(td_sum: torch.Tensor, td_count: torch.Tensor) -> None:

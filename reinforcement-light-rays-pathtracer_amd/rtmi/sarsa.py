@@ -14,6 +14,9 @@ import ctypes
 import numpy as np
 
 from ._lib import check, lib
+
+SEARCH_KD = 0    # RT_SARSA_SEARCH_KD
+SEARCH_GRID = 1  # RT_SARSA_SEARCH_GRID
 from .api import Context, Scene, _fp, _ip
 
 SECTORS = 144  # GRID_RESOLUTION^2
@@ -42,6 +45,18 @@ class RadianceMap:
         fr = ctypes.c_uint32(0)
         check(lib().rt_sarsa_info(self._h, None, None, ctypes.byref(fr)))
         return int(fr.value)
+
+    def set_search(self, mode: int) -> None:
+        """RT_SARSA_SEARCH_KD (0) or RT_SARSA_SEARCH_GRID (1, default); same results."""
+        check(lib().rt_sarsa_set_search(self._h, mode))
+
+    def search_stats(self) -> dict:
+        mode, ncls = ctypes.c_int32(0), ctypes.c_int32(0)
+        cells, fb = ctypes.c_int64(0), ctypes.c_uint64(0)
+        check(lib().rt_sarsa_search_stats(self._h, ctypes.byref(mode), ctypes.byref(ncls), ctypes.byref(cells),
+                                          ctypes.byref(fb)))
+        return {"mode": int(mode.value), "classes": int(ncls.value), "grid_cells": int(cells.value),
+                "kd_fallbacks": int(fb.value)}
 
     def volumes(self):
         n = self.n_volumes

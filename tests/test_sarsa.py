@@ -205,6 +205,69 @@ def test_gpu_nearest_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scene", ("door_room", "complex_light_room", "archway"))
+def test_gpu_nearest_grid_equals_kd(rtmi_mod, oracle_mod, gpu_ctx, scene):
+    """The grid fast path returns the KD walk's volume for every query, including
+    engineered ties (midpoints of same-normal volume pairs), volume positions, queries
+    far from any volume (KD fallback), mismatched and signed-zero normals."""
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    S = rtmi_mod.sarsa
+    try:
+        pos, nrm, _, _ = om.volumes()
+        rng = np.random.default_rng(11)
+        n = 100_000
+        i = rng.integers(0, om.n_volumes, n)
+        j = rng.integers(0, om.n_volumes, n)
+        near = pos[i] + rng.normal(0, 0.03, (n, 3)).astype(np.float32)
+        same = (nrm[i] == nrm[j]).all(axis=1)
+        mid = ((pos[i] + pos[j]) * np.float32(0.5)).astype(np.float32)[same]
+        far = rng.uniform(-3, 3, (n // 10, 3)).astype(np.float32)
+        q = np.concatenate([near, mid, pos[i[: n // 10]], far]).astype(np.float32)
+        qn = np.concatenate([nrm[i], nrm[i][same], nrm[i[: n // 10]], nrm[j[: n // 10]]]).astype(np.float32)
+        qn[::97] = nrm[rng.integers(0, om.n_volumes, len(qn[::97]))]
+        qn[::89] = np.where(qn[::89] == 0, np.float32(-0.0), qn[::89])   # -0 components
+        rm.set_search(S.SEARCH_KD)
+        a = rm.nearest(q, qn)
+        rm.set_search(S.SEARCH_GRID)
+        st0 = rm.search_stats()
+        b = rm.nearest(q, qn)
+        st1 = rm.search_stats()
+        assert st0["mode"] == S.SEARCH_GRID and st0["grid_cells"] > 0
+        assert np.array_equal(a, b)
+        assert np.array_equal(b, om.nearest(q, qn))
+        fb = st1["kd_fallbacks"] - st0["kd_fallbacks"]
+        assert fb < 0.25 * len(q), (fb, len(q))
+        # queries close to a volume of their own normal almost never need the KD walk
+        st0 = rm.search_stats()
+        rm.nearest(pos[i] + rng.normal(0, 0.005, (n, 3)).astype(np.float32), nrm[i])
+        assert rm.search_stats()["kd_fallbacks"] - st0["kd_fallbacks"] < 0.01 * n
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ("door_room", "complex_light_room"))
+def test_gpu_render_grid_equals_kd(rtmi_mod, gpu_ctx, scene):
+    g = geometry(rtmi_mod, scene)
+    sc = rtmi_mod.Scene(gpu_ctx, g)
+    maps = [rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) for _ in range(2)]
+    try:
+        maps[0].set_search(rtmi_mod.sarsa.SEARCH_KD)
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=96, spp=16, spp_split=4)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+        for _ in range(2):
+            (ia, ca), (ib, cb) = [m.render(cam, p, 1) for m in maps]
+            assert ca == cb and np.array_equal(ia, ib)
+            for a, b in zip(maps[0].read(), maps[1].read()):
+                assert np.array_equal(a, b)
+    finally:
+        for m in maps:
+            m.close()
+        sc.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("scene,split,hit_rule", [("door_room", 1, 1), ("door_room", 4, 1), ("cornell", 2, 1),
                                                    ("archway", 1, 0)])
 def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, split, hit_rule):

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--split", type=int, default=8)
     ap.add_argument("--frames", type=int, default=4)
     ap.add_argument("--tile", type=int, default=32)
+    ap.add_argument("--search", choices=("grid", "kd"), default="grid")
     ap.add_argument("--lib", default=None, help="librtmi.so variant directory (A/B timing)")
     args = ap.parse_args()
     if args.lib:
@@ -39,6 +40,7 @@ def main():
     ctx = rtmi.Context(0)
     sc = rtmi.Scene(ctx, g)
     rm = rtmi.sarsa.RadianceMap(ctx, sc, 1984)
+    rm.set_search(rtmi.sarsa.SEARCH_GRID if args.search == "grid" else rtmi.sarsa.SEARCH_KD)
     p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=args.width, height=args.width, spp=args.spp,
                             spp_split=args.split)
     cam = rtmi.camera(rtmi.CAMERAS[args.scene])
@@ -63,7 +65,7 @@ def main():
         print(json.dumps(frames[-1]), file=sys.stderr, flush=True)
     q, cdf, vis, acc = rm.read()
     res = {"lib": args.lib or "build", "scene": args.scene, "width": args.width, "spp": args.spp, "volumes": rm.n_volumes,
-           "frames": frames, "visits": int(vis.sum()), "q_max": float(q.max()),
+           "frames": frames, "search": rm.search_stats(), "visits": int(vis.sum()), "q_max": float(q.max()),
            "finite": bool(np.isfinite(out.cpu().numpy()).all())}
     print(json.dumps(res))
     rm.close()
