@@ -27,6 +27,9 @@
 #ifndef RT_SARSA_NO_KD
 #define RT_SARSA_NO_KD 0
 #endif
+#ifndef RT_SARSA_NO_FALLBACK  // grid answer even where the KD walk is needed (timing only)
+#define RT_SARSA_NO_FALLBACK 0
+#endif
 
 namespace rt {
 
@@ -89,49 +92,30 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
         const float4 G = m.class_org[cls];
         const int4 D = m.class_dim[cls];
         const float ic = m.grid_inv_cs;
-        const int ix = (int)floorf(fminf(fmaxf((pos.x - G.x) * ic, -1.0f), (float)D.x));
-        const int iy = (int)floorf(fminf(fmaxf((pos.y - G.y) * ic, -1.0f), (float)D.y));
-        const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, -1.0f), (float)D.z));
-        // axis D.w is stored fastest (rt_sarsa_host.cpp grid_cell_id): a row of up to 3
-        // cells along it is one contiguous range; 3 x 3 rows around the query
-        const int a0 = D.w;
-        const int n0 = (a0 == 0) ? D.x : ((a0 == 1) ? D.y : D.z);
-        const int i0 = (a0 == 0) ? ix : ((a0 == 1) ? iy : iz);
-        const int n1 = (a0 == 0) ? D.y : D.x, i1 = (a0 == 0) ? iy : ix;
-        const int n2 = (a0 == 2) ? D.y : D.z, i2 = (a0 == 2) ? iy : iz;
-        const int lo0 = max(i0 - 1, 0), hi0 = min(i0 + 1, n0 - 1);
-        const uint32_t base = __float_as_uint(G.w);
-        // all 9 row ranges first (independent loads), then the candidates 4 at a time
-        uint32_t rb[9], re[9];
-#pragma unroll
-        for (int r = 0; r < 9; ++r) {
-            const int b = i1 + (r % 3) - 1, c = i2 + (r / 3) - 1;
-            const bool ok = (b >= 0) && (b < n1) && (c >= 0) && (c < n2);
-            const uint32_t row = base + (uint32_t)(n0 * (b + n1 * c));
-            rb[r] = ok ? m.cell_start[row + lo0] : 0u;
-            re[r] = ok ? m.cell_start[row + hi0 + 1] : 0u;
-        }
+        // padded cell of the query (rt_sarsa_host.cpp grid_cell): its list holds every
+        // class volume of the 3x3x3 neighbourhood
+        const int ix = (int)floorf(fminf(fmaxf((pos.x - G.x) * ic, 0.0f), (float)(D.x - 1)));
+        const int iy = (int)floorf(fminf(fmaxf((pos.y - G.y) * ic, 0.0f), (float)(D.y - 1)));
+        const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, 0.0f), (float)(D.z - 1)));
+        const uint32_t c = __float_as_uint(G.w) + (uint32_t)((iz * D.y + iy) * D.x + ix);
+        const uint32_t k0 = m.cell_start[c], e = m.cell_start[c + 1];
         float b1 = INFINITY, b2 = INFINITY;
         int bv = -1;
+        for (uint32_t k = k0; k < e; k += 4) {  // 4 candidate loads in flight
+            float4 L[4];
 #pragma unroll
-        for (int r = 0; r < 9; ++r) {
-            const uint32_t e = re[r];
-            for (uint32_t k = rb[r]; k < e; k += 4) {
-                float4 L[4];
+            for (int u = 0; u < 4; ++u) L[u] = m.grid_leaf[min(k + (uint32_t)u, e - 1u)];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) L[u] = m.grid_leaf[min(k + (uint32_t)u, e - 1u)];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const float dx = L[u].x - pos.x, dy = L[u].y - pos.y, dz = L[u].z - pos.z;
-                    const float s = (dx * dx + dy * dy) + dz * dz;  // len3's sum
-                    if (k + (uint32_t)u < e) {
-                        if (s < b1) {
-                            b2 = b1;
-                            b1 = s;
-                            bv = __float_as_int(L[u].w);
-                        } else if (s < b2) {
-                            b2 = s;
-                        }
+            for (int u = 0; u < 4; ++u) {
+                const float dx = L[u].x - pos.x, dy = L[u].y - pos.y, dz = L[u].z - pos.z;
+                const float s = (dx * dx + dy * dy) + dz * dz;  // len3's sum
+                if (k + (uint32_t)u < e) {
+                    if (s < b1) {
+                        b2 = b1;
+                        b1 = s;
+                        bv = __float_as_int(L[u].w);
+                    } else if (s < b2) {
+                        b2 = s;
                     }
                 }
             }
@@ -142,6 +126,7 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
             return d < d0 ? bv : 0;
         }
         if (m.grid_fallbacks != nullptr) atomicAdd(m.grid_fallbacks, 1ull);
+        if (RT_SARSA_NO_FALLBACK) return bv >= 0 ? bv : 0;
     }
     return sarsa_nearest(m, pos, nrm, st);
 }

@@ -159,15 +159,18 @@ struct Tree {
 // so a leaf whose float distance to q is below h = sqrt(MAX_DIST) * 0.999 is always
 // visited.  Hence when the nearest same-normal volume is closer than h and unique in
 // float distance, it is the search's result (against the initial volume 0 at the
-// distance of element 0); otherwise the kernel runs the KD search itself.  The
-// candidates closer than h lie in the 3x3x3 cells around q in a grid of cell size
-// 1.01 h over the volumes of q's normal class.
+// distance of element 0); otherwise the kernel runs the KD search itself.  Every
+// leaf closer than h lies in the 3x3x3 cells around q in a grid of cell size 1.01 h
+// over the volumes of q's normal class; each cell stores that whole neighbourhood
+// as one contiguous candidate list (27 copies of every volume position), so a query
+// reads one range.  The grid has one padding cell per side (queries are clamped
+// into it; a clamped query has no volume within h and falls back).
 struct NearestGrid {
     std::vector<int32_t> tri_class;  // [n_surf]
     std::vector<float4> org, nrm;    // [n_class]
-    std::vector<int4> dim;           // [n_class]
+    std::vector<int4> dim;           // [n_class] padded cells per axis
     std::vector<uint32_t> start;     // [cells + 1]
-    std::vector<float4> leaf;        // [n]
+    std::vector<float4> leaf;        // [27 n]
     float inv_cs = 0.f, h = 0.f;
 };
 
@@ -185,21 +188,16 @@ std::array<uint32_t, 3> normal_key(const float* v) {
     return k;
 }
 
-// cell of coordinate p along one axis; the kernel evaluates the same float operations
-inline int grid_cell(float p, float o, float inv_cs) { return (int)floorf((p - o) * inv_cs); }
-
-// cell (x, y, z) -> offset in its class: axis d.w fastest, then the other two in order
-// (rt_sarsa.hip sarsa_nearest_fast)
-inline uint32_t grid_cell_id(int4 d, int x, int y, int z) {
-    const int n[3] = {d.x, d.y, d.z}, i[3] = {x, y, z};
-    const int a0 = d.w, a1 = (a0 == 0) ? 1 : 0, a2 = (a0 == 2) ? 1 : 2;
-    return (uint32_t)(i[a0] + n[a0] * (i[a1] + n[a1] * i[a2]));
+// padded cell of coordinate p along one axis (the kernel's float operations and clamp)
+inline int grid_cell(float p, float o, float inv_cs, int n) {
+    return (int)floorf(fminf(fmaxf((p - o) * inv_cs, 0.0f), (float)(n - 1)));
 }
 
 bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>& nrm, int n,
                         const float* normals, int n_surf, float max_dist, NearestGrid* g) {
     g->h = sqrtf(max_dist) * 0.999f;
-    g->inv_cs = 1.0f / (g->h * 1.01f);
+    const float cs = g->h * 1.01f;
+    g->inv_cs = 1.0f / cs;
     std::map<std::array<uint32_t, 3>, int> cls;
     std::vector<int> vc(n, -1);
     for (int i = 0; i < n; ++i) {
@@ -234,46 +232,68 @@ bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>&
     size_t cells = 0;
     for (int k = 0; k < nc; ++k) {
         int d[3];
+        float o[3];
         for (int c = 0; c < 3; ++c) {
             const float l = lo[(size_t)k * 3 + c], h = hi[(size_t)k * 3 + c];
-            if (!std::isfinite(l) || !std::isfinite(h)) return false;
-            const float span = (h - l) * g->inv_cs;
-            if (!(span < 1e6f)) return false;
-            d[c] = grid_cell(h, l, g->inv_cs) + 1;
+            if (!std::isfinite(l) || !std::isfinite(h) || !((h - l) * g->inv_cs < 1e6f)) return false;
+            o[c] = l - 1.5f * cs;  // a padding cell below (volumes bin to cells >= 1)
+            d[c] = (int)floorf((h - o[c]) * g->inv_cs) + 2;  // ... and at least one above
         }
-        uint32_t base = (uint32_t)cells;
+        const uint32_t base = (uint32_t)cells;
         float basef;
         memcpy(&basef, &base, 4);
-        g->org[k] = make_float4(lo[(size_t)k * 3], lo[(size_t)k * 3 + 1], lo[(size_t)k * 3 + 2], basef);
-        // the longest axis is the fastest (rows of 3 cells along it are contiguous)
-        const int a0 = (d[0] >= d[1] && d[0] >= d[2]) ? 0 : ((d[1] >= d[2]) ? 1 : 2);
-        g->dim[k] = make_int4(d[0], d[1], d[2], a0);
+        g->org[k] = make_float4(o[0], o[1], o[2], basef);
+        g->dim[k] = make_int4(d[0], d[1], d[2], 0);
         cells += (size_t)d[0] * d[1] * d[2];
         if (cells > kMaxGridCells) return false;
     }
-    std::vector<uint32_t> cell_of(n, 0xFFFFFFFFu), count(cells + 1, 0);
+    // volumes binned per cell
+    std::vector<uint32_t> cell_of(n, 0xFFFFFFFFu), cnt(cells + 1, 0);
     for (int i = 0; i < n; ++i) {
         if (vc[i] < 0) continue;
         const float4 o = g->org[vc[i]];
         const int4 d = g->dim[vc[i]];
         uint32_t base;
         memcpy(&base, &o.w, 4);
-        const int x = grid_cell(pos[4 * i], o.x, g->inv_cs), y = grid_cell(pos[4 * i + 1], o.y, g->inv_cs),
-                  z = grid_cell(pos[4 * i + 2], o.z, g->inv_cs);
-        if (x < 0 || y < 0 || z < 0 || x >= d.x || y >= d.y || z >= d.z) return false;
-        cell_of[i] = base + grid_cell_id(d, x, y, z);
-        ++count[cell_of[i] + 1];
+        const int x = grid_cell(pos[4 * i], o.x, g->inv_cs, d.x), y = grid_cell(pos[4 * i + 1], o.y, g->inv_cs, d.y),
+                  z = grid_cell(pos[4 * i + 2], o.z, g->inv_cs, d.z);
+        if (x < 1 || y < 1 || z < 1 || x > d.x - 2 || y > d.y - 2 || z > d.z - 2) return false;
+        cell_of[i] = base + (uint32_t)((z * d.y + y) * d.x + x);
+        ++cnt[cell_of[i] + 1];
     }
+    std::vector<uint32_t> own(cells + 1, 0);
+    for (size_t c = 0; c < cells; ++c) own[c + 1] = own[c] + cnt[c + 1];
+    std::vector<uint32_t> fill(own.begin(), own.end() - 1), vol_in(own[cells]);
+    for (int i = 0; i < n; ++i)
+        if (cell_of[i] != 0xFFFFFFFFu) vol_in[fill[cell_of[i]]++] = (uint32_t)i;
+    // neighbourhood lists
     g->start.assign(cells + 1, 0);
-    for (size_t c = 0; c < cells; ++c) g->start[c + 1] = g->start[c] + count[c + 1];
-    std::vector<uint32_t> fill(g->start.begin(), g->start.end() - 1);
-    g->leaf.assign(g->start[cells], make_float4(0.f, 0.f, 0.f, 0.f));
-    for (int i = 0; i < n; ++i) {
-        if (cell_of[i] == 0xFFFFFFFFu) continue;
-        float vf;
-        memcpy(&vf, &i, 4);
-        g->leaf[fill[cell_of[i]]++] = make_float4(pos[4 * i], pos[4 * i + 1], pos[4 * i + 2], vf);
+    g->leaf.clear();
+    g->leaf.reserve((size_t)27 * own[cells]);
+    for (int k = 0; k < nc; ++k) {
+        const int4 d = g->dim[k];
+        uint32_t base;
+        memcpy(&base, &g->org[k].w, 4);
+        for (int z = 0; z < d.z; ++z)
+            for (int y = 0; y < d.y; ++y)
+                for (int x = 0; x < d.x; ++x) {
+                    const uint32_t c = base + (uint32_t)((z * d.y + y) * d.x + x);
+                    g->start[c] = (uint32_t)g->leaf.size();
+                    for (int zz = std::max(z - 1, 0); zz <= std::min(z + 1, d.z - 1); ++zz)
+                        for (int yy = std::max(y - 1, 0); yy <= std::min(y + 1, d.y - 1); ++yy)
+                            for (int xx = std::max(x - 1, 0); xx <= std::min(x + 1, d.x - 1); ++xx) {
+                                const uint32_t nb = base + (uint32_t)((zz * d.y + yy) * d.x + xx);
+                                for (uint32_t t = own[nb]; t < own[nb + 1]; ++t) {
+                                    const int v = (int)vol_in[t];
+                                    float vf;
+                                    memcpy(&vf, &v, 4);
+                                    g->leaf.push_back(make_float4(pos[4 * v], pos[4 * v + 1], pos[4 * v + 2], vf));
+                                }
+                            }
+                    if (g->leaf.size() > ((size_t)1 << 31)) return false;
+                }
     }
+    g->start[cells] = (uint32_t)g->leaf.size();
     return true;
 }
 
