@@ -171,13 +171,14 @@ constexpr int kSarsaSectors = 144;
 struct SarsaMap {
     int n_vol = 0;
     const float4* vol_pos = nullptr;    // [n] sampled position
-    const float4* vol_frame = nullptr;  // [n*3] N, T, B (create_transformation_matrix)
+    const float4* vol_frame = nullptr;  // [n*3] N, T, B (create_transformation_matrix); w: position x, y, z
     const float* vol_brdf = nullptr;    // [n] luminance/pi of the volume's surface
     const float* cos_center = nullptr;  // [n*144] cos of the cell-centre directions
     const float* cos_corner = nullptr;  // [n*144] cos of the cell-corner directions
     const float* tri_lum = nullptr;     // [n_tri] Material/AreaLight luminance 0.5*(max+min)
     float* Q = nullptr;                 // [n*144] radiance_grid
     float* cdf = nullptr;               // [n*144] radiance_distribution
+    float4* cdf_top = nullptr;          // [n*4] {cdf[0], cdf[11], cdf[23], .., cdf[143], 0, 0, 0}: row ends
     uint32_t* visits = nullptr;         // [n*144]
     float* accum = nullptr;             // [n] irradiance_accum
     unsigned long long* acc_sum = nullptr;  // [n*144] frame TD targets, fixed point 2^-32

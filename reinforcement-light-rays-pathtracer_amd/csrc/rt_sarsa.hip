@@ -152,14 +152,14 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     // independent loads (the 12 row ends, then one 12-sector row) instead of 8
     // dependent probes; the rare equal / NaN cases run the search itself.
     bool exact = false;
-    const float c0 = cdf[0];
+    const float4* tp = m.cdf_top + (size_t)rv * 4;  // one 64-B line: cdf[0] and the row ends
+    const float4 t0 = tp[0], t1 = tp[1], t2 = tp[2], t3 = tp[3];
+    const float c0 = t0.x;
     if (r <= c0) {
         found = 0;
         mv = c0;
     } else {
-        float top[kGridRes];
-#pragma unroll
-        for (int x = 0; x < kGridRes; ++x) top[x] = cdf[x * kGridRes + kGridRes - 1];
+        const float top[kGridRes] = {t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w, t2.x, t2.y, t2.z, t2.w, t3.x};
         int row = 0;
         bool nan = false;
 #pragma unroll
@@ -215,10 +215,9 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     const int sy = found - sx * kGridRes;
     *sector = found;
     *pdf = kRho * ((found == 0 ? mv : (mv - pv)) / kGridRhoS);
-    const float4 p4 = m.vol_pos[rv];
     const float4 N4 = m.vol_frame[rv * 3 + 0], T4 = m.vol_frame[rv * 3 + 1], B4 = m.vol_frame[rv * 3 + 2];
     *dir = grid_direction((float)sx + rx, (float)sy + ry, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
-                          make3(B4.x, B4.y, B4.z), make3(p4.x, p4.y, p4.z));
+                          make3(B4.x, B4.y, B4.z), make3(N4.w, T4.w, B4.w));
     return true;
 }
 
@@ -421,11 +420,14 @@ __global__ __launch_bounds__(256) void k_sarsa_apply(const SarsaMap m) {
         total += t;
     }
     float prev = 0.0f;
+    float* top = reinterpret_cast<float*>(m.cdf_top + (size_t)v * 4);
     for (int k = 0; k < kSarsaSectors; ++k) {
         float t = m.Q[b + k] * m.cos_center[b + k];
         t = t > 0.0f ? t : 0.0f;
         const float rad = t / total + prev;
         m.cdf[b + k] = rad;
+        if (k == 0) top[0] = rad;
+        if (k % kGridRes == kGridRes - 1) top[1 + k / kGridRes] = rad;
         prev = rad;
     }
 }

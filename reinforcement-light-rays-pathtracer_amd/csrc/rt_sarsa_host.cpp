@@ -415,7 +415,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         const rt::f3 P = rt::make3(sa->pos[4 * i], sa->pos[4 * i + 1], sa->pos[4 * i + 2]);
         rt::f3 T, B;
         rt::normal_frame(N, &T, &B);
-        const float f[12] = {N.x, N.y, N.z, 0.f, T.x, T.y, T.z, 0.f, B.x, B.y, B.z, 0.f};
+        const float f[12] = {N.x, N.y, N.z, P.x, T.x, T.y, T.z, P.y, B.x, B.y, B.z, P.z};
         memcpy(&frame[(size_t)12 * i], f, sizeof(f));
         const float lum = luminance(albedo + 3 * sa->surf[i]);
         brdf[i] = lum / rt::kPi;
@@ -484,6 +484,8 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     if (e == hipSuccess) e = sa->alloc(&d_lum, tri_lum.size());
     if (e == hipSuccess) e = sa->alloc(&d_Q, nS);
     if (e == hipSuccess) e = sa->alloc(&d_cdf, nS);
+    float4* d_top = nullptr;
+    if (e == hipSuccess) e = sa->alloc(&d_top, (size_t)n * 4);
     if (e == hipSuccess) e = sa->alloc(&d_acc, n);
     if (e == hipSuccess) e = sa->alloc(&d_vis, nS);
     if (e == hipSuccess) e = sa->alloc(&d_cnt, nS);
@@ -514,6 +516,15 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     up(d_lum, tri_lum.data(), sizeof(float) * tri_lum.size());
     up(d_Q, Q.data(), sizeof(float) * nS);
     up(d_cdf, cdf.data(), sizeof(float) * nS);
+    {
+        std::vector<float> top((size_t)n * 16, 0.f);
+        for (int i = 0; i < n; ++i) {
+            top[(size_t)16 * i] = cdf[(size_t)i * S];
+            for (int x = 0; x < rt::kGridRes; ++x)
+                top[(size_t)16 * i + 1 + x] = cdf[(size_t)i * S + x * rt::kGridRes + rt::kGridRes - 1];
+        }
+        up(d_top, top.data(), sizeof(float) * top.size());
+    }
     up(d_acc, accum.data(), sizeof(float) * n);
     up(d_kd, kd4.data(), sizeof(uint4) * kd4.size());
     if (have_grid) {
@@ -542,6 +553,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     m.tri_lum = d_lum;
     m.Q = d_Q;
     m.cdf = d_cdf;
+    m.cdf_top = d_top;
     m.visits = d_vis;
     m.accum = d_acc;
     m.acc_sum = d_sum;

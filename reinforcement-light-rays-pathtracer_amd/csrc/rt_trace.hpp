@@ -12,6 +12,18 @@ namespace rt {
 
 constexpr float kRho = 1.0f / (2.0f * kPi);  // RHO: GPU/constants/image_settings.h:14
 
+// Triangle records are read-only for a launch: loads through the constant address
+// space are selected as scalar loads (SGPR broadcast) whenever the address is
+// wave-uniform, even in kernels with global stores or atomics in the loop (the
+// compiler otherwise falls back to per-lane vector loads of the same address there).
+typedef float __attribute__((ext_vector_type(4))) f32x4_t;
+typedef __attribute__((address_space(4))) const f32x4_t cfloat4;
+__device__ __forceinline__ cfloat4* as_const(const float4* p) { return (cfloat4*)p; }
+__device__ __forceinline__ float4 ldc(cfloat4* p) {
+    const f32x4_t v = *p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 struct Hit {
     float t;
     int tri;
@@ -128,8 +140,9 @@ __device__ __forceinline__ void exact_test(float detA, float det_t, float det_u,
 }
 
 template <int RULE>
-__device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n_tri, f3 o, f3 d,
+__device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri_g, int n_tri, f3 o, f3 d,
                                            float t_scale) {
+    cfloat4* __restrict__ tri = as_const(tri_g);
     const float nDx = -(d.x * t_scale);
     const float nDy = -(d.y * t_scale);
     const float nDz = -(d.z * t_scale);
@@ -142,9 +155,9 @@ __device__ __forceinline__ Hit closest_hit(const float4* __restrict__ tri, int n
 #endif
 #pragma unroll RT_UNROLL
     for (int i = 0; i < n_tri; ++i) {
-        const float4 A = tri[i * kIsectF4 + 0];
-        const float4 E1 = tri[i * kIsectF4 + 1];
-        const float4 E2 = tri[i * kIsectF4 + 2];
+        const float4 A = ldc(tri + i * kIsectF4 + 0);
+        const float4 E1 = ldc(tri + i * kIsectF4 + 1);
+        const float4 E2 = ldc(tri + i * kIsectF4 + 2);
         const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
         // detA = det(-D, e1, e2)
         const float s1 = nDy * E2.z - E2.y * nDz;
@@ -262,10 +275,10 @@ __device__ __forceinline__ void exact_one(const float4* __restrict__ tri, int i,
 // and an exact zero is +0), so each sign bit equals the comparison it stands for.
 // Finite inputs only (the caller keeps every triangle of a non-finite ray).
 template <int RULE>
-__device__ __forceinline__ void filter_eval(const float4* __restrict__ f, f3 o, f3 d, float Rx,
+__device__ __forceinline__ void filter_eval(cfloat4* __restrict__ f, f3 o, f3 d, float Rx,
                                             float Ry, float Rz, float ets, float* x1, float* x2,
                                             float* x3) {
-    const float4 F0 = f[0], F1 = f[1], F2 = f[2], F3 = f[3], F4 = f[4];
+    const float4 F0 = ldc(f + 0), F1 = ldc(f + 1), F2 = ldc(f + 2), F3 = ldc(f + 3), F4 = ldc(f + 4);
     const float ad = fmaf(d.x, F0.x, fmaf(d.y, F0.y, d.z * F0.z));
     const float tt = fmaf(-o.x, F0.x, fmaf(-o.y, F0.y, fmaf(-o.z, F0.z, F0.w)));
     const float uu = fmaf(F1.x, Rx, fmaf(F1.y, Ry, fmaf(F1.z, Rz,
@@ -295,7 +308,7 @@ __device__ __forceinline__ uint32_t keep_bit(float x1, float x2, float x3) {
 // at bit 0 (v_alignbit), so triangle j ends at bit cnt-1-j (the pad falls off the
 // bottom).  `finite`: false for a ray with a non-finite component (keep all).
 template <int RULE>
-__device__ __forceinline__ uint32_t filter_block(const float4* __restrict__ f, int cnt, bool finite,
+__device__ __forceinline__ uint32_t filter_block(cfloat4* __restrict__ f, int cnt, bool finite,
                                                  f3 o, f3 d, float Rx, float Ry, float Rz,
                                                  float ets) {
     uint32_t mask = 0u;
@@ -346,10 +359,10 @@ __device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ f
         const int c0 = min(32, n_tri - base);
         const int c1 = min(32, n_tri - base - 32);
         const uint32_t m0 =
-            filter_block<RULE>(filt + (size_t)base * kFiltF4, c0, finite, o, d, Rx, Ry, Rz, ets);
+            filter_block<RULE>(as_const(filt) + (size_t)base * kFiltF4, c0, finite, o, d, Rx, Ry, Rz, ets);
         uint32_t m1 = 0u;
         if (c1 > 0)
-            m1 = filter_block<RULE>(filt + (size_t)(base + 32) * kFiltF4, c1, finite, o, d, Rx, Ry,
+            m1 = filter_block<RULE>(as_const(filt) + (size_t)(base + 32) * kFiltF4, c1, finite, o, d, Rx, Ry,
                                     Rz, ets);
         exact_block<RULE>(tri, base, c0, m0, o, nDx, nDy, nDz, h);
         if (c1 > 0) exact_block<RULE>(tri, base + 32, c1, m1, o, nDx, nDy, nDz, h);
