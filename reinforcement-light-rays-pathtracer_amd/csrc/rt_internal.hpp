@@ -199,6 +199,7 @@ struct SarsaMap {
     const uint32_t* cell_start = nullptr;  // [cells + 1] first grid_leaf of each cell
     const float4* grid_leaf = nullptr;     // [n] volume positions by (class, cell), w = volume (int bits)
     float grid_inv_cs = 0.f;               // 1 / cell size
+    float grid_cs = 0.f;                   // cell size (cell centres: org + (i + 0.5) cs)
     float grid_h = 0.f;                    // accept radius: sqrt(MAX_DIST) * 0.999
     unsigned long long* grid_fallbacks = nullptr;  // optional count of KD fallbacks
 };

@@ -99,12 +99,25 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
         const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, 0.0f), (float)(D.z - 1)));
         const uint32_t c = __float_as_uint(G.w) + (uint32_t)((iz * D.y + iy) * D.x + ix);
         const uint32_t k0 = m.cell_start[c], e = m.cell_start[c + 1];
+        // The list is sorted by distance to the cell centre C: d(q, L) >= d(C, L) - d(q, C),
+        // so once d(C, L) exceeds best + d(q, C) (with a 2^-12 margin: such a candidate's
+        // float distance is strictly above the best, no tie either) no later one can win.
+        const float cx = G.x + ((float)ix + 0.5f) * m.grid_cs;
+        const float cy = G.y + ((float)iy + 0.5f) * m.grid_cs;
+        const float cz = G.z + ((float)iz + 0.5f) * m.grid_cs;
+        const float qx = pos.x - cx, qy = pos.y - cy, qz = pos.z - cz;
+        const float dq = __builtin_sqrtf((qx * qx + qy * qy) + qz * qz);
         float b1 = INFINITY, b2 = INFINITY;
         int bv = -1;
         for (uint32_t k = k0; k < e; k += 4) {  // 4 candidate loads in flight
             float4 L[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) L[u] = m.grid_leaf[min(k + (uint32_t)u, e - 1u)];
+            {
+                const float lim = (__builtin_sqrtf(b1) + dq) * (1.0f + 0x1p-12f) + 1e-6f;
+                const float ex = L[0].x - cx, ey = L[0].y - cy, ez = L[0].z - cz;
+                if ((ex * ex + ey * ey) + ez * ez > lim * lim) break;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const float dx = L[u].x - pos.x, dy = L[u].y - pos.y, dz = L[u].z - pos.z;

@@ -171,7 +171,7 @@ struct NearestGrid {
     std::vector<int4> dim;           // [n_class] padded cells per axis
     std::vector<uint32_t> start;     // [cells + 1]
     std::vector<float4> leaf;        // [27 n]
-    float inv_cs = 0.f, h = 0.f;
+    float inv_cs = 0.f, cs = 0.f, h = 0.f;
 };
 
 constexpr size_t kMaxGridCells = (size_t)1 << 26;
@@ -197,6 +197,7 @@ bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>&
                         const float* normals, int n_surf, float max_dist, NearestGrid* g) {
     g->h = sqrtf(max_dist) * 0.999f;
     const float cs = g->h * 1.01f;
+    g->cs = cs;
     g->inv_cs = 1.0f / cs;
     std::map<std::array<uint32_t, 3>, int> cls;
     std::vector<int> vc(n, -1);
@@ -290,6 +291,17 @@ bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>&
                                     g->leaf.push_back(make_float4(pos[4 * v], pos[4 * v + 1], pos[4 * v + 2], vf));
                                 }
                             }
+                    // ascending distance to the cell centre (the kernel's float centre):
+                    // the search stops at the first candidate that cannot beat its best
+                    const float cx = g->org[k].x + ((float)x + 0.5f) * cs;
+                    const float cy = g->org[k].y + ((float)y + 0.5f) * cs;
+                    const float cz = g->org[k].z + ((float)z + 0.5f) * cs;
+                    auto dc = [&](const float4& L) {
+                        const double dx = (double)L.x - cx, dy = (double)L.y - cy, dz = (double)L.z - cz;
+                        return dx * dx + dy * dy + dz * dz;
+                    };
+                    std::stable_sort(g->leaf.begin() + g->start[c], g->leaf.end(),
+                                     [&](const float4& a, const float4& b) { return dc(a) < dc(b); });
                     if (g->leaf.size() > ((size_t)1 << 31)) return false;
                 }
     }
@@ -573,6 +585,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         m.cell_start = d_cstart;
         m.grid_leaf = d_leaf;
         m.grid_inv_cs = grid.inv_cs;
+        m.grid_cs = grid.cs;
         m.grid_h = grid.h;
         sa->grid_cells = (int64_t)grid.start.size() - 1;
     }
