@@ -101,7 +101,8 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 // ---------------------------------------------------------------------------
 template <bool LAST, int MT>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
-                                          __bf16* out_lds, int out_stride, float* q_rows, int rows_valid) {
+                                          __bf16* out_lds, int out_stride, float* q, int row0, int ldq,
+                                          int rows_valid) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int K = net.K[L];
@@ -157,18 +158,24 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
             const int col = nt[j] * 16 + r16;
             const float bj = bias[col];
 #pragma unroll
-            for (int m = 0; m < MT; ++m)
+            for (int m = 0; m < MT; ++m) {
+                float v4[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = m * 16 + (lane >> 4) * 4 + r;
                     float v = acc[m][j][r] + bj;
                     v = v > 0.0f ? v : 0.0f;
+                    v4[r] = v;
                     if (LAST) {
-                        if (row < rows_valid) q_rows[(size_t)row * kDqnActions + col] = v;
+                        if (ldq == 0 && row < rows_valid) q[(size_t)(row0 + row) * kDqnActions + col] = v;
                     } else {
                         out_lds[row * out_stride + col] = (__bf16)v;
                     }
                 }
+                if (LAST && ldq > 0)  // 4 consecutive rows of one action: one 16-B store
+                    *reinterpret_cast<float4*>(q + (size_t)col * ldq + row0 + m * 16 + (lane >> 4) * 4) =
+                        make_float4(v4[0], v4[1], v4[2], v4[3]);
+            }
         }
     }
 }
@@ -178,7 +185,7 @@ template <int MT>
 __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
-                                                 float* __restrict__ q) {
+                                                 float* __restrict__ q, int ldq) {
     constexpr int kRows = MT * 16;
     __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrideA];
     __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrideB];
@@ -201,14 +208,13 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
         locs[row * 3 + 2] = z;
     }
     __syncthreads();
-    float* q_rows = q + (size_t)row0 * kDqnActions;
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
     __syncthreads();
-    mlp_layer<false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA, q_rows, rows_valid);
+    mlp_layer<false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA, q, row0, ldq, rows_valid);
     __syncthreads();
-    mlp_layer<false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB, q_rows, rows_valid);
+    mlp_layer<false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB, q, row0, ldq, rows_valid);
     __syncthreads();
-    mlp_layer<true, MT>(net, 3, bufB, kStrideB, nullptr, 0, q_rows, rows_valid);
+    mlp_layer<true, MT>(net, 3, bufB, kStrideB, nullptr, 0, q, row0, ldq, rows_valid);
 }
 
 struct SampleOut {
@@ -218,7 +224,8 @@ struct SampleOut {
 
 // importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray;
 // q: its 144 Q values, overwritten with Q*cos (as the reference does in place).
-__device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, f3 N, f3 T, f3 B, f3 pos,
+// q[a * qs]: qs = 1 for a [row][144] buffer, ldq for the action-major one.
+__device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t qs, f3 N, f3 T, f3 B, f3 pos,
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
                                                    uint32_t k0, uint32_t k1, f3* tp, bool update_tp) {
     uint32_t o[4];
@@ -235,8 +242,8 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, f3 N, 
             const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
             const f3 d = grid_direction((float)gxi + r1, (float)gyi + r2, N, T, B, pos);
             const float c = dot(N, d);
-            const float qc = q[a] * c;
-            q[a] = qc;
+            const float qc = q[(size_t)a * qs] * c;
+            q[(size_t)a * qs] = qc;
             total = total + qc;
         }
     }
@@ -246,7 +253,7 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, f3 N, 
     float q_sum = 0.0f;
     float qd_sel = 0.0f;
     for (int a = 0; a < kDqnActions; ++a) {
-        const float qd = q[a] / total;
+        const float qd = q[(size_t)a * qs] / total;
         q_sum = q_sum + qd;
         if (q_sum > rv) {
             res.action = a;
@@ -378,7 +385,7 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sampl
         const float4 T4 = a.scene.shade[tri * kShadeF4 + 1];
         const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
         const SampleOut so =
-            sample_from_q(a.rays.q + (size_t)i * kDqnActions, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+            sample_from_q(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                           make3(B4.x, B4.y, B4.z), pos, a.rays.pix[rid], (uint32_t)sample,
                           1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
@@ -436,7 +443,7 @@ __global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, fl
     const float4 T4 = s.shade[t * kShadeF4 + 1];
     const float4 B4 = s.shade[t * kShadeF4 + 2];
     f3 tpv = ld3(tp, i);
-    const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, make3(N4.x, N4.y, N4.z),
+    const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, 1, make3(N4.x, N4.y, N4.z),
                                        make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), ld3(loc, i),
                                        pix[i], (uint32_t)sample, 1u + (uint32_t)bounce, k0, k1, &tpv, true);
     st3(tp, i, tpv);
@@ -447,11 +454,12 @@ __global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, fl
 }  // namespace
 
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
-                          int max_rows, float* q, hipStream_t stream) {
+                          int max_rows, float* q, int ldq, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
     const int blocks = (max_rows + kTileM - 1) / kTileM;
+    if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(256), 0, stream, net, loc, list, count,
-                       max_rows, q);
+                       max_rows, q, ldq);
     return hipGetLastError();
 }
 
@@ -470,7 +478,7 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream)
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream) {
     const int cur = (bounce - 1) & 1;
     hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
-                                  a.rays.q, stream);
+                                  a.rays.q, a.rays.ldq, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dqn_bounce, dim3(ray_blocks(a)), dim3(256), 0, stream, a, sample, bounce);
     return hipGetLastError();

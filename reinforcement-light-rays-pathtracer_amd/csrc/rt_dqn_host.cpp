@@ -213,7 +213,7 @@ int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc, int n, floa
     hipError_t e = hipMalloc(&d_loc, sizeof(float) * 3 * (size_t)n);
     if (e == hipSuccess) e = hipMalloc(&d_q, sizeof(float) * rt::kDqnActions * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_loc, loc, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, 0);
+    if (e == hipSuccess) e = rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, 0, 0);
     if (e == hipSuccess) e = hipMemcpy(q, d_q, sizeof(float) * rt::kDqnActions * (size_t)n, hipMemcpyDeviceToHost);
     (void)hipFree(d_loc);
     (void)hipFree(d_q);
@@ -226,7 +226,7 @@ int rt_dqn_forward_device(rt_ctx* ctx, const rt_dqn* dqn, const float* d_loc, in
     if (!ctx || !dqn || (n > 0 && (!d_loc || !d_q))) return err(RT_E_INVALID, "NULL argument");
     if (n < 0) return err(RT_E_INVALID, "n < 0");
     RT_HIPE(hipSetDevice(rt::ctx_device(ctx)));
-    RT_HIPE(rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, (hipStream_t)stream));
+    RT_HIPE(rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, 0, (hipStream_t)stream));
     return RT_OK;
 }
 
@@ -301,13 +301,14 @@ struct Workspace {
                   alloc(sizeof(uint32_t) * n, (void**)&r.pix) && alloc(sizeof(int32_t) * n, (void**)&r.list[0]) &&
                   alloc(sizeof(int32_t) * n, (void**)&r.list[1]) && alloc(sizeof(int32_t) * 4, (void**)&r.count) &&
                   alloc(sizeof(unsigned long long), (void**)&r.casts) &&
-                  alloc(sizeof(float) * rt::kDqnActions * (size_t)n, (void**)&r.q);
+                  alloc(sizeof(float) * rt::kDqnActions * (size_t)((n + 63) / 64 * 64), (void**)&r.q);
         if (!ok) {
             release();
             return err(RT_E_NOMEM, "DQN workspace allocation failed");
         }
         cap = n;
         r.n = n;
+        r.ldq = (n + 63) / 64 * 64;
         return RT_OK;
     }
 };

@@ -117,8 +117,9 @@ struct DqnRays {
     int32_t* list[2] = {nullptr, nullptr};  // active ray lists (ping-pong)
     int32_t* count = nullptr;  // [2 + 1] list sizes, [2] = ray casts of this call (low 32 bits unused)
     unsigned long long* casts = nullptr;
-    float* q = nullptr;     // [n][144] Q values of the active list (list order)
+    float* q = nullptr;     // [144][ldq] Q values of the active list, action-major (list order)
     int n = 0;
+    int ldq = 0;            // leading dimension of q: n rounded up to the MLP tile (64)
 };
 
 struct DqnLaunch {
@@ -138,8 +139,10 @@ struct DqnLaunch {
     int use_filter;  // as RenderLaunch::use_filter
 };
 
+// q layout: ldq == 0 -> [row][144] (the C ABI's); ldq > 0 -> action-major q[a * ldq + row],
+// ldq a multiple of 64 covering every launched row (the renderer's, coalesced per action)
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
-                          const int32_t* count, int max_rows, float* q, hipStream_t stream);
+                          const int32_t* count, int max_rows, float* q, int ldq, hipStream_t stream);
 hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream);
 hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream);
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream);
