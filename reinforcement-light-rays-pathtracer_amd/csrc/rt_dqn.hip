@@ -319,8 +319,8 @@ __device__ __forceinline__ bool ray_pixel(const DqnLaunch& a, int rid, int* px, 
 }
 
 __global__ __launch_bounds__(256) void k_dqn_frame_begin(const DqnLaunch a) {
-    const int rid = blockIdx.x * 256 + threadIdx.x;
-    if (rid >= a.rays.n) return;
+    const int rid = blockIdx.x * 256 + threadIdx.x;  // pixel slot
+    if (rid >= a.rays.n_pix) return;
     int px, py;
     const bool valid = ray_pixel(a, rid, &px, &py);
     a.rays.pix[rid] = valid ? (uint32_t)py * (uint32_t)a.width + (uint32_t)px : 0u;
@@ -328,17 +328,19 @@ __global__ __launch_bounds__(256) void k_dqn_frame_begin(const DqnLaunch a) {
 }
 
 // initialise_ray + the first trace_ray (bounce 0: no Q evaluation)
-__global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a, int sample) {
+__global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a) {
     const int rid = blockIdx.x * 256 + threadIdx.x;
     bool keep = false;
     unsigned casts = 0;
     if (rid < a.rays.n) {
+        const int slot = rid / a.rays.n_pix, pi = rid - slot * a.rays.n_pix;
+        const int sample = a.rays.s0 + slot;
         int px, py;
-        const bool valid = ray_pixel(a, rid, &px, &py);
+        const bool valid = ray_pixel(a, pi, &px, &py);
         f3 tp = make3(valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f);
         if (valid) {
             float r1, r2;
-            draw2(a.rays.pix[rid], (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+            draw2(a.rays.pix[pi], (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
             const float x = (float)px + r1, y = (float)py + r2;
             f3 dir = normalize(make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height));
             const float w = 1.0f;
@@ -368,7 +370,7 @@ __global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a, int sampl
 }
 
 // one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
-__global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sample, int bounce) {
+__global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int bounce) {
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int n_act = a.rays.count[cur];
@@ -378,6 +380,9 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sampl
     int rid = 0;
     if (i < n_act) {
         rid = a.rays.list[cur][i];
+        const int slot = rid / a.rays.n_pix;
+        const int sample = a.rays.s0 + slot;
+        const uint32_t pixid = a.rays.pix[rid - slot * a.rays.n_pix];
         const int tri = a.rays.tri[rid];
         const f3 pos = ld3(a.rays.loc, rid);
         f3 tp = ld3(a.rays.tp, rid);
@@ -386,7 +391,7 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sampl
         const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
         const SampleOut so =
             sample_from_q(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
-                          make3(B4.x, B4.y, B4.z), pos, a.rays.pix[rid], (uint32_t)sample,
+                          make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                           1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
         f3 loc = pos;
@@ -410,16 +415,20 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int sampl
 
 // update_total_throughput (nn_rendering_helpers.cu:143-156)
 __global__ __launch_bounds__(256) void k_dqn_accumulate(const DqnLaunch a) {
-    const int rid = blockIdx.x * 256 + threadIdx.x;
-    if (rid >= a.rays.n) return;
-    const f3 t = ld3(a.rays.total, rid), p = ld3(a.rays.tp, rid);
-    st3(a.rays.total, rid, make3(t.x + p.x, t.y + p.y, t.z + p.z));
+    const int pi = blockIdx.x * 256 + threadIdx.x;
+    if (pi >= a.rays.n_pix) return;
+    f3 t = ld3(a.rays.total, pi);
+    for (int rid = pi; rid < a.rays.n; rid += a.rays.n_pix) {  // slots in sample order
+        const f3 p = ld3(a.rays.tp, rid);
+        t = make3(t.x + p.x, t.y + p.y, t.z + p.z);
+    }
+    st3(a.rays.total, pi, t);
 }
 
 // update_device_buffer (nn_rendering_helpers.cu:159-172): total / SPP into the tile output
 __global__ __launch_bounds__(256) void k_dqn_finish(const DqnLaunch a) {
-    const int rid = blockIdx.x * 256 + threadIdx.x;
-    if (rid >= a.rays.n) return;
+    const int rid = blockIdx.x * 256 + threadIdx.x;  // pixel slot
+    if (rid >= a.rays.n_pix) return;
     int px, py;
     if (!ray_pixel(a, rid, &px, &py)) return;
     const BlockDesc blk = a.blocks[rid >> 8];
@@ -464,33 +473,34 @@ hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* li
 }
 
 static unsigned ray_blocks(const DqnLaunch& a) { return (unsigned)((a.rays.n + 255) / 256); }
+static unsigned pix_blocks(const DqnLaunch& a) { return (unsigned)((a.rays.n_pix + 255) / 256); }
 
 hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_dqn_frame_begin, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_dqn_frame_begin, dim3(pix_blocks(a)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream) {
-    hipLaunchKernelGGL(k_dqn_camera, dim3(ray_blocks(a)), dim3(256), 0, stream, a, sample);
+hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
+    hipLaunchKernelGGL(k_dqn_camera, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
-hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream) {
+hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream) {
     const int cur = (bounce - 1) & 1;
     hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
                                   a.rays.q, a.rays.ldq, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dqn_bounce, dim3(ray_blocks(a)), dim3(256), 0, stream, a, sample, bounce);
+    hipLaunchKernelGGL(k_dqn_bounce, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce);
     return hipGetLastError();
 }
 
 hipError_t launch_dqn_accumulate(const DqnLaunch& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_dqn_accumulate, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_dqn_accumulate, dim3(pix_blocks(a)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 hipError_t launch_dqn_finish(const DqnLaunch& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_dqn_finish, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(k_dqn_finish, dim3(pix_blocks(a)), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 

@@ -7,7 +7,10 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <string>
 #include <vector>
@@ -315,11 +318,18 @@ struct Workspace {
 
 Workspace* g_ws_for(rt_ctx* ctx);
 
+constexpr int kRaysInFlight = 1 << 22;  // DQN wavefront size (q: 2.4 GB at 4 M rays)
+
 int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_camera* cam, const rt_params* p,
             const rt::BlockDesc* d_blocks, int n_blocks, int clip_x1, int clip_y1, int out_pitch, float* d_out,
             uint64_t* d_casts, hipStream_t stream) {
     Workspace* ws = g_ws_for(ctx);
-    int rc = ws->ensure(n_blocks * 256);
+    // samples in flight: about kRaysInFlight rays per pass (all of spp for small frames)
+    const int n_pix = n_blocks * 256;
+    int rays_in_flight = kRaysInFlight;
+    if (const char* env = getenv("RTMI_DQN_RAYS_IN_FLIGHT")) rays_in_flight = std::max(1, atoi(env));  // tests
+    const int in_flight = std::max(1, std::min(p->spp, rays_in_flight / n_pix));
+    int rc = ws->ensure(n_pix * in_flight);
     if (rc != RT_OK) return rc;
     rt::DqnLaunch a;
     memset(&a, 0, sizeof(a));
@@ -352,13 +362,17 @@ int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_came
     a.use_filter = rt::filter_usable(a.scene, a.cam_x, a.cam_y, a.cam_z, a.t_scale);
     int32_t* h_count = nullptr;
     RT_HIPE(hipHostMalloc((void**)&h_count, sizeof(int32_t), hipHostMallocDefault));
+    a.rays.n_pix = n_pix;
+    a.rays.n = n_pix;
     hipError_t e = rt::launch_dqn_frame_begin(a, stream);
-    for (int s = 0; e == hipSuccess && s < p->spp; ++s) {
+    for (int s = 0; e == hipSuccess && s < p->spp; s += in_flight) {
+        a.rays.s0 = s;
+        a.rays.n = n_pix * std::min(in_flight, p->spp - s);
         e = hipMemsetAsync(a.rays.count, 0, sizeof(int32_t) * 2, stream);
-        if (e == hipSuccess) e = rt::launch_dqn_camera(a, s, stream);
+        if (e == hipSuccess) e = rt::launch_dqn_camera(a, stream);
         for (int b = 1; e == hipSuccess && b < p->max_bounces; ++b) {
             e = hipMemsetAsync(a.rays.count + (b & 1), 0, sizeof(int32_t), stream);
-            if (e == hipSuccess) e = rt::launch_dqn_bounce(a, s, b, stream);
+            if (e == hipSuccess) e = rt::launch_dqn_bounce(a, b, stream);
             if (e == hipSuccess && (b % 4 == 0 || b == 1)) {  // stop once every path has ended
                 e = hipMemcpyAsync(h_count, a.rays.count + (b & 1), sizeof(int32_t), hipMemcpyDeviceToHost, stream);
                 if (e == hipSuccess) e = hipStreamSynchronize(stream);

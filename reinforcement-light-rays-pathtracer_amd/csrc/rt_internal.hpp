@@ -107,19 +107,24 @@ struct DqnNet {
 };
 
 // Ray state of the DQN wavefront renderer (SoA over the rays of a frame part).
+// Several samples are in flight at once: ray id = slot * n_pix + pixel index, slot k
+// tracing sample s0 + k, so late bounces (few surviving paths per sample) still fill
+// the GPU; the per-pixel totals add the slots in sample order (the sequential order).
 struct DqnRays {
     float* loc = nullptr;   // [n][3] current position (GPU: ray_locations_device)
     float* dir = nullptr;   // [n][3]
     float* tp = nullptr;    // [n][3] throughput
-    float* total = nullptr; // [n][3] sum over samples
+    float* total = nullptr; // [n_pix][3] sum over samples
     int32_t* tri = nullptr; // [n] triangle of the last surface hit (normal / frame)
-    uint32_t* pix = nullptr;   // [n] global pixel id (RNG key)
+    uint32_t* pix = nullptr;   // [n_pix] global pixel id (RNG key)
     int32_t* list[2] = {nullptr, nullptr};  // active ray lists (ping-pong)
     int32_t* count = nullptr;  // [2 + 1] list sizes, [2] = ray casts of this call (low 32 bits unused)
     unsigned long long* casts = nullptr;
     float* q = nullptr;     // [144][ldq] Q values of the active list, action-major (list order)
-    int n = 0;
-    int ldq = 0;            // leading dimension of q: n rounded up to the MLP tile (64)
+    int n = 0;              // rays of the current pass: n_pix * samples in flight
+    int n_pix = 0;          // pixel slots (16x16 blocks x 256)
+    int s0 = 0;             // sample of slot 0
+    int ldq = 0;            // leading dimension of q: ray capacity rounded up to the MLP tile (64)
 };
 
 struct DqnLaunch {
@@ -144,8 +149,8 @@ struct DqnLaunch {
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
                           const int32_t* count, int max_rows, float* q, int ldq, hipStream_t stream);
 hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream);
-hipError_t launch_dqn_camera(const DqnLaunch& a, int sample, hipStream_t stream);
-hipError_t launch_dqn_bounce(const DqnLaunch& a, int sample, int bounce, hipStream_t stream);
+hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream);  // samples s0 .. s0 + n/n_pix - 1
+hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream);
 hipError_t launch_dqn_accumulate(const DqnLaunch& a, hipStream_t stream);
 hipError_t launch_dqn_finish(const DqnLaunch& a, hipStream_t stream);
 // sampler alone (parity): rows i < n, Q [n][144] (overwritten with Q*cos), pixel/tri/loc per row

@@ -162,3 +162,22 @@ def test_dqn_tiles_equal_rect(rtmi_mod, gpu_ctx):
         torch.cuda.synchronize()
     img = rtmi_mod.tiles.assemble(out.cpu().numpy()[None], 64, 64, 32, 1)
     assert np.array_equal(img, full)
+
+
+@pytest.mark.gpu
+def test_dqn_samples_in_flight_bit_identical(rtmi_mod, gpu_ctx, monkeypatch):
+    """Samples traced concurrently (ray = slot * pixels + pixel) give the image of one
+    sample at a time: each path depends only on (pixel, sample), and the per-pixel
+    totals add the slots in sample order."""
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=32, spp=6, max_bounces=16)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    res = []
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        for rays in (1, 2 * 1536, 1 << 22):   # 1, 2 (4 + 2) and all 6 samples in flight
+            monkeypatch.setenv("RTMI_DQN_RAYS_IN_FLIGHT", str(rays))
+            res.append(rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p))
+    for img, casts in res[1:]:
+        assert casts == res[0][1]
+        assert np.array_equal(img.view(np.uint32), res[0][0].view(np.uint32))
