@@ -246,7 +246,7 @@ def main():
         }
         if not args.no_parity:
             line["parity"] = parity_window(geom, params, cam_pos, image)
-        if args.cpu_seconds > 0:
+        if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
         print(json.dumps(line), flush=True)
 

@@ -37,9 +37,44 @@ RT_HD float dot(f3 a, f3 b) {
     return (tx + ty) + tz;
 }
 
+#if defined(__HIPCC__)
+// Correctly rounded 1/x.  For |x| in [2^-125, 2^125], v_rcp_f32 (<= 1 ulp)
+// refined by one Newton step in FMA; the result equals IEEE 1.0f/x bit for bit
+// (verified over every float by rt_selftest(RT_SELFTEST_RCP), a GPU test).  Other
+// inputs take hipcc's IEEE division sequence.
+__device__ __forceinline__ float rcp_rn_from(float x, float r0) {
+    const float ax = fabsf(x);
+    const float e = fmaf(-x, r0, 1.0f);
+    float r = fmaf(e, r0, r0);
+    const bool out_of_range = !(ax >= 0x1p-125f && ax <= 0x1p125f);
+    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {  // wave-uniform, rare
+        const float q = 1.0f / x;
+        r = out_of_range ? q : r;
+    }
+    return r;
+}
+__device__ __forceinline__ float rcp_rn(float x) { return rcp_rn_from(x, __builtin_amdgcn_rcpf(x)); }
+
+// x / 12 for x = +0 or |x| in [2^-100, 2^100]: q = RN(x c), c = RN(1/12), corrected
+// by one FMA residual step; equal to IEEE x / 12.0f over that whole range (checked
+// exhaustively over every float on the host, tools/check_div12.c; -0 gives +0).
+// The grid coordinates gx = cell + jitter are +0 or in [2^-24, 12].
+__device__ __forceinline__ float div12(float x) {
+    const float c = 1.0f / 12.0f;
+    const float q = x * c;
+    const float r = fmaf(-q, 12.0f, x);
+    return fmaf(r, c, q);
+}
+#endif
+
 // glm normalize: v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
+// (device: the reciprocal by rcp_rn, bit-identical to the division)
 RT_HD f3 normalize(f3 v) {
-    float inv = 1.0f / sqrtf(dot(v, v));
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float inv = rcp_rn(sqrtf(dot(v, v)));
+#else
+    const float inv = 1.0f / sqrtf(dot(v, v));
+#endif
     return make3(v.x * inv, v.y * inv, v.z * inv);
 }
 
@@ -163,7 +198,11 @@ RT_HD void chiu_map(float x, float y, float* xr, float* yr, float* zr) {
 // world = mat4(T, N, B, pos) * (xh, yh, zh, 1) in glm order, direction = normalize(world - pos)
 RT_HD f3 grid_direction(float gx, float gy, f3 N, f3 T, f3 B, f3 pos) {
     float xh, yh, zh;
+#if defined(__HIP_DEVICE_COMPILE__)
+    chiu_map(div12(gx), div12(gy), &xh, &yh, &zh);  // gx, gy in [0, 12]
+#else
     chiu_map(gx / (float)kGridRes, gy / (float)kGridRes, &xh, &yh, &zh);
+#endif
     const f3 w = make3((T.x * xh + N.x * yh) + (B.x * zh + pos.x * 1.0f),
                        (T.y * xh + N.y * yh) + (B.y * zh + pos.y * 1.0f),
                        (T.z * xh + N.z * yh) + (B.z * zh + pos.z * 1.0f));

@@ -52,12 +52,8 @@ struct Hit {
 #define RT_UNROLL 1
 #endif
 //   RT_FAST_RCP 1: 1/detA by rcp_rn (v_rcp_f32 + Newton, exhaustively verified)
-//   RT_RCP_STEPS Newton steps of rcp_rn
 #ifndef RT_FAST_RCP
 #define RT_FAST_RCP 1
-#endif
-#ifndef RT_RCP_STEPS
-#define RT_RCP_STEPS 1
 #endif
 #if RT_FAST_RCP
 #define RT_RCP(x) rcp_rn(x)
@@ -65,39 +61,7 @@ struct Hit {
 #define RT_RCP(x) (1.0f / (x))
 #endif
 
-// Correctly rounded 1/x.  For |x| in [2^-125, 2^125], v_rcp_f32 (<= 1 ulp)
-// refined by Newton steps in FMA; the result equals IEEE 1.0f/x bit for bit
-// (verified over every such float by rt_selftest(RT_SELFTEST_RCP), a
-// GPU test).  Other inputs take hipcc's IEEE division sequence.
-__device__ __forceinline__ float rcp_rn(float x) {
-    const float ax = fabsf(x);
-    float r = __builtin_amdgcn_rcpf(x);
-    float e = fmaf(-x, r, 1.0f);
-    r = fmaf(e, r, r);
-#if RT_RCP_STEPS > 1
-    e = fmaf(-x, r, 1.0f);
-    r = fmaf(e, r, r);
-#endif
-    const bool out_of_range = !(ax >= 0x1p-125f && ax <= 0x1p125f);
-    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {  // wave-uniform, rare
-        const float q = 1.0f / x;
-        r = out_of_range ? q : r;
-    }
-    return r;
-}
-
-// rcp_rn's refinement of an already computed v_rcp_f32 value r0 = rcp(x)
-__device__ __forceinline__ float rcp_rn_from(float x, float r0) {
-    const float ax = fabsf(x);
-    const float e = fmaf(-x, r0, 1.0f);
-    float r = fmaf(e, r0, r0);
-    const bool out_of_range = !(ax >= 0x1p-125f && ax <= 0x1p125f);
-    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {
-        const float q = 1.0f / x;
-        r = out_of_range ? q : r;
-    }
-    return r;
-}
+// rcp_rn / rcp_rn_from: rt_math.hpp
 
 // Exact hit test of one triangle (the reference's arithmetic, see above).
 template <int RULE>
