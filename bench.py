@@ -130,35 +130,18 @@ def main():
 
     tiles = rtmi.tiles.rank_tiles(params.width, params.height, TILE, rank, world)
     k = tiles.shape[0]
-    # two frame buffers: frame i+1 renders while frame i is all-gathered over RCCL
-    outs = [torch.zeros((k, TILE, TILE, 3), dtype=torch.float32, device=dev) for _ in range(2)]
-    gathered = [torch.empty((world, k, TILE, TILE, 3), dtype=torch.float32, device=dev)
-                for _ in range(2)]
     casts = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
-    pending = [None, None]
 
-    def render(b):
-        if pending[b] is not None:  # the gather still reading this buffer
-            pending[b].wait()
-            pending[b] = None
-        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, outs[b].data_ptr(),
-                                 casts.data_ptr(), stream.cuda_stream)
+    def render(out):
+        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(), casts.data_ptr(),
+                                 stream.cuda_stream)
 
-    def gather(b):
-        if world > 1:
-            pending[b] = rtmi.dist.gather_tiles(outs[b], gathered[b], async_op=True)
-
-    def drain():
-        for b in range(2):
-            if pending[b] is not None:
-                pending[b].wait()
-                pending[b] = None
-
+    # two frame buffers: frame i+1 renders while frame i is all-gathered over RCCL
+    pipe = rtmi.dist.FramePipeline(render, (k, TILE, TILE, 3), world, dev)
     for i in range(args.warmup):
-        render(i % 2)
-        gather(i % 2)
-    drain()
+        pipe.gather_frame(pipe.render_frame(i))
+    pipe.drain()
     torch.cuda.synchronize()
     casts.zero_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -168,20 +151,16 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        b = i % 2
-        if pending[b] is not None:
-            pending[b].wait()
-            pending[b] = None
+        pipe.wait(i % 2)  # outside the kernel's event window
         ev[i][0].record(stream)
-        render(b)
+        b = pipe.render_frame(i)
         ev[i][1].record(stream)
-        gather(b)
-    drain()
+        pipe.gather_frame(b)
+    pipe.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    last = (args.steps - 1) % 2
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_casts = int(casts.item())
@@ -196,7 +175,7 @@ def main():
     else:
         total_casts = rank_casts
 
-    frame = outs[last][None] if world == 1 else gathered[last]
+    frame = pipe.frame(args.steps - 1)
     image = None
     if rank == 0:
         image = rtmi.tiles.assemble(frame.cpu().numpy(), params.width, params.height, TILE, world)

@@ -28,6 +28,46 @@ def gather_tiles(out: torch.Tensor, gathered: torch.Tensor, async_op: bool = Fal
     return work if async_op else gathered
 
 
+class FramePipeline:
+    """Two frame buffers per rank: frame i renders into buffer i % 2 while frame i-1
+    is all-gathered from the other one (bench.py).  `render(out)` queues one frame's
+    render into `out` ([k, T, T, 3]) on the current stream; a buffer is rendered into
+    again only after its previous gather completed (work.wait() orders the current
+    stream after the collective -- a host wait on gloo)."""
+
+    def __init__(self, render, shape, world: int, device):
+        self.render = render
+        self.world = world
+        self.outs = [torch.zeros(shape, dtype=torch.float32, device=device) for _ in range(2)]
+        self.gathered = [torch.empty((world,) + tuple(shape), dtype=torch.float32, device=device)
+                         for _ in range(2)]
+        self.pending = [None, None]
+
+    def wait(self, b: int) -> None:
+        if self.pending[b] is not None:
+            self.pending[b].wait()
+            self.pending[b] = None
+
+    def render_frame(self, i: int) -> int:
+        b = i % 2
+        self.wait(b)
+        self.render(self.outs[b])
+        return b
+
+    def gather_frame(self, b: int) -> None:
+        if self.world > 1:
+            self.pending[b] = gather_tiles(self.outs[b], self.gathered[b], async_op=True)
+
+    def drain(self) -> None:
+        for b in range(2):
+            self.wait(b)
+
+    def frame(self, i: int) -> torch.Tensor:
+        """[world, k, T, T, 3] tiles of frame i (after drain(), for the last two frames)."""
+        b = i % 2
+        return self.outs[b][None] if self.world == 1 else self.gathered[b]
+
+
 def sum_td(td_sum: torch.Tensor, td_count: torch.Tensor) -> None:
     """Expected-SARSA frame exchange: sum every rank's TD accumulators in place
     (int64 fixed-point target sums and int32 visit counts, [n_volumes*144]).
