@@ -75,6 +75,22 @@ def pmc_traffic(params):
     return None, None
 
 
+SQ_PROFILE = os.path.join("profiles", "r1v5_sq_summary.json")
+
+
+def pmc_valu_issue(params):
+    """Fraction of the VALU issue slots k_render used on this workload (SQ_INSTS_VALU of
+    the committed PMC pass over 1024 SIMDs x one wave-instruction per 2 cycles)."""
+    if (params.width, params.height, params.spp, params.spp_split) != DEFAULT_WORKLOAD:
+        return None
+    try:
+        c = json.load(open(os.path.join(ROOT, SQ_PROFILE)))["per_dispatch"]
+        cycles = c["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
+        return round(c["SQ_INSTS_VALU"] / (1024 * cycles / 2.0), 3)
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(geom, params, cam_pos, seconds):
     """Time the CPU restatement (oracle/, OpenMP) on a bounded strip of the same frame."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -221,6 +237,8 @@ def main():
                 "bytes_per_cast": b_cast,
                 "valu_tflops_est": round(valu_tflops, 2),
                 "valu_frac_est": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
+                "valu_issue_frac_pmc": pmc_valu_issue(params),
+                "valu_issue_source": SQ_PROFILE,
             },
         }
         if not args.no_parity:
