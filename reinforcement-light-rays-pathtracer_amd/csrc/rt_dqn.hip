@@ -44,6 +44,8 @@ constexpr int kTileM = RT_MLP_MT * 16;  // rays per MLP workgroup
 // DESIGN.md §4).
 constexpr int kStrideA = 320 + 8; // LDS row strides in bf16 elements (+16 B pad)
 constexpr int kStrideB = 224 + 8;
+constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
+static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
 
 __device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
@@ -159,22 +161,16 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
             const float bj = bias[col];
 #pragma unroll
             for (int m = 0; m < MT; ++m) {
-                float v4[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const int row = m * 16 + (lane >> 4) * 4 + r;
                     float v = acc[m][j][r] + bj;
                     v = v > 0.0f ? v : 0.0f;
-                    v4[r] = v;
-                    if (LAST) {
-                        if (ldq == 0 && row < rows_valid) q[(size_t)(row0 + row) * kDqnActions + col] = v;
-                    } else {
+                    if (LAST)  // fp32 Q tile staged in LDS, written out coalesced by the caller
+                        reinterpret_cast<float*>(out_lds)[row * kStageStride + col] = v;
+                    else
                         out_lds[row * out_stride + col] = (__bf16)v;
-                    }
                 }
-                if (LAST && ldq > 0)  // 4 consecutive rows of one action: one 16-B store
-                    *reinterpret_cast<float4*>(q + (size_t)col * ldq + row0 + m * 16 + (lane >> 4) * 4) =
-                        make_float4(v4[0], v4[1], v4[2], v4[3]);
             }
         }
     }
@@ -214,7 +210,27 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
     __syncthreads();
     mlp_layer<false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB, q, row0, ldq, rows_valid);
     __syncthreads();
-    mlp_layer<true, MT>(net, 3, bufB, kStrideB, nullptr, 0, q, row0, ldq, rows_valid);
+    mlp_layer<true, MT>(net, 3, bufB, kStrideB, bufA, 0, q, row0, ldq, rows_valid);
+    __syncthreads();
+    // Q tile [kRows][144] from LDS (odd row stride: conflict-free column reads) in
+    // 16-B stores: row-major rows are one contiguous run, action-major columns runs
+    // of kRows rows (ldq covers every launched row, so padding rows may be written).
+    const float* stage = reinterpret_cast<const float*>(bufA);
+    if (ldq == 0) {
+        float* dst = q + (size_t)row0 * kDqnActions;
+        for (int t = threadIdx.x; t < rows_valid * (kDqnActions / 4); t += 256) {
+            const int r = t / (kDqnActions / 4), c = (t - r * (kDqnActions / 4)) * 4;
+            const float* sp = stage + r * kStageStride + c;
+            *reinterpret_cast<float4*>(dst + (size_t)r * kDqnActions + c) = make_float4(sp[0], sp[1], sp[2], sp[3]);
+        }
+    } else {
+        for (int t = threadIdx.x; t < kDqnActions * (kRows / 4); t += 256) {
+            const int c = t / (kRows / 4), r = (t - c * (kRows / 4)) * 4;
+            const float* sp = stage + r * kStageStride + c;
+            *reinterpret_cast<float4*>(q + (size_t)c * ldq + row0 + r) =
+                make_float4(sp[0], sp[kStageStride], sp[2 * kStageStride], sp[3 * kStageStride]);
+        }
+    }
 }
 
 struct SampleOut {
