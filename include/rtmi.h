@@ -212,6 +212,18 @@ int rt_sarsa_info(const rt_sarsa* sarsa, int32_t* n_volumes, int32_t* n_nodes, u
 #define RT_SARSA_SEARCH_KD 0
 #define RT_SARSA_SEARCH_GRID 1
 int rt_sarsa_set_search(rt_sarsa* sarsa, int mode);
+/* On-disk formats of the reference's Q-tables.
+ * rt_sarsa_save_q: RadianceMap::save_q_vals_to_file (GPU/radiance_volumes/radiance_map.cu:236-266):
+ *   "144\n", then one line per volume in map order: "x y z Q0 .. Q143" (ostream defaults,
+ *   6 significant digits).
+ * rt_sarsa_save_selected: RadianceMap::save_selected_radiance_volumes_vals (radiance_map.cu:270-301):
+ *   for each "x y z nx ny nz" line of to_select_path (RMD/selected_radiance_volumes/to_select.txt),
+ *   the nearest volume (rt_sarsa_nearest) as "px py pz nx ny nz d0 .. d143" with its sector
+ *   distribution (the CDF differenced: convert_radiance_distribution, radiance_volume.cu:332-336);
+ *   out_path is replaced.  Both return RT_E_IO on file errors. */
+int rt_sarsa_save_q(const rt_sarsa* sarsa, const char* path);
+int rt_sarsa_save_selected(rt_ctx* ctx, const rt_sarsa* sarsa, const char* to_select_path,
+                           const char* out_path);
 int rt_sarsa_search_stats(const rt_sarsa* sarsa, int32_t* mode, int32_t* n_classes, int64_t* grid_cells,
                           uint64_t* kd_fallbacks);
 /* host copies: pos n x 3, normal n x 3, surface index n, KD array n_nodes x 12 words

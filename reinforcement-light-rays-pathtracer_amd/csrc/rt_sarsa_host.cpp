@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <array>
+#include <fstream>
 #include <map>
 #include <string>
 #include <vector>
@@ -671,6 +672,79 @@ int rt_sarsa_nearest(rt_ctx* ctx, const rt_sarsa* sa, const float* pos, const fl
     (void)hipFree(d_n);
     (void)hipFree(d_o);
     if (e != hipSuccess) return err(RT_E_HIP, std::string("rt_sarsa_nearest: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_sarsa_save_q(const rt_sarsa* sa, const char* path) {
+    if (!sa || !path) return err(RT_E_INVALID, "NULL argument");
+    const int S = rt::kSarsaSectors;
+    std::vector<float> q((size_t)sa->n_vol * S);
+    int rc = rt_sarsa_read(sa, q.data(), nullptr, nullptr, nullptr);
+    if (rc != RT_OK) return rc;
+    // RadianceMap::save_q_vals_to_file: ostream defaults (6 significant digits)
+    std::ofstream f(path);
+    if (!f.is_open()) return err(RT_E_IO, std::string("cannot write ") + path);
+    f << S << "\n";
+    for (int i = 0; i < sa->n_vol; ++i) {
+        f << sa->pos[4 * i] << " " << sa->pos[4 * i + 1] << " " << sa->pos[4 * i + 2];
+        for (int k = 0; k < S; ++k) f << " " << q[(size_t)i * S + k];
+        f << "\n";
+    }
+    f.close();
+    if (f.fail()) return err(RT_E_IO, std::string("write failed: ") + path);
+    return RT_OK;
+}
+
+int rt_sarsa_save_selected(rt_ctx* ctx, const rt_sarsa* sa, const char* to_select_path, const char* out_path) {
+    if (!ctx || !sa || !to_select_path || !out_path) return err(RT_E_INVALID, "NULL argument");
+    // read_hemisphere_locations_and_normals (hemisphere_helpers.cu:230-278): tokens
+    // split on ' ', std::stof, the first three the location, the rest the normal
+    std::ifstream in(to_select_path);
+    if (!in.is_open()) return err(RT_E_IO, std::string("cannot read ") + to_select_path);
+    std::vector<float> qp, qn;
+    std::string line;
+    try {
+        while (std::getline(in, line)) {
+            float loc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
+            size_t pos;
+            int idx = 0;
+            while ((pos = line.find(' ')) != std::string::npos) {
+                const float v = std::stof(line.substr(0, pos));
+                if (idx < 3) loc[idx] = v;
+                else nrm[idx % 3] = v;
+                ++idx;
+                line.erase(0, pos + 1);
+            }
+            nrm[idx % 3] = std::stof(line);
+            qp.insert(qp.end(), loc, loc + 3);
+            qn.insert(qn.end(), nrm, nrm + 3);
+        }
+    } catch (const std::exception&) {
+        return err(RT_E_IO, std::string("malformed location line in ") + to_select_path);
+    }
+    const int n = (int)qp.size() / 3;
+    std::vector<int32_t> idx(n);
+    int rc = rt_sarsa_nearest(ctx, sa, qp.data(), qn.data(), n, idx.data());
+    if (rc != RT_OK) return rc;
+    const int S = rt::kSarsaSectors;
+    std::vector<float> cdf((size_t)sa->n_vol * S);
+    rc = rt_sarsa_read(sa, nullptr, cdf.data(), nullptr, nullptr);
+    if (rc != RT_OK) return rc;
+    // the file is replaced, then each volume appended (write_volume_to_file,
+    // radiance_volume.cu:338-365) with its distribution: convert_radiance_distribution
+    // (:332-336) differences the CDF, sector 0 keeps cdf[0]
+    std::ofstream f(out_path);
+    if (!f.is_open()) return err(RT_E_IO, std::string("cannot write ") + out_path);
+    for (int i = 0; i < n; ++i) {
+        const int v = idx[i];
+        const float* c = &cdf[(size_t)v * S];
+        f << sa->pos[4 * v] << " " << sa->pos[4 * v + 1] << " " << sa->pos[4 * v + 2];
+        f << " " << sa->nrm[3 * v] << " " << sa->nrm[3 * v + 1] << " " << sa->nrm[3 * v + 2];
+        for (int k = 0; k < S; ++k) f << " " << (k == 0 ? c[0] : c[k] - c[k - 1]);
+        f << "\n";
+    }
+    f.close();
+    if (f.fail()) return err(RT_E_IO, std::string("write failed: ") + out_path);
     return RT_OK;
 }
 

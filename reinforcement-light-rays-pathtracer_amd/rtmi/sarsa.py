@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -57,6 +58,14 @@ class RadianceMap:
                                           ctypes.byref(fb)))
         return {"mode": int(mode.value), "classes": int(ncls.value), "grid_cells": int(cells.value),
                 "kd_fallbacks": int(fb.value)}
+
+    def save_q(self, path: str) -> None:
+        """radiance_map_data.txt format (RadianceMap::save_q_vals_to_file)."""
+        check(lib().rt_sarsa_save_q(self._h, os.fsencode(path)))
+
+    def save_selected(self, to_select: str, out: str) -> None:
+        """selected_sarsa.txt format for the locations of to_select.txt."""
+        check(lib().rt_sarsa_save_selected(self.ctx.handle, self._h, os.fsencode(to_select), os.fsencode(out)))
 
     def volumes(self):
         n = self.n_volumes
@@ -119,3 +128,20 @@ class RadianceMap:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def read_q_file(path: str):
+    """radiance_map_data.txt -> (positions [n, 3], Q [n, 144])."""
+    with open(path) as fh:
+        actions = int(fh.readline())
+        rows = [np.array(l.split(), np.float64) for l in fh if l.strip()]
+    a = np.array(rows).reshape(len(rows), 3 + actions)
+    return a[:, :3].astype(np.float32), a[:, 3:].astype(np.float32)
+
+
+def read_selected_file(path: str):
+    """selected_sarsa.txt / selected_deep.txt -> (positions, normals, distributions [n, 144])."""
+    with open(path) as fh:
+        rows = [np.array(l.split(), np.float64) for l in fh if l.strip()]
+    a = np.array(rows).reshape(len(rows), -1)
+    return a[:, :3].astype(np.float32), a[:, 3:6].astype(np.float32), a[:, 6:].astype(np.float32)

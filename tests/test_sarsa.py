@@ -161,6 +161,18 @@ def test_oracle_threads_and_split_do_not_change_learning(rtmi_mod, oracle_mod):
     assert np.array_equal(res[1][0], res[0][0])
 
 
+def test_selected_volume_format_reads_reference_fixture(rtmi_mod):
+    """The reference's selected_sarsa.txt (write_volume_to_file) parses with the reader
+    used for this build's own dumps: position, normal, 144-sector distribution."""
+    pos, nrm, dist = rtmi_mod.sarsa.read_selected_file(os.path.join(GOLDEN, "selected_sarsa_ref.txt"))
+    q = np.loadtxt(os.path.join(GOLDEN, "to_select.txt"), ndmin=2).astype(np.float32)
+    assert pos.shape == (3, 3) and nrm.shape == (3, 3) and dist.shape == (3, 144)
+    assert np.array_equal(nrm, q[:, 3:6])                          # same-normal volumes
+    assert np.all(np.abs(pos[:, 1] - q[:, 1]) < 1e-6)              # on the queried plane
+    assert np.all(np.linalg.norm(pos - q[:, :3], axis=1) < 0.5)   # the pruned KD walk is approximate
+    assert np.all(np.abs(dist.sum(axis=1) - 1) < 1e-5) and np.all(dist > 0)
+
+
 # ---------------------------------------------------------------- GPU ----------
 
 def _both(rtmi_mod, oracle_mod, gpu_ctx, scene, seed=1984):
@@ -359,3 +371,37 @@ def test_gpu_full_size_door_room_properties(rtmi_mod, gpu_ctx):
     finally:
         rm.close()
         sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_q_table_and_selected_volume_dumps(rtmi_mod, gpu_ctx, tmp_path):
+    """rt_sarsa_save_q / rt_sarsa_save_selected write the reference's text formats
+    (radiance_map_data.txt, selected_sarsa.txt) from the map's state after a frame."""
+    g = geometry(rtmi_mod, "door_room")
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        rm = rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984)
+        try:
+            p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=16, spp_split=4)
+            rm.render(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p, 1)
+            vpos, vnrm, _, _ = rm.volumes()
+            q, cdf, _, _ = rm.read()
+            rm.save_q(str(tmp_path / "radiance_map_data.txt"))
+            fpos, fq = rtmi_mod.sarsa.read_q_file(str(tmp_path / "radiance_map_data.txt"))
+            assert open(tmp_path / "radiance_map_data.txt").readline().strip() == "144"
+            assert fq.shape == (rm.n_volumes, 144)
+            np.testing.assert_allclose(fpos, vpos, rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(fq, q, rtol=1e-5, atol=1e-9)
+            sel = os.path.join(GOLDEN, "to_select.txt")
+            rm.save_selected(sel, str(tmp_path / "selected_sarsa.txt"))
+            spos, snrm, sdist = rtmi_mod.sarsa.read_selected_file(str(tmp_path / "selected_sarsa.txt"))
+            ref = rtmi_mod.sarsa.read_selected_file(os.path.join(GOLDEN, "selected_sarsa_ref.txt"))
+            assert sdist.shape == ref[2].shape
+            qs = np.loadtxt(sel, ndmin=2).astype(np.float32)
+            idx = rm.nearest(qs[:, :3], qs[:, 3:6])
+            np.testing.assert_allclose(spos, vpos[idx], rtol=1e-5, atol=1e-6)
+            assert np.array_equal(snrm, vnrm[idx])
+            pdf = np.diff(cdf[idx], axis=1, prepend=0)
+            np.testing.assert_allclose(sdist, pdf, rtol=1e-5, atol=1e-9)
+            assert np.all(np.abs(sdist.sum(axis=1) - 1) < 1e-4)
+        finally:
+            rm.close()
