@@ -174,6 +174,11 @@ int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc /* n x 3 */,
 /* Same on device buffers, asynchronous on `stream`. */
 int rt_dqn_forward_device(rt_ctx* ctx, const rt_dqn* dqn, const float* d_loc, int n, float* d_q,
                           void* stream);
+/* save_selected_radiance_volumes_vals_nn / write_q_values_for_position
+ * (GPU/deep_learning/q_value_extractor.cu:18-125): for each "x y z nx ny nz" line of
+ * to_select_path, the network's Q values at x (rt_dqn_forward) normalised by their sum,
+ * written as "x y z nx ny nz q0 .. q143" (selected_deep.txt); out_path is replaced. */
+int rt_dqn_save_selected(rt_ctx* ctx, const rt_dqn* dqn, const char* to_select_path, const char* out_path);
 /* importance_sample_direction (nn_rendering_helpers.cu:391-489) for n rays given their Q
  * values (host arrays; q is overwritten with Q*cos as in the reference).  tri: surface the
  * ray sits on; pix: global pixel id (RNG key); tp updated in place; action -1 = none. */

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <fstream>
 
 #include <string>
 #include <vector>
@@ -230,6 +231,34 @@ int rt_dqn_forward_device(rt_ctx* ctx, const rt_dqn* dqn, const float* d_loc, in
     if (n < 0) return err(RT_E_INVALID, "n < 0");
     RT_HIPE(hipSetDevice(rt::ctx_device(ctx)));
     RT_HIPE(rt::launch_dqn_mlp(dqn->net, d_loc, nullptr, nullptr, n, d_q, 0, (hipStream_t)stream));
+    return RT_OK;
+}
+
+int rt_dqn_save_selected(rt_ctx* ctx, const rt_dqn* dqn, const char* to_select_path, const char* out_path) {
+    if (!ctx || !dqn || !to_select_path || !out_path) return err(RT_E_INVALID, "NULL argument");
+    std::vector<float> loc, nrm;
+    int rc = rt::read_locations(to_select_path, &loc, &nrm);
+    if (rc != RT_OK) return rc;
+    const int n = (int)loc.size() / 3;
+    std::vector<float> q((size_t)n * rt::kDqnActions);
+    if (n > 0) {
+        rc = rt_dqn_forward(ctx, dqn, loc.data(), n, q.data());
+        if (rc != RT_OK) return rc;
+    }
+    // write_q_values_for_position (q_value_extractor.cu:18-71): Q normalised by its sum
+    std::ofstream f(out_path);
+    if (!f.is_open()) return err(RT_E_IO, std::string("cannot write ") + out_path);
+    for (int i = 0; i < n; ++i) {
+        const float* qi = &q[(size_t)i * rt::kDqnActions];
+        float sum = 0.f;
+        for (int a = 0; a < rt::kDqnActions; ++a) sum += qi[a];
+        f << loc[3 * i] << " " << loc[3 * i + 1] << " " << loc[3 * i + 2];
+        f << " " << nrm[3 * i] << " " << nrm[3 * i + 1] << " " << nrm[3 * i + 2];
+        for (int a = 0; a < rt::kDqnActions; ++a) f << " " << qi[a] / sum;
+        f << "\n";
+    }
+    f.close();
+    if (f.fail()) return err(RT_E_IO, std::string("write failed: ") + out_path);
     return RT_OK;
 }
 

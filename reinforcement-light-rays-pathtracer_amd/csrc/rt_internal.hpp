@@ -1,6 +1,8 @@
 // rt_internal.hpp — types shared by the C-ABI layer and the gfx950 kernels.
 #pragma once
 
+#include <vector>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -224,6 +226,9 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
 
 // exhaustive rcp_rn == 1.0f/x check over all 2^32 floats (4096 x 256 threads x 4096)
 hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream);
+
+// "x y z nx ny nz" location files (to_select.txt); RT_OK or RT_E_IO (rt_sarsa_host.cpp)
+int read_locations(const char* path, std::vector<float>* loc, std::vector<float>* nrm);
 
 // returns hipErrorInvalidValue for combinations the kernels do not instantiate
 hipError_t launch_render(const RenderLaunch& a, hipStream_t stream);

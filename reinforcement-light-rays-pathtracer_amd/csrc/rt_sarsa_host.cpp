@@ -29,6 +29,35 @@ void scene_host(const rt_scene* s, const float** tri, const float** normals, con
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 RenderLaunch render_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p);
+
+// read_hemisphere_locations_and_normals (GPU/utils/hemisphere_helpers.cu:230-278): one
+// "x y z nx ny nz" per line, tokens split on ' ' and read with std::stof, the first
+// three the location, the rest the normal
+int read_locations(const char* path, std::vector<float>* loc_out, std::vector<float>* nrm_out) {
+    std::ifstream in(path);
+    if (!in.is_open()) return set_error(RT_E_IO, (std::string("cannot read ") + path).c_str());
+    std::string line;
+    try {
+        while (std::getline(in, line)) {
+            float loc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
+            size_t pos;
+            int idx = 0;
+            while ((pos = line.find(' ')) != std::string::npos) {
+                const float v = std::stof(line.substr(0, pos));
+                if (idx < 3) loc[idx] = v;
+                else nrm[idx % 3] = v;
+                ++idx;
+                line.erase(0, pos + 1);
+            }
+            nrm[idx % 3] = std::stof(line);
+            loc_out->insert(loc_out->end(), loc, loc + 3);
+            nrm_out->insert(nrm_out->end(), nrm, nrm + 3);
+        }
+    } catch (const std::exception&) {
+        return set_error(RT_E_IO, (std::string("malformed location line in ") + path).c_str());
+    }
+    return RT_OK;
+}
 }  // namespace rt
 
 namespace {
@@ -697,34 +726,12 @@ int rt_sarsa_save_q(const rt_sarsa* sa, const char* path) {
 
 int rt_sarsa_save_selected(rt_ctx* ctx, const rt_sarsa* sa, const char* to_select_path, const char* out_path) {
     if (!ctx || !sa || !to_select_path || !out_path) return err(RT_E_INVALID, "NULL argument");
-    // read_hemisphere_locations_and_normals (hemisphere_helpers.cu:230-278): tokens
-    // split on ' ', std::stof, the first three the location, the rest the normal
-    std::ifstream in(to_select_path);
-    if (!in.is_open()) return err(RT_E_IO, std::string("cannot read ") + to_select_path);
     std::vector<float> qp, qn;
-    std::string line;
-    try {
-        while (std::getline(in, line)) {
-            float loc[3] = {0.f, 0.f, 0.f}, nrm[3] = {0.f, 0.f, 0.f};
-            size_t pos;
-            int idx = 0;
-            while ((pos = line.find(' ')) != std::string::npos) {
-                const float v = std::stof(line.substr(0, pos));
-                if (idx < 3) loc[idx] = v;
-                else nrm[idx % 3] = v;
-                ++idx;
-                line.erase(0, pos + 1);
-            }
-            nrm[idx % 3] = std::stof(line);
-            qp.insert(qp.end(), loc, loc + 3);
-            qn.insert(qn.end(), nrm, nrm + 3);
-        }
-    } catch (const std::exception&) {
-        return err(RT_E_IO, std::string("malformed location line in ") + to_select_path);
-    }
+    int rc = rt::read_locations(to_select_path, &qp, &qn);
+    if (rc != RT_OK) return rc;
     const int n = (int)qp.size() / 3;
     std::vector<int32_t> idx(n);
-    int rc = rt_sarsa_nearest(ctx, sa, qp.data(), qn.data(), n, idx.data());
+    rc = rt_sarsa_nearest(ctx, sa, qp.data(), qn.data(), n, idx.data());
     if (rc != RT_OK) return rc;
     const int S = rt::kSarsaSectors;
     std::vector<float> cdf((size_t)sa->n_vol * S);

@@ -43,7 +43,7 @@ EXPORTS = (
     "rt_sarsa_create", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
-    "rt_sarsa_save_selected",
+    "rt_sarsa_save_selected", "rt_dqn_save_selected",
 )
 
 
@@ -117,6 +117,7 @@ def _declare(lib):
         "rt_sarsa_info": (i, [_P, _IP, _IP, _UP]),
         "rt_sarsa_set_search": (i, [_P, i]),
         "rt_sarsa_save_q": (i, [_P, ctypes.c_char_p]),
+        "rt_dqn_save_selected": (i, [_P, _P, ctypes.c_char_p, ctypes.c_char_p]),
         "rt_sarsa_save_selected": (i, [_P, _P, ctypes.c_char_p, ctypes.c_char_p]),
         "rt_sarsa_search_stats": (i, [_P, _IP, _IP, ctypes.POINTER(ctypes.c_int64), _U64P]),
         "rt_sarsa_volumes": (i, [_P, _FP, _FP, _IP, _P]),

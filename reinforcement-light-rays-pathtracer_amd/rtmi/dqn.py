@@ -10,6 +10,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -91,6 +92,10 @@ class Dqn:
     def forward_device(self, loc_ptr: int, n: int, q_ptr: int, stream: int = 0) -> None:
         check(lib().rt_dqn_forward_device(self.ctx.handle, self._h, ctypes.c_void_p(loc_ptr), n,
                                           ctypes.c_void_p(q_ptr), ctypes.c_void_p(stream)))
+
+    def save_selected(self, to_select: str, out: str) -> None:
+        """selected_deep.txt format for the locations of to_select.txt (rt_dqn_save_selected)."""
+        check(lib().rt_dqn_save_selected(self.ctx.handle, self._h, os.fsencode(to_select), os.fsencode(out)))
 
     def flops_per_ray(self) -> int:
         """2 * sum(in*out) of the four layers (unpadded)"""

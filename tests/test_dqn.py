@@ -16,7 +16,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import MODELS
+from conftest import GOLDEN, MODELS
 
 DOOR_MODEL = os.path.join(MODELS, "door_room_12_12.model")
 
@@ -181,3 +181,24 @@ def test_dqn_samples_in_flight_bit_identical(rtmi_mod, gpu_ctx, monkeypatch):
     for img, casts in res[1:]:
         assert casts == res[0][1]
         assert np.array_equal(img.view(np.uint32), res[0][0].view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_dqn_selected_volume_dump(rtmi_mod, oracle_mod, gpu_ctx, tmp_path):
+    """rt_dqn_save_selected writes selected_deep.txt: location, normal, Q / sum(Q) of the
+    network at the location (q_value_extractor.cu); the normalised Q agree with the
+    oracle's fp32 (DyNet-arithmetic) forward within the bf16 tolerance."""
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    sel = os.path.join(GOLDEN, "to_select.txt")
+    with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        net.save_selected(sel, str(tmp_path / "selected_deep.txt"))
+        pos, nrm, dist = rtmi_mod.sarsa.read_selected_file(str(tmp_path / "selected_deep.txt"))
+        qs = np.loadtxt(sel, ndmin=2).astype(np.float32)
+        assert np.array_equal(pos, qs[:, :3]) and np.array_equal(nrm, qs[:, 3:6])
+        q = net.forward(qs[:, :3])
+        np.testing.assert_allclose(dist, q / q.sum(axis=1, keepdims=True), rtol=1e-5, atol=1e-9)
+    qf = oracle_mod.dqn_forward(W, b, g.nn_vertices, qs[:, :3], bf16=False)
+    ref = qf / qf.sum(axis=1, keepdims=True)
+    assert np.abs(dist - ref).mean() <= 1e-2 * np.abs(ref).mean()
+    assert np.all(np.abs(dist.sum(axis=1) - 1) < 1e-4)
