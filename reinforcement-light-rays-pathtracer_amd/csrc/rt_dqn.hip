@@ -96,15 +96,17 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 }
 
 // ---------------------------------------------------------------------------
-// MLP layers 1-3: MT*16 rows on 4 waves, A (bf16) from LDS.  Each wave owns every
-// M-tile and the N-tiles chunk, chunk+4, chunk+8, chunk+12 of each 16-tile chunk,
-// so a weight fragment (one contiguous 1 KB load) feeds MT MFMAs; the fragments of
-// K step k+32 are in flight while the MFMAs of step k run.
+// MLP layers 1-3: MT*16 rows on 4 waves, A (bf16) from LDS.  Wave w owns every
+// M-tile and the N-tiles w, w+4, .., w+4(NT-1) (NT = 5, 4, 3 for the widest accepted
+// layers 320, 224, 144), so a weight fragment (one contiguous 1 KB load) feeds MT
+// MFMAs; the fragments of K step k+32 are in flight while the MFMAs of step k run.
+// Slots past the layer's last tile recompute that tile (their MFMAs are
+// unconditional: a conditional MFMA makes the compiler shuttle every accumulator
+// between AGPRs and VGPRs each K step) and are not stored.
 // ---------------------------------------------------------------------------
-template <bool LAST, int MT>
+template <int NT, bool LAST, int MT>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
-                                          __bf16* out_lds, int out_stride, float* q, int row0, int ldq,
-                                          int rows_valid) {
+                                          __bf16* out_lds, int out_stride) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int K = net.K[L];
@@ -113,64 +115,68 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     const float* __restrict__ bias = net.b[L];
     const int r16 = lane & 15;
     const int kg = (lane >> 4) * 8;
-    for (int chunk = wave; chunk < n_tiles; chunk += 16) {
-        // this wave's n-tiles in the chunk: chunk, chunk+4, chunk+8, chunk+12
-        int nt[4];
-        bool use[4];
-        const uint16_t* wrow[4];
+    const uint16_t* wrow[NT];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            nt[j] = chunk + 4 * j;
-            use[j] = nt[j] < n_tiles;
-            wrow[j] = W + ((size_t)(use[j] ? nt[j] : chunk) * (K >> 5) * 64 + lane) * 8;
-        }
-        f32x4 acc[MT][4];
+    for (int j = 0; j < NT; ++j)
+        wrow[j] = W + ((size_t)min(wave + 4 * j, n_tiles - 1) * (K >> 5) * 64 + lane) * 8;
+    f32x4 acc[MT][NT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // weight fragments ping-pong between b0 and b1 (no register copies, which would
+    // make the loads of step k+1 wait inside step k): step k's MFMAs run while step
+    // k+1's fragments are in flight; sched_group_barrier keeps the order
+    // loads -> A reads -> MFMAs (the scheduler otherwise sinks each load to its use)
+    bf16x8 b0[NT], b1[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(wrow[j]);
+    auto step = [&](int k0, const bf16x8 (&bw)[NT]) {
+        bf16x8 a[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
+            a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + k0 + kg);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        bf16x8 bw[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bw[j] = *reinterpret_cast<const bf16x8*>(wrow[j]);
-        for (int k0 = 0; k0 < K; k0 += 32) {
-            const int kb = k0 + kg;
-            // prefetch the next K step's weight fragments (unused tiles re-read a used one)
-            const int kn = (k0 + 32 < K) ? k0 + 32 : k0;
-            bf16x8 bn[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bn[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kn * 16);
-            bf16x8 a[MT];
+        for (int j = 0; j < NT; ++j)
 #pragma unroll
             for (int m = 0; m < MT; ++m)
-                a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + kb);
+                acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], bw[j], acc[m][j], 0, 0, 0);
+    };
+    int k0 = 0;
+    for (; k0 + 32 < K; k0 += 64) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (use[j]) {
+        for (int j = 0; j < NT; ++j) b1[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + (k0 + 32) * 16);
+        step(k0, b0);
+        __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);       // VMEM reads
+        __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);       // LDS reads
+        __builtin_amdgcn_sched_group_barrier(0x008, NT * MT, 0);  // MFMA
+        const int kn = min(k0 + 64, K - 32);
 #pragma unroll
-                    for (int m = 0; m < MT; ++m)
-                        acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], bw[j], acc[m][j], 0, 0, 0);
-                }
+        for (int j = 0; j < NT; ++j) b0[j] = *reinterpret_cast<const bf16x8*>(wrow[j] + kn * 16);
+        step(k0 + 32, b1);
+        __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, NT * MT, 0);
+    }
+    if (k0 < K) step(k0, b0);  // odd number of K steps
+    // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) bw[j] = bn[j];
-        }
-        // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
+    for (int j = 0; j < NT; ++j) {
+        const int nt = wave + 4 * j;
+        if (nt >= n_tiles) continue;  // wave-uniform
+        const int col = nt * 16 + r16;
+        const float bj = bias[col];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (!use[j]) continue;
-            const int col = nt[j] * 16 + r16;
-            const float bj = bias[col];
+        for (int m = 0; m < MT; ++m) {
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int row = m * 16 + (lane >> 4) * 4 + r;
-                    float v = acc[m][j][r] + bj;
-                    v = v > 0.0f ? v : 0.0f;
-                    if (LAST)  // fp32 Q tile staged in LDS, written out coalesced by the caller
-                        reinterpret_cast<float*>(out_lds)[row * kStageStride + col] = v;
-                    else
-                        out_lds[row * out_stride + col] = (__bf16)v;
-                }
+            for (int r = 0; r < 4; ++r) {
+                const int row = m * 16 + (lane >> 4) * 4 + r;
+                float v = acc[m][j][r] + bj;
+                v = v > 0.0f ? v : 0.0f;
+                if (LAST)  // fp32 Q tile staged in LDS, written out coalesced by the caller
+                    reinterpret_cast<float*>(out_lds)[row * kStageStride + col] = v;
+                else
+                    out_lds[row * out_stride + col] = (__bf16)v;
             }
         }
     }
@@ -206,11 +212,11 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
     __syncthreads();
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
     __syncthreads();
-    mlp_layer<false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA, q, row0, ldq, rows_valid);
+    mlp_layer<5, false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
     __syncthreads();
-    mlp_layer<false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB, q, row0, ldq, rows_valid);
+    mlp_layer<4, false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB);  // N <= 224
     __syncthreads();
-    mlp_layer<true, MT>(net, 3, bufB, kStrideB, bufA, 0, q, row0, ldq, rows_valid);
+    mlp_layer<3, true, MT>(net, 3, bufB, kStrideB, bufA, 0);          // N = 144
     __syncthreads();
     // Q tile [kRows][144] from LDS (odd row stride: conflict-free column reads) in
     // 16-B stores: row-major rows are one contiguous run, action-major columns runs
