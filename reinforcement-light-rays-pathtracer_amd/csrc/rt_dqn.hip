@@ -139,8 +139,8 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
-            for (int m = 0; m < MT; ++m)
-                acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[m], bw[j], acc[m][j], 0, 0, 0);
+            for (int m = 0; m < MT; ++m)  // D^T = W * act^T: lane holds 4 features of one ray
+                acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[j], a[m], acc[m][j], 0, 0, 0);
     };
     int k0 = 0;
     for (; k0 + 32 < K; k0 += 64) {
@@ -160,23 +160,36 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
     if (k0 < K) step(k0, b0);  // odd number of K steps
     // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
+    // (the weights are the MFMA's A operand, the activations its B operand, so a lane
+    // holds 4 consecutive features of one ray: one 8-B (bf16) or 16-B (fp32) LDS store)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
         const int nt = wave + 4 * j;
         if (nt >= n_tiles) continue;  // wave-uniform
-        const int col = nt * 16 + r16;
-        const float bj = bias[col];
+        const int col = nt * 16 + (lane >> 4) * 4;
+        const float4 bj = *reinterpret_cast<const float4*>(bias + col);
+        const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
+            const int row = m * 16 + r16;
+            float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int row = m * 16 + (lane >> 4) * 4 + r;
-                float v = acc[m][j][r] + bj;
-                v = v > 0.0f ? v : 0.0f;
-                if (LAST)  // fp32 Q tile staged in LDS, written out coalesced by the caller
-                    reinterpret_cast<float*>(out_lds)[row * kStageStride + col] = v;
-                else
-                    out_lds[row * out_stride + col] = (__bf16)v;
+                v[r] = acc[m][j][r] + bb[r];
+                v[r] = v[r] > 0.0f ? v[r] : 0.0f;
+            }
+            if (LAST) {  // fp32 Q tile staged in LDS, written out coalesced by the caller
+                float* st = reinterpret_cast<float*>(out_lds) + row * kStageStride + col;
+                st[0] = v[0];
+                st[1] = v[1];
+                st[2] = v[2];
+                st[3] = v[3];
+            } else {
+                typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+                bf16x4 h;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) h[r] = (__bf16)v[r];
+                *reinterpret_cast<bf16x4*>(out_lds + row * out_stride + col) = h;
             }
         }
     }
