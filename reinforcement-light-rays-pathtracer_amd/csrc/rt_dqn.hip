@@ -72,26 +72,37 @@ __device__ __forceinline__ void list_append(bool keep, int32_t rid, int32_t* lis
 
 // ---------------------------------------------------------------------------
 // Layer 0, folded to an affine map of the ray position (rt_internal.hpp DqnNet):
-// fp32 on the VALU, one lane per (row, 8 consecutive outputs), ReLU, bf16 into LDS.
+// h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x))) as one fp32 MFMA per 16x16 tile,
+// v_mfma_f32_16x16x4_f32 with A = {-S0, -S1, -S2, c0} per feature and B = (x, y, z, 1)
+// per ray, C = 0: the instruction is the k-ordered fmaf chain, bit for bit
+// (MI355X_MICROARCH.md, Matrix cores), i.e. exactly the expression above.  Lane l
+// gets features 4(l/16)..+3 of ray l%16: one 8-B bf16 LDS store.
 // ---------------------------------------------------------------------------
 template <int MT>
 __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __restrict__ loc_lds,
                                            __bf16* out_lds, int out_stride) {
-    const int groups = net.N[0] >> 3;
-    const int items = MT * 16 * groups;
-    for (int it = threadIdx.x; it < items; it += 256) {
-        const int row = it / groups;
-        const int g = it - row * groups;
-        const float x = loc_lds[row * 3 + 0], y = loc_lds[row * 3 + 1], z = loc_lds[row * 3 + 2];
-        bf16x8 v;
+    typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int r16 = lane & 15, kq = lane >> 4;
+    const int n_tiles = net.N[0] >> 4;
+    float b[MT];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float4 c = net.l0[g * 8 + e];
-            float h = c.w - fmaf(c.z, z, fmaf(c.y, y, c.x * x));
-            h = h > 0.0f ? h : 0.0f;
-            v[e] = (__bf16)h;
+    for (int m = 0; m < MT; ++m) b[m] = (kq < 3) ? loc_lds[(m * 16 + r16) * 3 + kq] : 1.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // 224 features = 14 tiles: slots wave, wave + 4, ..
+        const int nt = wave + 4 * j;
+        if (nt >= n_tiles) continue;  // wave-uniform
+        const float* c = reinterpret_cast<const float*>(net.l0 + nt * 16 + r16);
+        const float a = c[kq];
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[m], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            bf16x4 h;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (__bf16)(d[r] > 0.0f ? d[r] : 0.0f);
+            *reinterpret_cast<bf16x4*>(out_lds + (m * 16 + r16) * out_stride + nt * 16 + kq * 4) = h;
         }
-        *reinterpret_cast<bf16x8*>(out_lds + row * out_stride + g * 8) = v;
     }
 }
 
@@ -223,7 +234,9 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
         locs[row * 3 + 2] = z;
     }
     __syncthreads();
+#ifndef RT_MLP_SKIP_L0  // timing only: layer 0 not evaluated (wrong Q)
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
+#endif
     __syncthreads();
     mlp_layer<5, false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
     __syncthreads();

@@ -169,7 +169,7 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
             c0 += (double)w[i] * (double)nn_vertices[i];
             S[i % 3] += (double)w[i];
         }
-        l0[o] = make_float4((float)S[0], (float)S[1], (float)S[2], (float)c0);
+        l0[o] = make_float4(-(float)S[0], -(float)S[1], -(float)S[2], (float)c0);  // MFMA A operand
     }
     void* p = nullptr;
     int rc = upload(l0.data(), l0.size() * sizeof(float4), &p);

@@ -91,14 +91,14 @@ inline int filter_usable(const DeviceScene& s, float cx, float cy, float cz, flo
 // position p (nn_rendering_helpers.cu:280-298), so W1 x + b1 = (W1 v + b1) - S p
 // with S[o][c] = sum over the vertices of W1[o][3v + c]: an affine map of the 3
 // coordinates of p.  The host folds it once per network in double
-// (rt_dqn_create); the kernel evaluates it in fp32 on the VALU (the reference's
-// own precision) instead of a K = n_in bf16 contraction.  Layers 1-3 run on MFMA:
+// (rt_dqn_create); the kernel evaluates it in fp32 (an exact f32 MFMA, the
+// reference's own precision) instead of a K = n_in bf16 contraction.  Layers 1-3 run on MFMA:
 // device weights bf16, zero padded, stored in MFMA B-fragment order.
 constexpr int kDqnActions = 144;  // GRID_RESOLUTION^2 (GPU/constants/radiance_volumes_settings.h:9)
 constexpr int kDqnGrid = 12;
 
 struct DqnNet {
-    // layer 0 folded: [N[0]] x {S0, S1, S2, c0}; h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x)))
+    // layer 0 folded: [N[0]] x {-S0, -S1, -S2, c0}; h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x)))
     const float4* l0 = nullptr;
     // layers 1-3: bf16 bits in fragment order [N/16][K/32][lane 64][8], lane = kq*16 + r
     // holding W[nt*16 + r][ks*32 + kq*8 .. +7] -- a wave's fragment load is one contiguous 1 KB
