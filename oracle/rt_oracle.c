@@ -726,6 +726,16 @@ static v3 grid_dir(float gx, float gy, v3 N, v3 T, v3 B, v3 pos) {
     return normalize3(mk(w.x - pos.x, w.y - pos.y, w.z - pos.z));
 }
 
+/* cos(theta) of the Chiu-map direction of (gx, gy): 1 - xx^2, xx = max(|2x-1|, |2y-1|)
+ * (the octant branches of chiu_map_t select exactly that; the origin gives 1) -- the
+ * same angle as the reference's dot(N, normalize(M v - p)) up to float rounding */
+static float chiu_cos(float gx, float gy) {
+    float x = 2.0f * (gx / 12.0f) - 1.0f, y = 2.0f * (gy / 12.0f) - 1.0f;
+    float ax = fabsf(x), ay = fabsf(y);
+    float xx = ax > ay ? ax : ay;
+    return 1.0f - xx * xx;
+}
+
 static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint32_t smp, uint32_t ev,
                       v3 *tp, v3 *dir_out) {
     v3 T, B;
@@ -741,8 +751,7 @@ static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint3
         for (int h = 0; h < 2; h++) {
             int a = 2 * a2 + h;
             int gxi = a / 12, gyi = a - gxi * 12;
-            v3 d = grid_dir((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]), N, T, B, pos);
-            float c = dot3(N, d);
+            float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
             float qc = q[a] * c;
             q[a] = qc;
             total = total + qc;

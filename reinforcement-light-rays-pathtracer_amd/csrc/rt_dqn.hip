@@ -288,8 +288,7 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
             const int gxi = a / kDqnGrid;
             const int gyi = a - gxi * kDqnGrid;
             const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
-            const f3 d = grid_direction((float)gxi + r1, (float)gyi + r2, N, T, B, pos);
-            const float c = dot(N, d);
+            const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
             const float qc = q[(size_t)a * qs] * c;
             q[(size_t)a * qs] = qc;
             total = total + qc;

@@ -194,6 +194,20 @@ RT_HD void chiu_map(float x, float y, float* xr, float* yr, float* zr) {
     *zr = origin ? 0.0f : s * sp;
 }
 
+// cos(theta) of the Chiu-map direction of grid point (gx, gy): the map's y component
+// 1 - xx^2 with xx = max(|2x - 1|, |2y - 1|) (chiu_map's octant branches select exactly
+// that), the origin giving 1.  The reference takes dot(N, normalize(M v - p)) of the
+// world direction, the same angle up to float rounding.
+RT_HD float chiu_cos(float gx, float gy) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float x = 2.0f * div12(gx) - 1.0f, y = 2.0f * div12(gy) - 1.0f;  // gx, gy in [0, 12]
+#else
+    const float x = 2.0f * (gx / (float)kGridRes) - 1.0f, y = 2.0f * (gy / (float)kGridRes) - 1.0f;
+#endif
+    const float xx = fmaxf(fabsf(x), fabsf(y));
+    return 1.0f - xx * xx;
+}
+
 // convert_grid_pos_to_direction(_random) (hemisphere_helpers.cu:95-121): map(gx/12, gy/12),
 // world = mat4(T, N, B, pos) * (xh, yh, zh, 1) in glm order, direction = normalize(world - pos)
 RT_HD f3 grid_direction(float gx, float gy, f3 N, f3 T, f3 B, f3 pos) {

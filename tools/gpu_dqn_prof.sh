@@ -3,7 +3,7 @@
 tag=${1:-dqn_prof}
 cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
 out=gpurun_out/$tag; mkdir -p $out
-RUN="python3 tools/bench_dqn.py --scene archway --width 512 --spp 1 --steps 1"
+RUN="python3 tools/bench_dqn.py --scene archway --width 512 --spp 16 --steps 1"
 pass() {
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 "$@" -d $out/$name -o $name --output-format csv -- $RUN > $out/$name.log 2>&1
