@@ -279,19 +279,28 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     uint32_t o[4];
     philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
     const float rv = u01(o[0]);
+    // Q is read in groups of kQGroup cells (all loads of a group in flight at once:
+    // one-at-a-time loads put an HBM round trip on every cell)
+    constexpr int kQGroup = 16;
     float total = 0.0f;
-    for (int a2 = 0; a2 < kDqnActions / 2; ++a2) {
-        philox4x32_10(pix, smp, ev, 1u + (uint32_t)a2, k0, k1, o);
+    for (int g = 0; g < kDqnActions; g += kQGroup) {
+        float qv[kQGroup];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const int a = 2 * a2 + h;
-            const int gxi = a / kDqnGrid;
-            const int gyi = a - gxi * kDqnGrid;
-            const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
-            const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
-            const float qc = q[(size_t)a * qs] * c;
-            q[(size_t)a * qs] = qc;
-            total = total + qc;
+        for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
+#pragma unroll
+        for (int u2 = 0; u2 < kQGroup; u2 += 2) {
+            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u2) >> 1), k0, k1, o);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int a = g + u2 + h;
+                const int gxi = a / kDqnGrid;
+                const int gyi = a - gxi * kDqnGrid;
+                const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
+                const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
+                const float qc = qv[u2 + h] * c;
+                q[(size_t)a * qs] = qc;
+                total = total + qc;
+            }
         }
     }
     SampleOut res;
@@ -299,13 +308,20 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     res.dir = make3(0.0f, 0.0f, 0.0f);
     float q_sum = 0.0f;
     float qd_sel = 0.0f;
-    for (int a = 0; a < kDqnActions; ++a) {
-        const float qd = q[(size_t)a * qs] / total;
-        q_sum = q_sum + qd;
-        if (q_sum > rv) {
-            res.action = a;
-            qd_sel = qd;
-            break;
+    for (int g = 0; g < kDqnActions && res.action < 0; g += kQGroup) {
+        float qv[kQGroup];
+#pragma unroll
+        for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
+#pragma unroll
+        for (int u = 0; u < kQGroup; ++u) {
+            if (res.action < 0) {
+                const float qd = qv[u] / total;
+                q_sum = q_sum + qd;
+                if (q_sum > rv) {
+                    res.action = g + u;
+                    qd_sel = qd;
+                }
+            }
         }
     }
     if (res.action >= 0) {
