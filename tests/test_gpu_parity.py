@@ -89,6 +89,28 @@ def test_intersect_edge_cases(rtmi_mod, oracle_mod, gpu_ctx):
         check_intersect(rtmi_mod, oracle_mod, gpu_ctx, geom, o, d, 512.0, rule)
 
 
+@pytest.mark.gpu
+def test_intersect_non_finite_and_extreme_rays(rtmi_mod, oracle_mod, gpu_ctx):
+    """NaN / inf components, zero directions and far-away origins take the exact
+    single-phase test (the filter keeps every triangle of a non-finite ray)."""
+    geom = rtmi_mod.cornell_geometry(0)
+    rng = np.random.default_rng(9)
+    n = 512
+    o = rng.uniform(-1, 1, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3))
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    o[0:8, 0] = np.nan
+    d[8:16, 1] = np.nan
+    o[16:24, 2] = np.inf
+    d[24:32, 0] = -np.inf
+    d[32:40] = 0.0
+    o[40:48] *= np.float32(1e30)
+    o[48:56] *= np.float32(1e-30)
+    d[56:64] *= np.float32(1e-20)
+    for rule in (0, 1):
+        check_intersect(rtmi_mod, oracle_mod, gpu_ctx, geom, o, d, 512.0, rule)
+
+
 def test_intersect_empty_batch(rtmi_mod, gpu_ctx):
     geom = rtmi_mod.cornell_geometry(0)
     with rtmi_mod.Scene(gpu_ctx, geom) as sc:
@@ -116,6 +138,9 @@ RENDER_CASES = [
     ("door_room", 1, dict(width=40, height=40, spp=4), None),
     ("archway", 1, dict(width=40, height=40, spp=4, hit_rule=0), None),
     ("complex_light_room", 1, dict(width=40, height=40, spp=4), None),
+    # the bench's chunking (32 lanes per pixel) on an image that is no multiple of 16
+    ("cornell_cpu", 0, dict(width=37, height=23, spp=64, spp_split=32), None),
+    ("cornell_gpu", 1, dict(width=21, height=19, spp=32, spp_split=32), None),
 ]
 
 
