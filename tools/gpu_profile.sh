@@ -21,5 +21,5 @@ step write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $out/write -o write 
 step sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU --kernel-trace -d $out/sq -o sq --output-format csv -- $BENCH
 # kernel statistics of the learned-sampling paths (configs 3 and 4)
 step kt_sarsa 300 rocprofv3 --kernel-trace --stats -d $out/kt_sarsa -o kt_sarsa --output-format csv -- python3 tools/bench_sarsa.py --frames 2
-step kt_dqn 300 rocprofv3 --kernel-trace --stats -d $out/kt_dqn -o kt_dqn --output-format csv -- python3 tools/bench_dqn.py --scene archway --width 512 --spp 1 --steps 2
+step kt_dqn 300 rocprofv3 --kernel-trace --stats -d $out/kt_dqn -o kt_dqn --output-format csv -- python3 tools/bench_dqn.py --scene archway --width 512 --spp 16 --steps 1
 step fetch_dqn 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $out/fetch_dqn -o fetch_dqn --output-format csv -- python3 tools/bench_dqn.py --scene archway --width 256 --spp 1 --steps 1
