@@ -42,8 +42,8 @@ VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
 TILE = 32
 # HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
 # (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
-PMC_PROFILE = os.path.join("profiles", "r1v6_pmc.json")
-DEFAULT_WORKLOAD = (512, 512, 256, 32)
+PMC_PROFILE = os.path.join("profiles", "r1v7_pmc.json")
+DEFAULT_WORKLOAD = (512, 512, 256, 64)
 
 
 def parse():
@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--width", type=int, default=512)
     ap.add_argument("--height", type=int, default=512)
     ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--spp-split", type=int, default=32)
+    ap.add_argument("--spp-split", type=int, default=64)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target CPU-baseline sample duration (0 disables)")
     ap.add_argument("--no-parity", action="store_true")
@@ -75,7 +75,7 @@ def pmc_traffic(params):
     return None, None
 
 
-SQ_PROFILE = os.path.join("profiles", "r1v6_sq_summary.json")
+SQ_PROFILE = os.path.join("profiles", "r1v7_sq_summary.json")
 
 
 def pmc_valu_issue(params):

@@ -42,6 +42,7 @@ def main():
     t1 = None
     for world in args.worlds:
         per_rank = []
+        casts_rank = []
         for rank in range(world):
             tiles = rtmi.tiles.rank_tiles(p.width, p.height, TILE, rank, world)
             out = torch.zeros((tiles.shape[0], TILE, TILE, 3), dtype=torch.float32, device=dev)
@@ -61,10 +62,15 @@ def main():
                 torch.cuda.synchronize()
                 ts.append(e0.elapsed_time(e1))
             per_rank.append(float(np.median(ts)))
+            casts.zero_()
+            run()
+            torch.cuda.synchronize()
+            casts_rank.append(int(casts.item()))
         tmax = max(per_rank)
         if world == 1:
             t1 = tmax
         res["worlds"][world] = {"ms_per_rank": [round(t, 4) for t in per_rank], "ms_max": round(tmax, 4),
+                                "casts_per_rank": casts_rank,
                                 "kernel_speedup": round(t1 / tmax, 3) if t1 else None}
     print(json.dumps(res), flush=True)
     scene.close()
