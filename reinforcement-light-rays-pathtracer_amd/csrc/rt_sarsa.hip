@@ -19,13 +19,22 @@
 
 #include "rt_trace.hpp"
 
-// A/B knobs (timing only; both change results): RT_SARSA_NO_TD drops the TD atomics,
-// RT_SARSA_NO_KD replaces the nearest-volume search by volume 0
+// A/B knobs (timing / statistics builds only; all but SCAN_STATS change results):
+// RT_SARSA_NO_TD drops the TD atomics, RT_SARSA_NO_KD replaces the nearest-volume
+// search by volume 0, RT_SARSA_FIRST_ONLY takes the first candidate of the grid list
+// (same normal class: frame-0 paths keep their statistics), RT_SARSA_SCAN_STATS
+// counts the grid scan steps (4 candidates each) in grid_fallbacks
 #ifndef RT_SARSA_NO_TD
 #define RT_SARSA_NO_TD 0
 #endif
 #ifndef RT_SARSA_NO_KD
 #define RT_SARSA_NO_KD 0
+#endif
+#ifndef RT_SARSA_SCAN_STATS
+#define RT_SARSA_SCAN_STATS 0
+#endif
+#ifndef RT_SARSA_FIRST_ONLY
+#define RT_SARSA_FIRST_ONLY 0
 #endif
 #ifndef RT_SARSA_NO_FALLBACK  // grid answer even where the KD walk is needed (timing only)
 #define RT_SARSA_NO_FALLBACK 0
@@ -109,7 +118,16 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
         const float dq = __builtin_sqrtf((qx * qx + qy * qy) + qz * qz);
         float b1 = INFINITY, b2 = INFINITY;
         int bv = -1;
+#if RT_SARSA_SCAN_STATS  // statistics builds only: grid_fallbacks counts scan steps instead
+        uint32_t steps = 0;
+#endif
+#if RT_SARSA_FIRST_ONLY  // timing only: the first listed candidate (wrong volumes)
+        if (k0 < e) return __float_as_int(m.grid_leaf[k0].w);
+#endif
         for (uint32_t k = k0; k < e; k += 4) {  // 4 candidate loads in flight
+#if RT_SARSA_SCAN_STATS
+            ++steps;
+#endif
             float4 L[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) L[u] = m.grid_leaf[min(k + (uint32_t)u, e - 1u)];
@@ -133,6 +151,9 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
                 }
             }
         }
+#if RT_SARSA_SCAN_STATS
+        atomicAdd(m.grid_fallbacks, (unsigned long long)steps);
+#endif
         const float d = sqrtf(b1);
         if (bv >= 0 && d < m.grid_h && sqrtf(b2) != d) {
             const float d0 = len3(pos.x - m.root_x, pos.y - m.root_y, pos.z - m.root_z);
