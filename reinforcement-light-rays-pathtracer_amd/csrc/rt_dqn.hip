@@ -39,6 +39,14 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 #define RT_MLP_MT 4  // 16-row M-tiles per MLP workgroup
 #endif
 constexpr int kTileM = RT_MLP_MT * 16;  // rays per MLP workgroup
+#ifndef RT_MLP_WAVES
+#define RT_MLP_WAVES 4  // waves per MLP workgroup (each owns every M-tile, 1/W of the N-tiles)
+#endif
+constexpr int kMlpWaves = RT_MLP_WAVES;
+constexpr int kMlpThreads = 64 * kMlpWaves;
+static_assert(kTileM <= kMlpThreads, "one ray position per thread at load");
+// N-tile slots per wave for the widest accepted layers (out 224 | 320, 224, 144)
+constexpr int slots(int tiles) { return (tiles + kMlpWaves - 1) / kMlpWaves; }
 // MT = 8 (one 142 KB workgroup per CU) is 1.4x slower; a single flattened weight
 // stream over layers 1-3 with a 2-4 deep register ring was 2x slower (round-1 A/B,
 // DESIGN.md §4).
@@ -90,8 +98,8 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 #pragma unroll
     for (int m = 0; m < MT; ++m) b[m] = (kq < 3) ? loc_lds[(m * 16 + r16) * 3 + kq] : 1.0f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // 224 features = 14 tiles: slots wave, wave + 4, ..
-        const int nt = wave + 4 * j;
+    for (int j = 0; j < slots(14); ++j) {  // 224 features = 14 tiles: slots wave, wave + W, ..
+        const int nt = wave + kMlpWaves * j;
         if (nt >= n_tiles) continue;  // wave-uniform
         const float* c = reinterpret_cast<const float*>(net.l0 + nt * 16 + r16);
         const float a = c[kq];
@@ -129,7 +137,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     const uint16_t* wrow[NT];
 #pragma unroll
     for (int j = 0; j < NT; ++j)
-        wrow[j] = W + ((size_t)min(wave + 4 * j, n_tiles - 1) * (K >> 5) * 64 + lane) * 8;
+        wrow[j] = W + ((size_t)min(wave + kMlpWaves * j, n_tiles - 1) * (K >> 5) * 64 + lane) * 8;
     f32x4 acc[MT][NT];
 #pragma unroll
     for (int m = 0; m < MT; ++m)
@@ -175,7 +183,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     // holds 4 consecutive features of one ray: one 8-B (bf16) or 16-B (fp32) LDS store)
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-        const int nt = wave + 4 * j;
+        const int nt = wave + kMlpWaves * j;
         if (nt >= n_tiles) continue;  // wave-uniform
         const int col = nt * 16 + (lane >> 4) * 4;
         const float4 bj = *reinterpret_cast<const float4*>(bias + col);
@@ -208,7 +216,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
 
 // One workgroup = MT*16 rays (LDS: MT=4 -> 71 KB, two workgroups per CU).
 template <int MT>
-__global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
+__global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
                                                  float* __restrict__ q, int ldq) {
@@ -238,11 +246,11 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
 #endif
     __syncthreads();
-    mlp_layer<5, false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
+    mlp_layer<slots(20), false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
     __syncthreads();
-    mlp_layer<4, false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB);  // N <= 224
+    mlp_layer<slots(14), false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB);  // N <= 224
     __syncthreads();
-    mlp_layer<3, true, MT>(net, 3, bufB, kStrideB, bufA, 0);          // N = 144
+    mlp_layer<slots(9), true, MT>(net, 3, bufB, kStrideB, bufA, 0);           // N = 144
     __syncthreads();
     // Q tile [kRows][144] from LDS (odd row stride: conflict-free column reads) in
     // 16-B stores: row-major rows are one contiguous run, action-major columns runs
@@ -250,13 +258,13 @@ __global__ __launch_bounds__(256) void k_dqn_mlp(const DqnNet net, const float* 
     const float* stage = reinterpret_cast<const float*>(bufA);
     if (ldq == 0) {
         float* dst = q + (size_t)row0 * kDqnActions;
-        for (int t = threadIdx.x; t < rows_valid * (kDqnActions / 4); t += 256) {
+        for (int t = threadIdx.x; t < rows_valid * (kDqnActions / 4); t += kMlpThreads) {
             const int r = t / (kDqnActions / 4), c = (t - r * (kDqnActions / 4)) * 4;
             const float* sp = stage + r * kStageStride + c;
             *reinterpret_cast<float4*>(dst + (size_t)r * kDqnActions + c) = make_float4(sp[0], sp[1], sp[2], sp[3]);
         }
     } else {
-        for (int t = threadIdx.x; t < kDqnActions * (kRows / 4); t += 256) {
+        for (int t = threadIdx.x; t < kDqnActions * (kRows / 4); t += kMlpThreads) {
             const int c = t / (kRows / 4), r = (t - c * (kRows / 4)) * 4;
             const float* sp = stage + r * kStageStride + c;
             *reinterpret_cast<float4*>(q + (size_t)c * ldq + row0 + r) =
@@ -530,7 +538,7 @@ hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* li
     if (max_rows <= 0) return hipSuccess;
     const int blocks = (max_rows + kTileM - 1) / kTileM;
     if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(256), 0, stream, net, loc, list, count,
+    hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc, list, count,
                        max_rows, q, ldq);
     return hipGetLastError();
 }
