@@ -116,6 +116,13 @@ def cpu_baseline(geom, params, cam_pos, seconds):
         _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
+    # the 1-thread figure on a 2-row strip of the same frame
+    oracle.set_threads(1)
+    y1 = params.height // 2 - 1
+    t0 = time.perf_counter()
+    _, casts1 = oracle.render(geom, ocam, op, (0, y1, w, 2))
+    dt1 = time.perf_counter() - t0
+    oracle.set_threads(threads)
     return {
         "value": round(casts / best / 1e6, 3),
         "unit": "Mrays/s",
@@ -123,6 +130,8 @@ def cpu_baseline(geom, params, cam_pos, seconds):
         "kind": "port",
         "sample": f"rows {y0}..{y0 + rows - 1} of the {w}x{params.height}/{params.spp}-spp frame "
                   f"({casts} ray casts, {best:.1f} s, OpenMP over rows)",
+        "value_1thread": round(casts1 / max(dt1, 1e-9) / 1e6, 3),
+        "sample_1thread": f"rows {y1}..{y1 + 1} ({casts1} ray casts, {dt1:.2f} s, 1 thread)",
     }
 
 

@@ -54,6 +54,10 @@ def lib():
                                  ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams),
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _FP,
                                  ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_render_sequential.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, _FP,
+                                            ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _IP]
         L.orc_pack_argb.argtypes = [_FP, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_threads.argtypes = [ctypes.c_int]
@@ -146,6 +150,30 @@ def render(geom, cam: OrcCamera, params: OrcParams, rect=None):
     lib().orc_render(_f(tri), _f(alb), n_surf, _f(em), _i(grp), n_light, ctypes.byref(cam),
                      ctypes.byref(params), x0, y0, w, h, _f(out), ctypes.byref(casts))
     return out, int(casts.value)
+
+
+def render_sequential(geom, cam: OrcCamera, params: OrcParams):
+    """The whole frame in the CPU engine's own order and glibc rand() stream
+    (rt_oracle.c orc_render_sequential; SURVEY.md §8(c) gate 3): CPU preset only."""
+    get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
+    tri = np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32)
+    alb = np.ascontiguousarray(get("albedo"), np.float32)
+    em = np.ascontiguousarray(get("emission"), np.float32)
+    grp = np.ascontiguousarray(get("light_group"), np.int32)
+    n_surf, n_light = get("tri").shape[0], get("light").shape[0]
+    out = np.zeros((params.height, params.width, 3), np.float32)
+    casts = ctypes.c_uint64(0)
+    rc = lib().orc_render_sequential(_f(tri), _f(alb), n_surf, _f(em), _i(grp), n_light, ctypes.byref(cam),
+                                     ctypes.byref(params), _f(out), ctypes.byref(casts))
+    if rc != 0:
+        raise ValueError("reference_sequential needs the CPU preset, uniform sampler and CPU hit rule")
+    return out, int(casts.value)
+
+
+def glibc_rand(seed: int, n: int) -> np.ndarray:
+    out = np.zeros(n, np.int32)
+    lib().orc_glibc_rand(seed, n, _i(out))
+    return out
 
 
 def pack_argb(rgb) -> np.ndarray:

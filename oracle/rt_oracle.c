@@ -38,7 +38,9 @@
  * OpenMP.  Both this oracle and the HIP kernels draw from a counter-based
  * Philox4x32-10 keyed on (seed, global pixel, sample, event) — the spec in
  * DESIGN.md §3.  sin/cos of 2*pi*r use the spec's own quarter-turn
- * polynomial so host and device agree bit for bit.
+ * polynomial so host and device agree bit for bit.  orc_render_sequential
+ * restates the reference's own stream (glibc rand(), one thread, its loop
+ * order and libm trig) as the statistical bridge of SURVEY.md §8(c) gate 3.
  *
  * PARITY PINNING: the reference ships no tests and no golden outputs for
  * this path; its code could not be compiled or run here (SURVEY.md §8(c),
@@ -377,6 +379,17 @@ static void normal_frame(v3 n, v3 *T, v3 *Bv) {
     *Bv = cross3(n, *T);
 }
 
+/* reference_sequential mode (parity gate 3): the CPU engine's own
+ * random stream — glibc rand() (never seeded by the reference: seed 1), drawn as
+ * (float)rand() / RAND_MAX (CPU/path_tracing/default_path_tracing.cpp:26-27,
+ * CPU/utils/hemisphere_helpers.cpp:69-70) in the order of one thread running the
+ * x-outer / y-inner pixel loop (default_path_tracing.cpp:9-17) — and its libm trig
+ * (phi = 2 * M_PI * r2 in double, then cosf/sinf, hemisphere_helpers.cpp:14-20).
+ * Set only inside orc_render_sequential, which runs on one thread. */
+static int g_seq = 0;
+
+static float rand01(void) { return (float)rand() / (float)RAND_MAX; }
+
 /* CPU/utils/hemisphere_helpers.cpp:4-21 (sampler 0) + cosine variant (sampler 1);
  * world = (s.x*B + s.y*N) + s.z*T, :73-77 */
 static v3 sample_dir(v3 n, float r1, float r2, int sampler, float *cos_theta) {
@@ -391,7 +404,13 @@ static v3 sample_dir(v3 n, float r1, float r2, int sampler, float *cos_theta) {
         sin_theta = sqrtf(1.0f - r1);
     }
     float sphi, cphi;
-    orc_sincos_turn(r2, &sphi, &cphi);
+    if (g_seq) {
+        const float phi = (float)(2 * 3.14159265358979323846 * (double)r2); /* M_PI */
+        sphi = sinf(phi);
+        cphi = cosf(phi);
+    } else {
+        orc_sincos_turn(r2, &sphi, &cphi);
+    }
     float sx = sin_theta * cphi, sz = sin_theta * sphi;
     *cos_theta = y;
     return mk((sx * Bv.x + y * n.x) + sz * T.x,
@@ -455,7 +474,12 @@ static v3 trace_recursive(const orc_scene *sc, const orc_params *p, uint32_t pix
     v3 pos = mk(o.x + h.t * D.x, o.y + h.t * D.y, o.z + h.t * D.z);
     const float *nn = sc->normal + (size_t)h.tri * 3;
     float r1, r2;
-    draw2(p->seed, pix, smp, 1u + (uint32_t)bounces, &r1, &r2);
+    if (g_seq) {
+        r1 = rand01();
+        r2 = rand01();
+    } else {
+        draw2(p->seed, pix, smp, 1u + (uint32_t)bounces, &r1, &r2);
+    }
     float cos_theta;
     v3 s = sample_dir(mk(nn[0], nn[1], nn[2]), r1, r2, p->sampler, &cos_theta);
     v3 start = mk(pos.x + 1e-5f * s.x, pos.y + 1e-5f * s.y, pos.z + 1e-5f * s.z);
@@ -560,6 +584,51 @@ ORC_API int orc_render(const float *tri, const float *albedo, int n_surf,
     free(sc.normal);
     if (out_casts) *out_casts = total;
     return 0;
+}
+
+/*
+ * The whole frame in the reference's own sampling order and random stream
+ * (g_seq above): CPU preset, uniform sampler, CPU hit rule only.  out_rgb: W*H*3,
+ * row-major.  srand(seed) first (seed 1 = the reference's unseeded stream).  Its
+ * images match the Philox renders only statistically (gate 3, tests/).
+ */
+ORC_API int orc_render_sequential(const float *tri, const float *albedo, int n_surf,
+                                  const float *emission, const int32_t *light_group, int n_light,
+                                  const orc_camera *cam, const orc_params *p, float *out_rgb,
+                                  uint64_t *out_casts) {
+    if (p->preset != 0 || p->sampler != 0 || p->hit_rule != 0) return -1;
+    orc_scene sc;
+    scene_init(&sc, tri, albedo, n_surf, emission, light_group, n_light);
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    uint64_t casts = 0;
+    srand((unsigned)p->seed);
+    g_seq = 1;
+    for (int px = 0; px < p->width; px++) {
+        for (int py = 0; py < p->height; py++) {
+            v3 acc = mk(0.0f, 0.0f, 0.0f);
+            for (int s = 0; s < p->spp; s++) {
+                const float r1 = rand01();
+                const float r2 = rand01();
+                v3 o, d;
+                camera_ray(cam, p, cy, sy, 1.0f, 0.0f, px, py, r1, r2, &o, &d);
+                v3 L = trace_recursive(&sc, p, 0u, 0u, o, d, 0, &casts);
+                acc.x = acc.x + L.x; acc.y = acc.y + L.y; acc.z = acc.z + L.z;
+            }
+            const float fs = (float)p->spp;
+            float *dst = out_rgb + ((size_t)py * p->width + px) * 3;
+            dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+        }
+    }
+    g_seq = 0;
+    free(sc.normal);
+    if (out_casts) *out_casts = casts;
+    return 0;
+}
+
+/* the first n values of glibc rand() after srand(seed) (pins the stream above) */
+ORC_API void orc_glibc_rand(unsigned seed, int n, int32_t *out) {
+    srand(seed);
+    for (int i = 0; i < n; i++) out[i] = (int32_t)rand();
 }
 
 /* CPU/sdl/sdl_screen.cpp:100-112: uint32(clamp(255*c, 0, 255)), (128<<24)+(r<<16)+(g<<8)+b */

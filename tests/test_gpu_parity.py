@@ -199,3 +199,20 @@ def test_full_size_properties(rtmi_mod, oracle_mod, gpu_ctx):
                                 (240, 120, 16, 16))
     assert rc == cw
     assert np.array_equal(win, ref)
+
+
+def test_config1_gpu_vs_reference_sequential(rtmi_mod, oracle_mod, gpu_ctx):
+    """SURVEY.md §8(c) gate 3 on BASELINE config 1 (Cornell 256^2, 4 spp, CPU preset):
+    the GPU frame (Philox stream) against the CPU engine's own sampling order and glibc
+    rand() stream (oracle.render_sequential): per-channel image-mean z score < 3, and
+    the same ray casts per sample within 1%."""
+    geom = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_CPU)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_CPU, width=256, height=256, spp=4)
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        img, casts = rtmi_mod.render(gpu_ctx, sc, rtmi_mod.camera(CORNELL_CAM), p)
+    ref, ref_casts = oracle_mod.render_sequential(geom, oracle_mod.camera(CORNELL_CAM),
+                                                  oracle_mod.params_from(p))
+    d = (img.astype(np.float64) - ref.astype(np.float64)).reshape(-1, 3)
+    z = d.mean(0) / (d.std(0) / np.sqrt(d.shape[0]))
+    assert np.all(np.abs(z) < 3.0), z
+    assert abs(casts - ref_casts) <= 0.01 * ref_casts

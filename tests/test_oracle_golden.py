@@ -185,3 +185,46 @@ def test_oracle_render_deterministic_and_split_consistent(rtmi_mod, oracle_mod):
     # rectangle renders are crops of the full frame
     r, _ = oracle_mod.render(g, cam, oracle_mod.params_from(p), rect=(5, 7, 11, 9))
     assert np.array_equal(r, c[7:16, 5:16])
+
+
+# --- reference_sequential mode (parity gate 3) ---------------
+
+def mean_z(a, b):
+    """per-channel z score of the mean per-pixel difference of two independent
+    unbiased renders of the same frame (0 expected; |z| < 3 is the gate)"""
+    d = (np.asarray(a, np.float64) - np.asarray(b, np.float64)).reshape(-1, 3)
+    return d.mean(0) / (d.std(0) / math.sqrt(d.shape[0]))
+
+
+def test_glibc_rand_kat(oracle_mod):
+    # glibc's rand() after srand(1) (= the reference's never-seeded stream)
+    assert list(oracle_mod.glibc_rand(1, 4)) == [1804289383, 846930886, 1681692777, 1714636915]
+
+
+def test_reference_sequential_deterministic_and_guarded(rtmi_mod, oracle_mod):
+    g = oracle_mod.cornell(0)
+    cam = oracle_mod.camera(CORNELL_CAM)
+    p = rtmi_mod.default_params(0, width=24, height=16, spp=4)
+    a, ca = oracle_mod.render_sequential(g, cam, oracle_mod.params_from(p))
+    b, cb = oracle_mod.render_sequential(g, cam, oracle_mod.params_from(p))
+    assert np.array_equal(a, b) and ca == cb and ca >= 24 * 16 * 4
+    p.seed = 7  # srand(seed): another stream
+    c, _ = oracle_mod.render_sequential(g, cam, oracle_mod.params_from(p))
+    assert not np.array_equal(a, c)
+    p.sampler = 1
+    with pytest.raises(ValueError):
+        oracle_mod.render_sequential(g, cam, oracle_mod.params_from(p))
+
+
+@pytest.mark.parametrize("width,spp", [(128, 16), (64, 128)])
+def test_reference_sequential_statistical(rtmi_mod, oracle_mod, width, spp):
+    """Gate 3: the Philox renders (this oracle = the GPU kernel, bit for bit) agree
+    with the reference's own rand() stream and loop order in the image mean."""
+    g = oracle_mod.cornell(0)
+    cam = oracle_mod.camera(CORNELL_CAM)
+    p = rtmi_mod.default_params(0, width=width, height=width, spp=spp)
+    a, ca = oracle_mod.render_sequential(g, cam, oracle_mod.params_from(p))
+    b, cb = oracle_mod.render(g, cam, oracle_mod.params_from(p))
+    z = mean_z(a, b)
+    assert np.all(np.abs(z) < 3.0), z
+    assert abs(ca - cb) <= 0.01 * cb  # ray casts per sample: same path-length law
