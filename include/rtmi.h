@@ -196,6 +196,37 @@ int rt_render_dqn_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_dqn*
                                int n_tiles, int tile_size, float* d_out, uint64_t* d_casts,
                                void* stream);
 
+/* ---- Neural-Q training ---------------------------
+ * The learning rule of NeuralQPathtracer::render_frame
+ * (GPU/deep_learning/neural_q_pathtracer.cu:420-513), which the reference runs through
+ * DyNet on the host, on device buffers in fp32: parameters, gradients and Adam moments
+ * live on the device; rt_dqn_trainer_params copies the weights out (row-major, the
+ * rt_dqn_create layout) to rebuild the bf16 inference network. */
+typedef struct rt_dqn_trainer rt_dqn_trainer;
+/* DQNetwork::initialize (NN_Builders/dq_network.cu:8-33) with the given parameters +
+ * dynet::AdamTrainer(model) (neural_q_pathtracer.cu:47): DyNet defaults beta1 0.9,
+ * beta2 0.999, eps 1e-8, global gradient-norm clipping at 5; learning_rate (DyNet 1e-3). */
+int rt_dqn_trainer_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t* hidden /* 3 */,
+                          int n_out, const float* const* W /* 4 */, const float* const* b /* 4 */,
+                          float learning_rate, rt_dqn_trainer** out);
+int rt_dqn_trainer_destroy(rt_dqn_trainer* trainer);
+int rt_dqn_trainer_params(const rt_dqn_trainer* trainer, float* const* W /* 4 */, float* const* b /* 4 */);
+/* Steps 5-7 of the training loop (neural_q_pathtracer.cu:478-513) on n rays: forward on the
+ * current states (network input nn_vertices - loc), pick the taken actions, loss =
+ * sum (target - q_a)^2 (sum_batches), backward, trainer.update().  Device arrays:
+ * d_loc n x 3, d_action n (an action outside [0, n_out) contributes nothing), d_target n.
+ * loss_out / grad_norm_out (host, optional; either one synchronises the stream): the loss
+ * and the gradient L2 norm before clipping. */
+int rt_dqn_train_step_device(rt_ctx* ctx, rt_dqn_trainer* trainer, const float* d_loc, const int32_t* d_action,
+                             const float* d_target, int n, float* loss_out, float* grad_norm_out, void* stream);
+/* compute_td_targets (GPU/deep_learning/nn_rendering_helpers.cu:91-140): target =
+ * reward + max_a(Q(s',a) cos_a) * discount, reward alone where terminal == 1; action 0 is
+ * not cosine-weighted (as in the reference); cos_a of a jittered direction in cell a
+ * (Philox: pixel, sample, event 1 + bounce).  d_next_q: n x 144 row-major. */
+int rt_dqn_td_targets_device(rt_ctx* ctx, uint64_t seed, const float* d_next_q, const int32_t* d_terminal,
+                             const float* d_reward, const float* d_discount, const uint32_t* d_pix, int sample,
+                             int bounce, int n, float* d_target, void* stream);
+
 /* ---- Expected-SARSA radiance volumes (BASELINE config 3) ------------------ */
 typedef struct rt_sarsa rt_sarsa;
 

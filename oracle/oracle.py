@@ -57,6 +57,8 @@ def lib():
         L.orc_render_sequential.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, _FP,
                                             ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_td_targets.argtypes = [ctypes.c_uint64, _FP, _IP, _FP, _FP, ctypes.POINTER(ctypes.c_uint32),
+                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, _FP]
         L.orc_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _IP]
         L.orc_pack_argb.argtypes = [_FP, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
         L.orc_num_threads.restype = ctypes.c_int
@@ -343,3 +345,81 @@ class Sarsa:
         self._L.orc_render_sarsa(self._h, ctypes.byref(cam), ctypes.byref(params), frames, _f(out),
                                  ctypes.byref(casts))
         return out, int(casts.value)
+
+
+# --- Neural-Q training ------------------------------------
+
+def td_targets(seed, next_q, terminal, reward, discount, pix, sample, bounce):
+    """compute_td_targets restated (rt_oracle.c orc_td_targets), float32 in and out."""
+    q = np.ascontiguousarray(next_q, np.float32)
+    n = q.shape[0]
+    term = np.ascontiguousarray(terminal, np.int32)
+    rw = np.ascontiguousarray(reward, np.float32)
+    dc = np.ascontiguousarray(discount, np.float32)
+    px = np.ascontiguousarray(pix, np.uint32)
+    out = np.zeros(n, np.float32)
+    lib().orc_td_targets(seed, _f(q), _i(term), _f(rw), _f(dc),
+                         px.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), sample, bounce, n, _f(out))
+    return out
+
+
+class AdamRef:
+    """fp64 restatement of one Neural-Q learning step (neural_q_pathtracer.cu:478-513):
+    DQNetwork forward (b + W x, rectify x 4; NN_Builders/fc_layer.cu:40-72), pick, loss =
+    sum (target - q_a)^2, backward, dynet::AdamTrainer update with DyNet's defaults
+    (global-norm clipping at 5: scale 5/||g||; m = b1 m + (1-b1) s g; v = b2 v + (1-b2) s^2 g^2;
+    x -= lr sqrt(1-b2^t)/(1-b1^t) m/(sqrt(v)+eps)).  DyNet is absent here:
+    parity unpinned against DyNet itself; this is the published algorithm."""
+
+    def __init__(self, nn_vertices, W, b, lr=1e-3, b1=0.9, b2=0.999, eps=1e-8, clip=5.0):
+        self.v = np.asarray(nn_vertices, np.float64).ravel()
+        self.P = [np.asarray(w, np.float64).copy() for w in W] + [np.asarray(x, np.float64).ravel().copy() for x in b]
+        self.M = [np.zeros_like(p) for p in self.P]
+        self.V = [np.zeros_like(p) for p in self.P]
+        self.lr, self.b1, self.b2, self.eps, self.clip = lr, b1, b2, eps, clip
+        self.t = 0
+
+    def forward(self, loc):
+        loc = np.asarray(loc, np.float64).reshape(-1, 3)
+        h = self.v[None, :] - np.tile(loc, (1, self.v.size // 3))
+        hs = [h]
+        for l in range(4):
+            h = np.maximum(h @ self.P[l].T + self.P[4 + l][None, :], 0.0)
+            hs.append(h)
+        return hs
+
+    def step(self, loc, action, target):
+        loss, G = self.loss_grads(loc, action, target)
+        gn = float(np.sqrt(sum(float(np.sum(g * g)) for g in G)))
+        s = self.clip / gn if (self.clip > 0 and gn > self.clip) else 1.0
+        self.t += 1
+        lr_t = self.lr * np.sqrt(1.0 - self.b2 ** self.t) / (1.0 - self.b1 ** self.t)
+        for i, g in enumerate(G):
+            self.M[i] = self.M[i] * self.b1 + g * ((1.0 - self.b1) * s)
+            self.V[i] = self.V[i] * self.b2 + (g * g) * ((1.0 - self.b2) * s * s)
+            self.P[i] = self.P[i] - self.M[i] / (np.sqrt(self.V[i]) + self.eps) * lr_t
+        return loss, gn
+
+    def loss_grads(self, loc, action, target):
+        """loss and its gradients [dW0..dW3, db0..db3]"""
+        hs = self.forward(loc)
+        q = hs[4]
+        n = q.shape[0]
+        act = np.asarray(action, np.int64)
+        ok = (act >= 0) & (act < q.shape[1])
+        rows = np.nonzero(ok)[0]
+        qa = q[rows, act[ok]]
+        diff = np.asarray(target, np.float64)[ok] - qa
+        loss = float(np.sum(diff * diff))
+        d = np.zeros_like(q)
+        d[rows, act[ok]] = np.where(qa > 0.0, -2.0 * diff, 0.0)
+        gW, gb = [None] * 4, [None] * 4
+        for l in range(3, -1, -1):
+            gW[l] = d.T @ hs[l]
+            gb[l] = d.sum(0)
+            if l > 0:
+                d = (d @ self.P[l]) * (hs[l] > 0.0)
+        return loss, gW + gb
+
+    def params(self):
+        return self.P[:4], self.P[4:]

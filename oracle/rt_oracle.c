@@ -1436,3 +1436,36 @@ ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_para
     if (out_casts) *out_casts = total;
     return 0;
 }
+
+/* ================================================================== */
+/* Neural-Q TD targets                        */
+/* ================================================================== */
+/* compute_td_targets (GPU/deep_learning/nn_rendering_helpers.cu:91-140): target =
+ * reward + max_a(Q(s',a) cos_a) * discount (reward alone when terminal == 1); the max starts
+ * at the raw Q of action 0 and weights actions 1.. by the cosine of a jittered direction in
+ * their cell (here the Chiu map's cos with the sampler's Philox jitters: counter
+ * (pix, sample, 1 + bounce, 1 + a/2)), as rt_dqn_td_targets_device. */
+ORC_API void orc_td_targets(uint64_t seed, const float *next_q, const int32_t *terminal, const float *reward,
+                            const float *discount, const uint32_t *pix, int sample, int bounce, int n,
+                            float *target) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int b = 0; b < n; b++) {
+        if (terminal[b] == 1) { target[b] = reward[b]; continue; }
+        const float *q = next_q + (size_t)b * 144;
+        float best = q[0];
+        for (int a2 = 0; a2 < 144; a2 += 2) {
+            uint32_t ctr[4] = {pix[b], (uint32_t)sample, 1u + (uint32_t)bounce, 1u + (uint32_t)(a2 >> 1)};
+            uint32_t o[4];
+            orc_philox4x32_10(ctr, key, o);
+            for (int h = 0; h < 2; h++) {
+                int a = a2 + h;
+                if (a == 0) continue;
+                int gxi = a / 12, gyi = a - gxi * 12;
+                float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
+                float t = q[a] * c;
+                if (best < t) best = t;
+            }
+        }
+        target[b] = reward[b] + best * discount[b];
+    }
+}

@@ -44,6 +44,8 @@ EXPORTS = (
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
     "rt_sarsa_save_selected", "rt_dqn_save_selected",
+    "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
+    "rt_dqn_td_targets_device",
 )
 
 
@@ -105,6 +107,12 @@ def _declare(lib):
         "rt_dqn_create": (i, [_P, _FP, i, _IP, i, ctypes.POINTER(_FP), ctypes.POINTER(_FP),
                               ctypes.POINTER(_P)]),
         "rt_dqn_destroy": (i, [_P]),
+        "rt_dqn_trainer_create": (i, [_P, _FP, i, _IP, i, ctypes.POINTER(_FP), ctypes.POINTER(_FP), f,
+                                      ctypes.POINTER(_P)]),
+        "rt_dqn_trainer_destroy": (i, [_P]),
+        "rt_dqn_trainer_params": (i, [_P, ctypes.POINTER(_FP), ctypes.POINTER(_FP)]),
+        "rt_dqn_train_step_device": (i, [_P, _P, _P, _P, _P, i, _FP, _FP, _P]),
+        "rt_dqn_td_targets_device": (i, [_P, ctypes.c_uint64, _P, _P, _P, _P, _P, i, i, i, _P, _P]),
         "rt_dqn_forward": (i, [_P, _P, _FP, i, _FP]),
         "rt_dqn_forward_device": (i, [_P, _P, _P, i, _P, _P]),
         "rt_dqn_sample": (i, [_P, _P, ctypes.c_uint64, _FP, _FP, _IP, _UP, i, i, i, _FP, _FP, _IP]),

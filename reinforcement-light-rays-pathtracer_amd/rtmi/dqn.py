@@ -6,6 +6,8 @@
                           reference does not ship (archway: 918 inputs)
   Dqn(ctx, nn_vertices, weights)   device network (rt_dqn_create)
   forward / sample / render / render_tiles_device
+  DqnTrainer(ctx, nn_vertices, weights)   Neural-Q training (rt_dqn_trainer_*): TD targets,
+                          one Adam step per batch, parameters out for a new Dqn
 """
 from __future__ import annotations
 
@@ -151,3 +153,68 @@ def render_tiles_device(ctx: Context, scene: Scene, dqn: Dqn, cam, params, tiles
                                            ctypes.byref(params), _ip(t), t.shape[0], tile_size,
                                            ctypes.c_void_p(out_ptr), ctypes.c_void_p(casts_ptr),
                                            ctypes.c_void_p(stream)))
+
+
+class DqnTrainer:
+    """The Neural-Q learning rule (neural_q_pathtracer.cu:420-513) on the device: fp32
+    parameters + DyNet-default Adam (rt_dqn_trainer_create).  Batches are device pointers
+    (e.g. torch tensors' data_ptr())."""
+
+    def __init__(self, ctx: Context, nn_vertices: np.ndarray, W: Sequence[np.ndarray],
+                 b: Sequence[np.ndarray], learning_rate: float = 1e-3):
+        self.ctx = ctx
+        self.nn_vertices = np.ascontiguousarray(nn_vertices, np.float32).ravel()
+        W = [np.ascontiguousarray(w, np.float32) for w in W]
+        b = [np.ascontiguousarray(x, np.float32).ravel() for x in b]
+        self.shapes = [w.shape for w in W]
+        hidden = np.array([w.shape[0] for w in W[:3]], np.int32)
+        Wp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(w) for w in W])
+        bp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(x) for x in b])
+        self._h = ctypes.c_void_p()
+        check(lib().rt_dqn_trainer_create(ctx.handle, _fp(self.nn_vertices), int(W[0].shape[1]), _ip(hidden),
+                                          int(W[3].shape[0]), Wp, bp, float(learning_rate),
+                                          ctypes.byref(self._h)))
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_dqn_trainer_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step_device(self, loc_ptr: int, action_ptr: int, target_ptr: int, n: int,
+                    stream: int = 0) -> Tuple[float, float]:
+        """One Adam step; returns (loss, gradient L2 norm before clipping)."""
+        loss, gn = ctypes.c_float(0.0), ctypes.c_float(0.0)
+        check(lib().rt_dqn_train_step_device(self.ctx.handle, self._h, ctypes.c_void_p(loc_ptr),
+                                             ctypes.c_void_p(action_ptr), ctypes.c_void_p(target_ptr), n,
+                                             ctypes.byref(loss), ctypes.byref(gn), ctypes.c_void_p(stream)))
+        return float(loss.value), float(gn.value)
+
+    def params(self) -> Tuple[list, list]:
+        W = [np.zeros(s, np.float32) for s in self.shapes]
+        b = [np.zeros(s[0], np.float32) for s in self.shapes]
+        Wp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(w) for w in W])
+        bp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(x) for x in b])
+        check(lib().rt_dqn_trainer_params(self._h, Wp, bp))
+        return W, b
+
+
+def td_targets_device(ctx: Context, seed: int, next_q_ptr: int, terminal_ptr: int, reward_ptr: int,
+                      discount_ptr: int, pix_ptr: int, sample: int, bounce: int, n: int, target_ptr: int,
+                      stream: int = 0) -> None:
+    """compute_td_targets (rt_dqn_td_targets_device) on device buffers."""
+    v = ctypes.c_void_p
+    check(lib().rt_dqn_td_targets_device(ctx.handle, seed, v(next_q_ptr), v(terminal_ptr), v(reward_ptr),
+                                         v(discount_ptr), v(pix_ptr), sample, bounce, n, v(target_ptr),
+                                         v(stream)))

@@ -202,3 +202,157 @@ def test_dqn_selected_volume_dump(rtmi_mod, oracle_mod, gpu_ctx, tmp_path):
     ref = qf / qf.sum(axis=1, keepdims=True)
     assert np.abs(dist - ref).mean() <= 1e-2 * np.abs(ref).mean()
     assert np.all(np.abs(dist.sum(axis=1) - 1) < 1e-4)
+
+
+# --- Neural-Q training -------------------------------
+
+def _tiny_net(rng, n_in=12, hidden=(7, 9, 6), n_out=144):
+    dims = [n_in, *hidden, n_out]
+    W = [rng.standard_normal((dims[i + 1], dims[i])) * np.sqrt(2.0 / dims[i]) for i in range(4)]
+    b = [np.full(dims[i + 1], 0.1) for i in range(4)]
+    return W, b
+
+
+def test_train_ref_gradients_match_finite_differences(oracle_mod):
+    """The fp64 learning-rule restatement's backward pass against central differences."""
+    rng = np.random.default_rng(5)
+    W, b = _tiny_net(rng)
+    ref = oracle_mod.AdamRef(rng.standard_normal(12), W, b)
+    loc = rng.uniform(-1, 1, (9, 3))
+    act = rng.integers(0, 144, 9)
+    act[3] = -1  # ignored row
+    tgt = rng.uniform(0, 2, 9)
+    loss, G = ref.loss_grads(loc, act, tgt)
+    h = 1e-6
+    for i in range(8):
+        P = ref.P[i]
+        for idx in [tuple(rng.integers(0, s) for s in P.shape) for _ in range(6)]:
+            old = P[idx]
+            P[idx] = old + h
+            lp, _ = ref.loss_grads(loc, act, tgt)
+            P[idx] = old - h
+            lm, _ = ref.loss_grads(loc, act, tgt)
+            P[idx] = old
+            fd = (lp - lm) / (2 * h)
+            assert abs(fd - G[i][idx]) <= 1e-5 * max(1.0, abs(fd)), (i, idx, fd, G[i][idx])
+
+
+def test_train_ref_adam_reduces_loss_and_clips(oracle_mod):
+    rng = np.random.default_rng(6)
+    W, b = _tiny_net(rng)
+    ref = oracle_mod.AdamRef(rng.standard_normal(12), W, b, lr=1e-2)
+    loc = rng.uniform(-1, 1, (32, 3))
+    act = rng.integers(0, 144, 32)
+    tgt = rng.uniform(0, 3, 32)
+    losses = [ref.step(loc, act, tgt)[0] for _ in range(30)]
+    assert losses[-1] < 0.5 * losses[0]
+    # clipping: the first Adam step moves every parameter by at most lr (|m/sqrt(v)| <= 1)
+    ref2 = oracle_mod.AdamRef(rng.standard_normal(12), W, b, lr=1e-3)
+    P0 = [p.copy() for p in ref2.P]
+    ref2.step(loc, act, tgt * 100.0)
+    assert max(float(np.max(np.abs(p - q))) for p, q in zip(ref2.P, P0)) <= 1e-3 * (1 + 1e-9)
+
+
+def test_td_targets_oracle_rule(oracle_mod):
+    """compute_td_targets: terminal rows take the reward; action 0 enters the max unweighted;
+    cosines lie in (0, 1]."""
+    rng = np.random.default_rng(7)
+    n = 64
+    q = rng.uniform(0, 1, (n, 144)).astype(np.float32)
+    q[:8, 0] = 10.0  # action 0 dominates (no cosine)
+    term = (np.arange(n) % 5 == 4).astype(np.int32)
+    rw = rng.uniform(0, 1, n).astype(np.float32)
+    dc = rng.uniform(0.2, 1, n).astype(np.float32)
+    pix = rng.integers(0, 1 << 20, n).astype(np.uint32)
+    t = oracle_mod.td_targets(1984, q, term, rw, dc, pix, 3, 2)
+    assert np.array_equal(t[term == 1], rw[term == 1])
+    live = (term == 0)
+    ub = rw + np.maximum(q[:, 0], q[:, 1:].max(1)) * dc
+    assert np.all(t[live] <= ub[live] + 1e-6)
+    first = np.arange(n) < 8
+    assert np.allclose(t[first & live], (rw + np.float32(10.0) * dc)[first & live])
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+@pytest.mark.gpu
+def test_train_step_matches_fp64_restatement(rtmi_mod, oracle_mod, gpu_ctx):
+    """Three Adam steps of the device learning rule on the trained door_room network
+    (342 -> 200 -> 300 -> 200 -> 144), 777 rays (ragged), against the fp64 restatement:
+    loss and gradient norm within 1e-4 relative; parameter updates within 1% of the
+    learning rate on all but 0.1% of the parameters (Adam's first steps are ~sign(g) * lr,
+    so a gradient that is rounding noise in one of the two may flip), never more than
+    2 lr per step."""
+    import torch
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+    W, b = trained(rtmi_mod)
+    pts, _ = room_points(g, 777, 11)
+    rng = np.random.default_rng(12)
+    act = rng.integers(0, 144, 777).astype(np.int32)
+    act[::97] = -1
+    tgt = rng.uniform(0.0, 2.0, 777).astype(np.float32)
+    lr = 1e-3
+    ref = oracle_mod.AdamRef(g.nn_vertices, W, b, lr=lr)
+    P0 = [p.copy() for p in ref.P]
+    d_loc, d_act, d_tgt = _dev(pts), _dev(act), _dev(tgt)
+    with rtmi_mod.dqn.DqnTrainer(gpu_ctx, g.nn_vertices, W, b, learning_rate=lr) as tr:
+        for _ in range(3):
+            loss, gn = tr.step_device(d_loc.data_ptr(), d_act.data_ptr(), d_tgt.data_ptr(), 777)
+            rl, rg = ref.step(pts, act, tgt)
+            assert abs(loss - rl) <= 1e-4 * rl, (loss, rl)
+            assert abs(gn - rg) <= 1e-4 * rg, (gn, rg)
+        torch.cuda.synchronize()
+        Wg, bg = tr.params()
+    got = Wg + bg
+    n_par = sum(p.size for p in got)
+    bad = 0
+    for p_gpu, p_ref, p0 in zip(got, ref.P, P0):
+        dg = p_gpu.astype(np.float64) - p0
+        dr = p_ref - p0
+        diff = np.abs(dg - dr)
+        assert diff.max() <= 2 * 3 * lr * (1 + 1e-3)
+        bad += int(np.count_nonzero(diff > 1e-2 * lr))
+    assert bad <= 1e-3 * n_par, (bad, n_par)
+
+
+@pytest.mark.gpu
+def test_train_steps_reduce_loss_and_feed_inference(rtmi_mod, gpu_ctx):
+    """Repeated steps on one batch drive its loss down; the trained parameters build an
+    inference network (rt_dqn_create) whose Q moves toward the targets."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    pts, _ = room_points(g, 1024, 13)
+    rng = np.random.default_rng(14)
+    act = rng.integers(0, 144, 1024).astype(np.int32)
+    tgt = rng.uniform(0.5, 1.5, 1024).astype(np.float32)
+    d_loc, d_act, d_tgt = _dev(pts), _dev(act), _dev(tgt)
+    with rtmi_mod.dqn.DqnTrainer(gpu_ctx, g.nn_vertices, W, b, learning_rate=1e-3) as tr:
+        losses = [tr.step_device(d_loc.data_ptr(), d_act.data_ptr(), d_tgt.data_ptr(), 1024)[0]
+                  for _ in range(40)]
+        W2, b2 = tr.params()
+    assert all(np.isfinite(losses)) and losses[-1] < 0.5 * losses[0], losses[::8]
+    with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W2, b2) as net:
+        q = net.forward(pts)
+    err = np.mean((q[np.arange(1024), act] - tgt) ** 2)
+    assert err * 1024 < 0.6 * losses[0], (err * 1024, losses[0])
+
+
+@pytest.mark.gpu
+def test_td_targets_bit_exact(rtmi_mod, oracle_mod, gpu_ctx):
+    import torch
+    rng = np.random.default_rng(15)
+    n = 1000
+    q = rng.uniform(0, 1, (n, 144)).astype(np.float32)
+    term = (rng.random(n) < 0.2).astype(np.int32)
+    rw = rng.uniform(0, 1, n).astype(np.float32)
+    dc = rng.uniform(0.2, 1, n).astype(np.float32)
+    pix = rng.integers(0, 1 << 22, n).astype(np.uint32)
+    out = torch.zeros(n, dtype=torch.float32, device="cuda")
+    bufs = [_dev(x) for x in (q, term, rw, dc, pix.view(np.int32))]  # kept alive over the launch
+    rtmi_mod.dqn.td_targets_device(gpu_ctx, 1984, *[t.data_ptr() for t in bufs], 5, 3, n, out.data_ptr())
+    torch.cuda.synchronize()
+    want = oracle_mod.td_targets(1984, q, term, rw, dc, pix, 5, 3)
+    assert np.array_equal(out.cpu().numpy(), want)
