@@ -62,19 +62,24 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const float* 
     __shared__ float Bs[kTK][kT + 4];
     const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
     const int m0 = blockIdx.y * kT, n0 = blockIdx.x * kT;
+    // split K (gridDim.z > 1, EPI 0 only): slice z covers [z kc, (z + 1) kc) and writes the
+    // partial product to C + z M ldc; k_sum_slices adds the slices in order
+    const int kc = (K + (int)gridDim.z - 1) / (int)gridDim.z;
+    const int kb = (int)blockIdx.z * kc, ke = min(K, kb + kc);
+    C += (size_t)blockIdx.z * M * ldc;
     float acc[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = 0.0f;
-    for (int k0 = 0; k0 < K; k0 += kTK) {
+    for (int k0 = kb; k0 < ke; k0 += kTK) {
         // tiles staged with the stored matrix's contiguous index fastest (coalesced)
         for (int e = threadIdx.x; e < kT * kTK; e += 256) {
             const int mm = TA ? (e % kT) : (e / kTK);
             const int kk = TA ? (e / kT) : (e % kTK);
             const int gm = m0 + mm, gk = k0 + kk;
             float v = 0.0f;
-            if (gm < M && gk < K) v = TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
+            if (gm < M && gk < ke) v = TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
             As[kk][mm] = v;
         }
         for (int e = threadIdx.x; e < kT * kTK; e += 256) {
@@ -82,7 +87,7 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const float* 
             const int kk = TB ? (e % kTK) : (e / kT);
             const int gn = n0 + nn, gk = k0 + kk;
             float v = 0.0f;
-            if (gn < N && gk < K) v = TB ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
+            if (gn < N && gk < ke) v = TB ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
             Bs[kk][nn] = v;
         }
         __syncthreads();
@@ -157,14 +162,26 @@ __global__ __launch_bounds__(256) void k_loss_grad(const float* __restrict__ q, 
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
 }
 
-// bias gradient: column sums of the layer's output gradient, rows in order
-__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ d, int n, int cols,
-                                                float* __restrict__ out) {
+// bias gradient: column sums of the layer's output gradient.  Stage 1: chunk y of the
+// rows (in order) per column -> part[y][c]; stage 2 (k_sum_slices): the chunks in order.
+__global__ __launch_bounds__(256) void k_colsum(const float* __restrict__ d, int n, int cols, int rows_per,
+                                                float* __restrict__ part) {
     const int c = blockIdx.x * 256 + threadIdx.x;
     if (c >= cols) return;
+    const int r0 = blockIdx.y * rows_per, r1 = min(n, r0 + rows_per);
     float s = 0.0f;
-    for (int b = 0; b < n; ++b) s += d[(size_t)b * cols + c];
-    out[c] = s;
+    for (int b = r0; b < r1; ++b) s += d[(size_t)b * cols + c];
+    part[(size_t)blockIdx.y * cols + c] = s;
+}
+
+// out[i] = sum_z slices[z][i], z in order (split-K and column-sum partials)
+__global__ __launch_bounds__(256) void k_sum_slices(const float* __restrict__ slices, int n_slices, size_t len,
+                                                    float* __restrict__ out) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= len) return;
+    float s = slices[i];
+    for (int z = 1; z < n_slices; ++z) s += slices[(size_t)z * len + i];
+    out[i] = s;
 }
 
 // per-block partial sums of squares of the flat gradient (grid-stride, fixed order)
@@ -262,8 +279,8 @@ unsigned blocks_for(size_t n) { return (unsigned)((n + 255) / 256); }
 
 template <int TA, int TB, int EPI>
 hipError_t gemm(hipStream_t st, int M, int N, int K, const float* A, int lda, const float* B, int ldb, float* C,
-                int ldc, const float* bias = nullptr, const float* mask = nullptr, int ldm = 0) {
-    const dim3 grid((unsigned)((N + kT - 1) / kT), (unsigned)((M + kT - 1) / kT));
+                int ldc, const float* bias = nullptr, const float* mask = nullptr, int ldm = 0, int split = 1) {
+    const dim3 grid((unsigned)((N + kT - 1) / kT), (unsigned)((M + kT - 1) / kT), (unsigned)split);
     hipLaunchKernelGGL((k_gemm<TA, TB, EPI>), grid, dim3(256), 0, st, M, N, K, A, lda, B, ldb, C, ldc, bias, mask,
                        ldm);
     return hipGetLastError();
@@ -283,9 +300,12 @@ struct rt_dqn_trainer {
     int cap = 0;
     float *X = nullptr, *H[4] = {nullptr, nullptr, nullptr, nullptr}, *D[2] = {nullptr, nullptr};
     float *part_loss = nullptr, *part_g = nullptr, *scal = nullptr;
+    float* slices = nullptr;  // split-K partial products of the weight gradients
+    size_t slice_cap = 0;
     void free_ws() {
-        for (float* p : {X, H[0], H[1], H[2], H[3], D[0], D[1], part_loss}) (void)hipFree(p);
-        X = D[0] = D[1] = part_loss = nullptr;
+        for (float* p : {X, H[0], H[1], H[2], H[3], D[0], D[1], part_loss, slices}) (void)hipFree(p);
+        X = D[0] = D[1] = part_loss = slices = nullptr;
+        slice_cap = 0;
         for (auto& h : H) h = nullptr;
         cap = 0;
     }
@@ -298,6 +318,17 @@ struct rt_dqn_trainer {
 
 namespace {
 
+constexpr int kColChunks = 256;  // row chunks of the bias-gradient column sums
+
+// K slices of a weight-gradient GEMM (M x N tiles over a batch of K rays): enough
+// workgroups to fill the 256 CUs, slices of at least 256 rays
+int split_for(int M, int N, int K) {
+    const int tiles = ((M + kT - 1) / kT) * ((N + kT - 1) / kT);
+    int s = (1024 + tiles - 1) / tiles;
+    s = std::min(s, std::max(1, K / 256));
+    return std::max(1, std::min(s, 64));
+}
+
 int ensure_ws(rt_dqn_trainer* t, int n) {
     if (n <= t->cap) return RT_OK;
     t->free_ws();
@@ -308,6 +339,14 @@ int ensure_ws(rt_dqn_trainer* t, int n) {
     for (int l = 0; l < 4; ++l) RT_HIPE(hipMalloc(&t->H[l], sizeof(float) * (size_t)cap * t->dims[l + 1]));
     for (int k = 0; k < 2; ++k) RT_HIPE(hipMalloc(&t->D[k], sizeof(float) * (size_t)cap * widest));
     RT_HIPE(hipMalloc(&t->part_loss, sizeof(float) * (size_t)(cap / 256)));
+    size_t sl = 0;
+    for (int l = 0; l < 4; ++l) {
+        const int s = split_for(t->dims[l + 1], t->dims[l], cap);
+        sl = std::max(sl, (size_t)s * t->dims[l + 1] * t->dims[l]);
+        sl = std::max(sl, (size_t)kColChunks * t->dims[l + 1]);
+    }
+    RT_HIPE(hipMalloc(&t->slices, sizeof(float) * sl));
+    t->slice_cap = sl;
     t->cap = cap;
     return RT_OK;
 }
@@ -413,9 +452,23 @@ int rt_dqn_train_step_device(rt_ctx* ctx, rt_dqn_trainer* t, const float* d_loc,
     int cur = 0;
     for (int l = 3; l >= 0; --l) {
         const float* prev = (l == 0) ? t->X : t->H[l - 1];
-        RT_HIPE((gemm<1, 0, 0>(st, d[l + 1], d[l], n, t->D[cur], d[l + 1], prev, d[l], t->G + t->w_off[l], d[l])));
-        hipLaunchKernelGGL(k_colsum, dim3(blocks_for((size_t)d[l + 1])), dim3(256), 0, st, t->D[cur], n, d[l + 1],
-                           t->G + t->b_off[l]);
+        const int sk = split_for(d[l + 1], d[l], n);
+        const size_t wlen = (size_t)d[l + 1] * d[l];
+        if (sk == 1) {
+            RT_HIPE((gemm<1, 0, 0>(st, d[l + 1], d[l], n, t->D[cur], d[l + 1], prev, d[l], t->G + t->w_off[l], d[l])));
+        } else {
+            RT_HIPE((gemm<1, 0, 0>(st, d[l + 1], d[l], n, t->D[cur], d[l + 1], prev, d[l], t->slices, d[l], nullptr,
+                                   nullptr, 0, sk)));
+            hipLaunchKernelGGL(k_sum_slices, dim3(blocks_for(wlen)), dim3(256), 0, st, t->slices, sk, wlen,
+                               t->G + t->w_off[l]);
+            RT_HIPE(hipGetLastError());
+        }
+        const int rows_per = (n + kColChunks - 1) / kColChunks;
+        hipLaunchKernelGGL(k_colsum, dim3(blocks_for((size_t)d[l + 1]), (unsigned)kColChunks), dim3(256), 0, st,
+                           t->D[cur], n, d[l + 1], rows_per, t->slices);
+        RT_HIPE(hipGetLastError());
+        hipLaunchKernelGGL(k_sum_slices, dim3(blocks_for((size_t)d[l + 1])), dim3(256), 0, st, t->slices,
+                           kColChunks, (size_t)d[l + 1], t->G + t->b_off[l]);
         RT_HIPE(hipGetLastError());
         if (l > 0) {
             RT_HIPE((gemm<0, 0, 2>(st, n, d[l], d[l + 1], t->D[cur], d[l + 1], t->P + t->w_off[l], d[l],

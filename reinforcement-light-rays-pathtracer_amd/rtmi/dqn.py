@@ -193,13 +193,15 @@ class DqnTrainer:
             pass
 
     def step_device(self, loc_ptr: int, action_ptr: int, target_ptr: int, n: int,
-                    stream: int = 0) -> Tuple[float, float]:
-        """One Adam step; returns (loss, gradient L2 norm before clipping)."""
+                    stream: int = 0, sync: bool = True) -> Optional[Tuple[float, float]]:
+        """One Adam step; returns (loss, gradient L2 norm before clipping), which waits for
+        the stream; sync=False leaves the step in flight and returns None."""
         loss, gn = ctypes.c_float(0.0), ctypes.c_float(0.0)
         check(lib().rt_dqn_train_step_device(self.ctx.handle, self._h, ctypes.c_void_p(loc_ptr),
                                              ctypes.c_void_p(action_ptr), ctypes.c_void_p(target_ptr), n,
-                                             ctypes.byref(loss), ctypes.byref(gn), ctypes.c_void_p(stream)))
-        return float(loss.value), float(gn.value)
+                                             ctypes.byref(loss) if sync else None,
+                                             ctypes.byref(gn) if sync else None, ctypes.c_void_p(stream)))
+        return (float(loss.value), float(gn.value)) if sync else None
 
     def params(self) -> Tuple[list, list]:
         W = [np.zeros(s, np.float32) for s in self.shapes]
