@@ -42,7 +42,7 @@ VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
 TILE = 32
 # HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
 # (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
-PMC_PROFILE = os.path.join("profiles", "r1v7_pmc.json")
+PMC_PROFILE = os.path.join("profiles", "r1v8_pmc.json")
 DEFAULT_WORKLOAD = (512, 512, 256, 64)
 
 
@@ -75,7 +75,7 @@ def pmc_traffic(params):
     return None, None
 
 
-SQ_PROFILE = os.path.join("profiles", "r1v7_sq_summary.json")
+SQ_PROFILE = os.path.join("profiles", "r1v8_sq_summary.json")
 
 
 def pmc_valu_issue(params):

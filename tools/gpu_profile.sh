@@ -23,3 +23,5 @@ step sq 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES G
 step kt_sarsa 300 rocprofv3 --kernel-trace --stats -d $out/kt_sarsa -o kt_sarsa --output-format csv -- python3 tools/bench_sarsa.py --frames 2
 step kt_dqn 300 rocprofv3 --kernel-trace --stats -d $out/kt_dqn -o kt_dqn --output-format csv -- python3 tools/bench_dqn.py --scene archway --width 512 --spp 16 --steps 1
 step fetch_dqn 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $out/fetch_dqn -o fetch_dqn --output-format csv -- python3 tools/bench_dqn.py --scene archway --width 256 --spp 1 --steps 1
+# Neural-Q training step
+step kt_train 300 rocprofv3 --kernel-trace --stats -d $out/kt_train -o kt_train --output-format csv -- python3 tools/bench_train.py --batch 4096 --steps 10
