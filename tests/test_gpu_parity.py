@@ -141,6 +141,12 @@ RENDER_CASES = [
     # the bench's chunking (32 lanes per pixel) on an image that is no multiple of 16
     ("cornell_cpu", 0, dict(width=37, height=23, spp=64, spp_split=32), None),
     ("cornell_gpu", 1, dict(width=21, height=19, spp=32, spp_split=32), None),
+    # GPU preset: sample stealing (k_render STEAL) with 64 / 16 / 4 lanes per pixel,
+    # clipped blocks, one sample per lane, and the fixed-chunk fallback (LDS too large)
+    ("cornell_gpu", 1, dict(width=37, height=29, spp=64, spp_split=64), None),
+    ("complex_light_room", 1, dict(width=33, height=17, spp=16, spp_split=16), None),
+    ("archway", 1, dict(width=24, height=24, spp=12, spp_split=4), (3, 5, 17, 13)),
+    ("cornell_gpu", 1, dict(width=32, height=32, spp=512, spp_split=2), None),
 ]
 
 
