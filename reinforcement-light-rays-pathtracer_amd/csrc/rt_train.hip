@@ -72,25 +72,34 @@ __global__ __launch_bounds__(256) void k_gemm(int M, int N, int K, const float* 
     for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = 0.0f;
-    for (int k0 = kb; k0 < ke; k0 += kTK) {
-        // tiles staged with the stored matrix's contiguous index fastest (coalesced)
-        for (int e = threadIdx.x; e < kT * kTK; e += 256) {
+    // tiles staged with the stored matrix's contiguous index fastest (coalesced); the
+    // next k step's elements are loaded into registers while this step computes
+    constexpr int kPer = kT * kTK / 256;  // tile elements per thread
+    float ra[kPer], rb[kPer];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = (int)threadIdx.x + 256 * u;
             const int mm = TA ? (e % kT) : (e / kTK);
             const int kk = TA ? (e / kT) : (e % kTK);
             const int gm = m0 + mm, gk = k0 + kk;
-            float v = 0.0f;
-            if (gm < M && gk < ke) v = TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk];
-            As[kk][mm] = v;
-        }
-        for (int e = threadIdx.x; e < kT * kTK; e += 256) {
+            ra[u] = (gm < M && gk < ke) ? (TA ? A[(size_t)gk * lda + gm] : A[(size_t)gm * lda + gk]) : 0.0f;
             const int nn = TB ? (e / kTK) : (e % kT);
-            const int kk = TB ? (e % kTK) : (e / kT);
-            const int gn = n0 + nn, gk = k0 + kk;
-            float v = 0.0f;
-            if (gn < N && gk < ke) v = TB ? B[(size_t)gn * ldb + gk] : B[(size_t)gk * ldb + gn];
-            Bs[kk][nn] = v;
+            const int kb2 = TB ? (e % kTK) : (e / kT);
+            const int gn = n0 + nn, gk2 = k0 + kb2;
+            rb[u] = (gn < N && gk2 < ke) ? (TB ? B[(size_t)gn * ldb + gk2] : B[(size_t)gk2 * ldb + gn]) : 0.0f;
+        }
+    };
+    if (kb < ke) load(kb);
+    for (int k0 = kb; k0 < ke; k0 += kTK) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = (int)threadIdx.x + 256 * u;
+            As[TA ? (e / kT) : (e % kTK)][TA ? (e % kT) : (e / kTK)] = ra[u];
+            Bs[TB ? (e % kTK) : (e / kT)][TB ? (e / kTK) : (e % kT)] = rb[u];
         }
         __syncthreads();
+        if (k0 + kTK < ke) load(k0 + kTK);
 #pragma unroll
         for (int kk = 0; kk < kTK; ++kk) {
             float a[4], b[4];
@@ -318,7 +327,7 @@ struct rt_dqn_trainer {
 
 namespace {
 
-constexpr int kColChunks = 256;  // row chunks of the bias-gradient column sums
+constexpr int kColChunks = 256;  // most row chunks of the bias-gradient column sums
 
 // K slices of a weight-gradient GEMM (M x N tiles over a batch of K rays): enough
 // workgroups to fill the 256 CUs, slices of at least 256 rays
@@ -463,12 +472,15 @@ int rt_dqn_train_step_device(rt_ctx* ctx, rt_dqn_trainer* t, const float* d_loc,
                                t->G + t->w_off[l]);
             RT_HIPE(hipGetLastError());
         }
-        const int rows_per = (n + kColChunks - 1) / kColChunks;
-        hipLaunchKernelGGL(k_colsum, dim3(blocks_for((size_t)d[l + 1]), (unsigned)kColChunks), dim3(256), 0, st,
+        // chunks of >= 64 rows, at most kColChunks of them (measured: 4096 rays -> 64 chunks,
+        // 65536 rays -> 256 chunks balance the two stages)
+        const int rows_per = std::max(64, (n + kColChunks - 1) / kColChunks);
+        const int chunks = (n + rows_per - 1) / rows_per;
+        hipLaunchKernelGGL(k_colsum, dim3(blocks_for((size_t)d[l + 1]), (unsigned)chunks), dim3(256), 0, st,
                            t->D[cur], n, d[l + 1], rows_per, t->slices);
         RT_HIPE(hipGetLastError());
         hipLaunchKernelGGL(k_sum_slices, dim3(blocks_for((size_t)d[l + 1])), dim3(256), 0, st, t->slices,
-                           kColChunks, (size_t)d[l + 1], t->G + t->b_off[l]);
+                           chunks, (size_t)d[l + 1], t->G + t->b_off[l]);
         RT_HIPE(hipGetLastError());
         if (l > 0) {
             RT_HIPE((gemm<0, 0, 2>(st, n, d[l], d[l + 1], t->D[cur], d[l + 1], t->P + t->w_off[l], d[l],
