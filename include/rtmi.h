@@ -300,6 +300,9 @@ int rt_pack_argb(const float* rgb, int n, uint32_t* out_argb);
 
 /* SDLScreen::SDL_SaveImage replacement: 32-bit BMP of an ARGB buffer (headless). */
 int rt_save_bmp(const char* path, const uint32_t* argb, int width, int height);
+/* The same frame as an 8-bit RGB PNG (the thesis images, Images/<scene>/reference.png;
+ * SURVEY.md §8(f) item 4); stored deflate blocks, no compression. */
+int rt_save_png(const char* path, const uint32_t* argb, int width, int height);
 
 #ifdef __cplusplus
 }

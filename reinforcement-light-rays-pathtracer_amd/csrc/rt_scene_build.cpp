@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -375,6 +376,93 @@ int rt_save_bmp(const char* path, const uint32_t* argb, int width, int height) {
     int ok = fwrite(h, 1, 54, f) == 54;
     for (int y = 0; ok && y < height; ++y)  // little-endian ARGB = B,G,R,A bytes
         ok = fwrite(argb + (size_t)y * width, 4, (size_t)width, f) == (size_t)width;
+    ok = (fclose(f) == 0) && ok;
+    return ok ? RT_OK : rt::set_error(RT_E_IO, "write failed");
+}
+
+// 8-bit RGB PNG of the frame buffer (the thesis images are
+// PNGs, Images/*/reference.png).  No zlib in the image: the IDAT stream is zlib with
+// stored (uncompressed) deflate blocks of <= 65535 bytes, filter type 0 per row,
+// CRC-32 per chunk and Adler-32 over the raw rows.  RGB from the ARGB packing of
+// PutPixelSDL (alpha dropped).
+int rt_save_png(const char* path, const uint32_t* argb, int width, int height) {
+    if (!path || !argb || width <= 0 || height <= 0 || width > (1 << 24) || height > (1 << 24))
+        return rt::set_error(RT_E_INVALID, "bad argument");
+    static uint32_t crc_tab[256];
+    static bool crc_init = false;
+    if (!crc_init) {
+        for (uint32_t n = 0; n < 256; ++n) {
+            uint32_t c = n;
+            for (int k = 0; k < 8; ++k) c = (c & 1u) ? 0xedb88320u ^ (c >> 1) : c >> 1;
+            crc_tab[n] = c;
+        }
+        crc_init = true;
+    }
+    auto crc = [&](uint32_t c, const unsigned char* b, size_t n) {
+        for (size_t i = 0; i < n; ++i) c = crc_tab[(c ^ b[i]) & 0xffu] ^ (c >> 8);
+        return c;
+    };
+    const size_t row = (size_t)width * 3 + 1;
+    std::vector<unsigned char> raw(row * (size_t)height);
+    for (int y = 0; y < height; ++y) {
+        unsigned char* r = raw.data() + (size_t)y * row;
+        r[0] = 0;  // filter: none
+        for (int x = 0; x < width; ++x) {
+            const uint32_t v = argb[(size_t)y * width + x];
+            r[1 + 3 * x] = (unsigned char)(v >> 16);
+            r[2 + 3 * x] = (unsigned char)(v >> 8);
+            r[3 + 3 * x] = (unsigned char)v;
+        }
+    }
+    std::vector<unsigned char> z;
+    z.reserve(raw.size() + raw.size() / 65535 * 5 + 16);
+    z.push_back(0x78);
+    z.push_back(0x01);
+    uint32_t a1 = 1, a2 = 0;
+    for (size_t off = 0; off < raw.size() || off == 0; ) {
+        const size_t n = std::min<size_t>(65535, raw.size() - off);
+        const bool last = off + n >= raw.size();
+        z.push_back(last ? 1 : 0);
+        z.push_back((unsigned char)n);
+        z.push_back((unsigned char)(n >> 8));
+        z.push_back((unsigned char)~n);
+        z.push_back((unsigned char)(~n >> 8));
+        z.insert(z.end(), raw.begin() + off, raw.begin() + off + n);
+        for (size_t i = off; i < off + n; ++i) {
+            a1 = (a1 + raw[i]) % 65521u;
+            a2 = (a2 + a1) % 65521u;
+        }
+        off += n;
+        if (last) break;
+    }
+    const uint32_t adler = (a2 << 16) | a1;
+    for (int k = 3; k >= 0; --k) z.push_back((unsigned char)(adler >> (8 * k)));
+    FILE* f = fopen(path, "wb");
+    if (!f) return rt::set_error(RT_E_IO, "cannot open output file");
+    bool ok = true;
+    auto put32 = [&](unsigned char* b, uint32_t v) {
+        b[0] = (unsigned char)(v >> 24); b[1] = (unsigned char)(v >> 16);
+        b[2] = (unsigned char)(v >> 8); b[3] = (unsigned char)v;
+    };
+    auto chunk = [&](const char* type, const unsigned char* data, size_t n) {
+        unsigned char hd[8];
+        put32(hd, (uint32_t)n);
+        memcpy(hd + 4, type, 4);
+        uint32_t c = crc(0xffffffffu, hd + 4, 4);
+        c = crc(c, data, n) ^ 0xffffffffu;
+        unsigned char tl[4];
+        put32(tl, c);
+        ok = ok && fwrite(hd, 1, 8, f) == 8 && (n == 0 || fwrite(data, 1, n, f) == n) && fwrite(tl, 1, 4, f) == 4;
+    };
+    static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    ok = fwrite(sig, 1, 8, f) == 8;
+    unsigned char ihdr[13];
+    put32(ihdr, (uint32_t)width);
+    put32(ihdr + 4, (uint32_t)height);
+    ihdr[8] = 8; ihdr[9] = 2; ihdr[10] = 0; ihdr[11] = 0; ihdr[12] = 0;  // 8-bit RGB
+    chunk("IHDR", ihdr, 13);
+    chunk("IDAT", z.data(), z.size());
+    chunk("IEND", nullptr, 0);
     ok = (fclose(f) == 0) && ok;
     return ok ? RT_OK : rt::set_error(RT_E_IO, "write failed");
 }

@@ -36,7 +36,7 @@ EXPORTS = (
     "rt_cornell_counts", "rt_cornell_geometry", "rt_obj_geometry",
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
     "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
-    "rt_pack_argb", "rt_save_bmp", "rt_selftest",
+    "rt_pack_argb", "rt_save_bmp", "rt_save_png", "rt_selftest",
     "rt_dynet_read", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
@@ -101,6 +101,7 @@ def _declare(lib):
                                        _IP, i, i, _P, _P, _P]),
         "rt_pack_argb": (i, [_FP, i, _UP]),
         "rt_save_bmp": (i, [ctypes.c_char_p, _UP, i, i]),
+        "rt_save_png": (i, [ctypes.c_char_p, _UP, i, i]),
         "rt_selftest": (i, [_P, i, _U64P]),
         "rt_dynet_read": (i, [ctypes.c_char_p, i, _IP, _IP, _FP, ctypes.POINTER(i),
                               ctypes.POINTER(ctypes.c_int64)]),

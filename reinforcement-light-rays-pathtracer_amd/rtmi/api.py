@@ -238,3 +238,10 @@ def save_bmp(path: str, argb: np.ndarray) -> None:
     a = np.ascontiguousarray(argb, np.uint32)
     h, w = a.shape
     check(lib().rt_save_bmp(path.encode(), a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), w, h))
+
+
+def save_png(path: str, argb: np.ndarray) -> None:
+    """8-bit RGB PNG of an ARGB frame buffer (rt_save_png)."""
+    a = np.ascontiguousarray(argb, np.uint32)
+    h, w = a.shape
+    check(lib().rt_save_png(path.encode(), a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), w, h))

@@ -73,3 +73,40 @@ def test_save_bmp(rtmi_mod, tmp_path):
 def test_obj_models_present():
     for k in ("door_room", "archway", "complex_light_room"):
         assert os.path.exists(os.path.join(MODELS, f"{k}.obj"))
+
+
+def test_png_writer_round_trip(rtmi_mod, tmp_path):
+    """rt_save_png (stored deflate) decodes to the packed RGB; BMP and PNG agree; the
+    MAPE CLI (Graphing/mape.py) reads both."""
+    from PIL import Image
+    rng = np.random.default_rng(3)
+    for h, w in [(1, 1), (7, 13), (300, 251)]:  # last: > one 64 KB deflate block
+        rgb = rng.random((h, w, 3), dtype=np.float32) * 1.2
+        argb = rtmi_mod.pack_argb(rgb)
+        png, bmp = str(tmp_path / "f.png"), str(tmp_path / "f.bmp")
+        rtmi_mod.save_png(png, argb)
+        rtmi_mod.save_bmp(bmp, argb)
+        want = rtmi_mod.metrics.argb_to_rgb8(argb)
+        with Image.open(png) as im:
+            im.load()
+            assert im.mode == "RGB" and im.size == (w, h)
+            assert np.array_equal(np.asarray(im), want)
+        assert np.array_equal(rtmi_mod.metrics.read_rgb8(bmp), want)
+        assert rtmi_mod.metrics.mape_files(png, bmp) == 0.0
+    with pytest.raises(rtmi_mod.RtError):
+        rtmi_mod.save_png(str(tmp_path / "missing" / "x.png"), np.zeros((2, 2), np.uint32))
+
+
+def test_mape_cli_matches_formula(rtmi_mod, tmp_path, capsys):
+    from PIL import Image
+    rng = np.random.default_rng(4)
+    a = rng.integers(0, 256, (9, 11, 3), dtype=np.uint8)
+    b = np.clip(a.astype(int) + rng.integers(-3, 4, a.shape), 0, 255).astype(np.uint8)
+    pa, pb = str(tmp_path / "a.png"), str(tmp_path / "b.png")
+    Image.fromarray(a).save(pa)
+    Image.fromarray(b).save(pb)
+    gt, p = a.astype(np.intc), b.astype(np.intc)
+    want = round(float(np.sum(np.abs(gt / 255 - p / 255) / ((gt + 0.01) / 255)) / gt.size), 4)
+    assert rtmi_mod.metrics.main([pa, pb]) == 0
+    assert float(capsys.readouterr().out.strip()) == want
+    assert rtmi_mod.metrics.main([pa]) == 1
