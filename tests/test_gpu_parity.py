@@ -222,3 +222,22 @@ def test_config1_gpu_vs_reference_sequential(rtmi_mod, oracle_mod, gpu_ctx):
     z = d.mean(0) / (d.std(0) / np.sqrt(d.shape[0]))
     assert np.all(np.abs(z) < 3.0), z
     assert abs(casts - ref_casts) <= 0.01 * ref_casts
+
+
+def test_gpu_preset_cornell_matches_reference_render(rtmi_mod):
+    """The reference's own GPU-engine render, Images/cornell/reference.png (720x720, 4096
+    spp; its 45x45-pixel block means kept in tests/golden/cornell_ref_stats.json by
+    tests/golden/make_goldens.py): our GPU-preset frame at 1024 spp, packed to 8 bits by
+    the PutPixelSDL rule, agrees block by block (measured: mean |d| 0.21, max 1.6 of 255)."""
+    import json
+    from conftest import GOLDEN
+    ref = np.array(json.load(open(os.path.join(GOLDEN, "cornell_ref_stats.json")))["reference.png"]["means"])
+    geom = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=1024, spp_split=16)
+    with rtmi_mod.Context(0) as ctx, rtmi_mod.Scene(ctx, geom) as sc:
+        img, _ = rtmi_mod.render(ctx, sc, rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"]), p)
+    rgb8 = rtmi_mod.metrics.argb_to_rgb8(rtmi_mod.pack_argb(img)).astype(np.float64)
+    ours = rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3))
+    d = np.abs(ours - ref)
+    assert d.mean() <= 0.5 and d.max() <= 3.0, (d.mean(), d.max())
+    assert abs(ours.mean() - ref.mean()) <= 0.002 * ref.mean()
