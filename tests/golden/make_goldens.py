@@ -91,6 +91,28 @@ def main(ref):
             json.dump(stats, f)
     except ImportError:
         pass
+    scene_image_stats(ref)
+
+
+def scene_image_stats(ref):
+    """scenes_ref_stats.json: 45x45 block means of the reference renders of the OBJ scenes
+    (Images/<scene>/reference.png, GPU engine, 720x720)."""
+    try:
+        import numpy as np
+        from PIL import Image
+    except ImportError:
+        return
+    stats = {}
+    for scene in ("door_room", "archway", "complex_light"):
+        p = os.path.join(ref, "Images", scene, "reference.png")
+        a = np.asarray(Image.open(p).convert("RGB"), np.float64)
+        h, w, _ = a.shape
+        b = 45
+        blocks = a[: h // b * b, : w // b * b].reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3))
+        stats[scene] = {"file": f"Images/{scene}/reference.png", "shape": [h, w], "block": b,
+                        "means": blocks.round(4).tolist()}
+    with open(os.path.join(HERE, "scenes_ref_stats.json"), "w") as f:
+        json.dump(stats, f)
 
 
 if __name__ == "__main__":

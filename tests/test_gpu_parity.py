@@ -241,3 +241,24 @@ def test_gpu_preset_cornell_matches_reference_render(rtmi_mod):
     d = np.abs(ours - ref)
     assert d.mean() <= 0.5 and d.max() <= 3.0, (d.mean(), d.max())
     assert abs(ours.mean() - ref.mean()) <= 0.002 * ref.mean()
+
+
+@pytest.mark.parametrize("scene,key", [("archway", "archway"), ("complex_light_room", "complex_light")])
+def test_gpu_preset_obj_scene_matches_reference_render(rtmi_mod, scene, key):
+    """Images/<scene>/reference.png of the reference (GPU engine, 720x720; block means in
+    tests/golden/scenes_ref_stats.json) against our GPU-preset frame at 512 spp
+    (measured at 256 spp: archway mean |d| 0.52, complex_light_room 0.39 of 255).
+    door_room's reference.png was rendered with a scene variant the repository does not
+    pin (ours is 57% brighter) and is not compared."""
+    import json
+    from conftest import GOLDEN
+    ref = np.array(json.load(open(os.path.join(GOLDEN, "scenes_ref_stats.json")))[key]["means"])
+    geom = rtmi_mod.obj_geometry(os.path.join(MODELS, f"{scene}.obj"), scene)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=512, spp_split=16)
+    with rtmi_mod.Context(0) as ctx, rtmi_mod.Scene(ctx, geom) as sc:
+        img, _ = rtmi_mod.render(ctx, sc, rtmi_mod.camera(rtmi_mod.CAMERAS[scene]), p)
+    rgb8 = rtmi_mod.metrics.argb_to_rgb8(rtmi_mod.pack_argb(img)).astype(np.float64)
+    ours = rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3))
+    d = np.abs(ours - ref)
+    assert d.mean() <= 0.8 and d.max() <= 8.0, (d.mean(), d.max())
+    assert abs(ours.mean() - ref.mean()) <= 0.01 * ref.mean()
