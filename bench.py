@@ -42,7 +42,7 @@ VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
 TILE = 32
 # HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
 # (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
-PMC_PROFILE = os.path.join("profiles", "r1v8_pmc.json")
+PMC_PROFILE = os.path.join("profiles", "r1v9_pmc.json")
 DEFAULT_WORKLOAD = (512, 512, 256, 64)
 
 
@@ -70,12 +70,12 @@ def pmc_traffic(params):
     except (OSError, ValueError):
         return None, None
     for name, e in prof.get("selected", {}).items():
-        if "k_render<0, 0, 0>" in name and "traffic_bytes_per_launch" in e:
+        if "k_render<0, 0, 0" in name and "traffic_bytes_per_launch" in e:
             return int(e["traffic_bytes_per_launch"]), PMC_PROFILE
     return None, None
 
 
-SQ_PROFILE = os.path.join("profiles", "r1v8_sq_summary.json")
+SQ_PROFILE = os.path.join("profiles", "r1v9_sq_summary.json")
 
 
 def pmc_valu_issue(params):
