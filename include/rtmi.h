@@ -160,6 +160,16 @@ typedef struct rt_dqn rt_dqn;
 int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols, float* values,
                   int* n_params, int64_t* n_values);
 
+/* DyNet TextFileSaver format writer (the reference saves its trained networks with
+ * dynet::TextFileSaver, GPU_Rendering_Engine/Source/deep_learning/neural_q_pathtracer.cu:193 and
+ * NN_Q_Value_Trainer/Source/main.cu:290, into Radiance_Map_Data/<name>.model):
+ * "#Parameter# /_<k> {rows,cols} <bytes> ZERO_GRAD" (vectors "{rows}") then one line of
+ * column-major "%+.8e " values; <bytes> counts that line with its newline.  values: the
+ * n_params parameters concatenated, each row-major [rows][cols] (the rt_dynet_read layout),
+ * so a write -> read round trip returns the same floats bit for bit. */
+int rt_dynet_write(const char* path, int n_params, const int32_t* rows, const int32_t* cols,
+                   const float* values);
+
 /* DQNetwork::initialize + the parameters it loads (NN_Builders/dq_network.cu:8-33,
  * fc_layer.cu:29-35): ReLU(W x + b) x 4, n_in -> hidden[0] -> hidden[1] -> hidden[2] -> n_out.
  * W[l]: row-major [out][in] fp32, b[l]: [out].  nn_vertices: Scene::vertices (n_in floats);

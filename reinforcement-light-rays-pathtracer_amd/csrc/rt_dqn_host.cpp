@@ -120,6 +120,39 @@ int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols
     return RT_OK;
 }
 
+int rt_dynet_write(const char* path, int n_params, const int32_t* rows, const int32_t* cols,
+                   const float* values) {
+    if (!path || n_params < 0 || (n_params > 0 && (!rows || !cols || !values)))
+        return err(RT_E_INVALID, "NULL argument");
+    for (int p = 0; p < n_params; ++p)
+        if (rows[p] <= 0 || cols[p] <= 0) return err(RT_E_INVALID, "bad parameter shape");
+    FILE* f = fopen(path, "w");
+    if (!f) return err(RT_E_IO, std::string("cannot open ") + path);
+    std::string line;
+    const float* src = values;
+    for (int p = 0; p < n_params && f; ++p) {
+        const int r = rows[p], c = cols[p];
+        // values line first: the header carries its byte count (newline included)
+        line.clear();
+        char num[32];
+        for (int64_t k = 0; k < (int64_t)r * c; ++k) {
+            const int64_t i = k % r, j = k / r;  // column-major, as Eigen stores it
+            snprintf(num, sizeof(num), "%+.8e ", (double)src[i * c + j]);
+            line += num;
+        }
+        line += '\n';
+        if (c == 1)
+            fprintf(f, "#Parameter# /_%d {%d} %zu ZERO_GRAD\n", p, r, line.size());
+        else
+            fprintf(f, "#Parameter# /_%d {%d,%d} %zu ZERO_GRAD\n", p, r, c, line.size());
+        fputs(line.c_str(), f);
+        src += (int64_t)r * c;
+    }
+    const bool bad = ferror(f) != 0;
+    if (fclose(f) != 0 || bad) return err(RT_E_IO, std::string("write failed: ") + path);
+    return RT_OK;
+}
+
 int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t* hidden, int n_out,
                   const float* const* W, const float* const* b, rt_dqn** out) {
     if (!ctx || !nn_vertices || !hidden || !W || !b || !out) return err(RT_E_INVALID, "NULL argument");

@@ -2,6 +2,7 @@
 
   read_dynet(path)        the reference's DyNet text models (Radiance_Map_Data/*.model),
                           via rt_dynet_read; W row-major [out][in]
+  write_dynet(path, params)   the same format out (rt_dynet_write), e.g. DqnTrainer.params()
   synthetic_weights(...)  seeded He-normal weights for scenes whose trained model the
                           reference does not ship (archway: 918 inputs)
   Dqn(ctx, nn_vertices, weights)   device network (rt_dqn_create)
@@ -42,6 +43,24 @@ def read_dynet(path: str) -> List[np.ndarray]:
         out.append(a[:, 0].copy() if c == 1 else a.copy())
         off += n
     return out
+
+
+def write_dynet(path: str, params: Sequence[np.ndarray]) -> None:
+    """DyNet TextFileSaver model (neural_q_pathtracer.cu:193) of `params` in order: matrices
+    row-major [rows][cols], vectors [rows]; read_dynet(path) returns them bit for bit."""
+    arrs = [np.ascontiguousarray(p, np.float32) for p in params]
+    for a in arrs:
+        if a.ndim not in (1, 2) or a.size == 0:
+            raise ValueError(f"DyNet parameters are non-empty vectors or matrices, got {a.shape}")
+    rows = np.array([a.shape[0] for a in arrs], np.int32)
+    cols = np.array([a.shape[1] if a.ndim == 2 else 1 for a in arrs], np.int32)
+    vals = np.concatenate([a.ravel() for a in arrs]) if arrs else np.zeros(1, np.float32)
+    check(lib().rt_dynet_write(os.fsencode(path), len(arrs), _ip(rows), _ip(cols), _fp(vals)))
+
+
+def join_layers(W: Sequence[np.ndarray], b: Sequence[np.ndarray]) -> list:
+    """([W1..W4], [b1..b4]) -> [W1, b1, ..., W4, b4] (the reference's parameter order)"""
+    return [x for pair in zip(W, b) for x in pair]
 
 
 def split_layers(params: Sequence[np.ndarray]) -> Tuple[list, list]:

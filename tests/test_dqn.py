@@ -356,3 +356,28 @@ def test_td_targets_bit_exact(rtmi_mod, oracle_mod, gpu_ctx):
     torch.cuda.synchronize()
     want = oracle_mod.td_targets(1984, q, term, rw, dc, pix, 5, 3)
     assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_dynet_writer_reproduces_reference_model(rtmi_mod, tmp_path):
+    """rt_dynet_write of the parameters read from the reference's door_room model gives the
+    reference's file back byte for byte (TextFileSaver format, neural_q_pathtracer.cu:193)."""
+    params = rtmi_mod.dqn.read_dynet(DOOR_MODEL)
+    out = tmp_path / "door_room_rewritten.model"
+    rtmi_mod.dqn.write_dynet(str(out), params)
+    assert out.read_bytes() == open(DOOR_MODEL, "rb").read()
+
+
+def test_dynet_write_read_round_trip(rtmi_mod, tmp_path):
+    """trained / synthetic weights -> DyNet text -> rt_dynet_read: bit-exact, shapes kept,
+    extreme and denormal floats included; bad shapes are refused."""
+    W, b = rtmi_mod.dqn.synthetic_weights(918, seed=7)
+    W[0][0, :4] = [np.float32(1e-40), np.float32(-3.4e38), np.float32(0.0), np.float32(-0.0)]
+    params = rtmi_mod.dqn.join_layers(W, b)
+    out = str(tmp_path / "archway.model")
+    rtmi_mod.dqn.write_dynet(out, params)
+    back = rtmi_mod.dqn.read_dynet(out)
+    assert [x.shape for x in back] == [x.shape for x in params]
+    for x, y in zip(back, params):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+    with pytest.raises(ValueError):
+        rtmi_mod.dqn.write_dynet(out, [np.zeros((2, 2, 2), np.float32)])
