@@ -319,7 +319,7 @@ def test_train_step_matches_fp64_restatement(rtmi_mod, oracle_mod, gpu_ctx):
 
 
 @pytest.mark.gpu
-def test_train_steps_reduce_loss_and_feed_inference(rtmi_mod, gpu_ctx):
+def test_train_steps_reduce_loss_and_feed_inference(rtmi_mod, gpu_ctx, tmp_path):
     """Repeated steps on one batch drive its loss down; the trained parameters build an
     inference network (rt_dqn_create) whose Q moves toward the targets."""
     g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
@@ -338,6 +338,12 @@ def test_train_steps_reduce_loss_and_feed_inference(rtmi_mod, gpu_ctx):
         q = net.forward(pts)
     err = np.mean((q[np.arange(1024), act] - tgt) ** 2)
     assert err * 1024 < 0.6 * losses[0], (err * 1024, losses[0])
+    # saved in the reference's DyNet format and loaded back: the same network, bit for bit
+    path = str(tmp_path / "archway_trained.model")
+    rtmi_mod.dqn.write_dynet(path, rtmi_mod.dqn.join_layers(W2, b2))
+    W3, b3 = rtmi_mod.dqn.split_layers(rtmi_mod.dqn.read_dynet(path))
+    with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W3, b3) as net:
+        assert np.array_equal(net.forward(pts), q)
 
 
 @pytest.mark.gpu
