@@ -127,9 +127,9 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
                 if (depth >= 2) {
                     const float4 c = shade[f_tri1 * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
                     if (SAMPLER == 0) {
-                        L.x = ((L.x * c.x) * f_cos1) / kRho;
-                        L.y = ((L.y * c.y) * f_cos1) / kRho;
-                        L.z = ((L.z * c.z) * f_cos1) / kRho;
+                        L.x = div_rho((L.x * c.x) * f_cos1);
+                        L.y = div_rho((L.y * c.y) * f_cos1);
+                        L.z = div_rho((L.z * c.z) * f_cos1);
                     } else {
                         L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
                     }
@@ -137,9 +137,9 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
                 if (depth >= 1) {
                     const float4 c = shade[f_tri0 * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
                     if (SAMPLER == 0) {
-                        L.x = ((L.x * c.x) * f_cos0) / kRho;
-                        L.y = ((L.y * c.y) * f_cos0) / kRho;
-                        L.z = ((L.z * c.z) * f_cos0) / kRho;
+                        L.x = div_rho((L.x * c.x) * f_cos0);
+                        L.y = div_rho((L.y * c.y) * f_cos0);
+                        L.z = div_rho((L.z * c.z) * f_cos0);
                     } else {
                         L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
                     }
@@ -183,9 +183,9 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
             } else {
                 if (SAMPLER == 0) {
                     const float4 c = shade[h.tri * kShadeF4 + 3];
-                    tp.x = ((tp.x * c.x) * cos_theta) / kRho;
-                    tp.y = ((tp.y * c.y) * cos_theta) / kRho;
-                    tp.z = ((tp.z * c.z) * cos_theta) / kRho;
+                    tp.x = div_rho((tp.x * c.x) * cos_theta);
+                    tp.y = div_rho((tp.y * c.y) * cos_theta);
+                    tp.z = div_rho((tp.z * c.z) * cos_theta);
                 } else {
                     const float4 c = shade[h.tri * kShadeF4 + 4];
                     tp = make3(tp.x * c.x, tp.y * c.y, tp.z * c.z);
@@ -260,6 +260,275 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
     }
 }
 
+// k_render_ps: the CPU-engine preset (PRESET 0) in two phases per wave.
+//
+// Primary rays are a known family: the camera position and the pixel rectangle of the
+// wave bound every direction, so a triangle whose filter certainly rejects all of them
+// (rect_cull, rt_trace.hpp) cannot be hit by any of them.  Phase P traces every sample's
+// primary ray of the lane against the few remaining candidates only (exact test, index
+// order: the reference's hit bit for bit) and parks the result in LDS: the direction and
+// hit of a path that continues, or the value of one that ends at its first cast.  Phase S
+// is the bounce loop of k_render without camera rays: when a path ends, the lane takes
+// its next sample's primary hit from LDS (adding the values of samples that ended at the
+// first cast on the way, in sample order) and shades it, so every trip casts a secondary
+// ray on every live lane.  The image, the ray casts and the sum order are those of
+// k_render<0, ...> (oracle/ parity); PRESET 0 paths are 1-3 casts, so about 37% of the
+// casts of the frame move from the full-scene scan to a few exact tests.
+//
+// LDS: per wave and sample slot k, five 64-lane rows (lane-contiguous: conflict-free):
+//   continuing: d.x, d.y, d.z, t, triangle;  ended: L.x, L.y, L.z, -, -1.
+constexpr int kPsFields = 5;
+constexpr int kPsMaxTri = 256;
+
+template <int SAMPLER, int RULE>
+__global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
+    extern __shared__ float s_ps[];
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    const int part = blockIdx.x & (a.split - 1);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int chunk = threadIdx.x & (a.split - 1);
+    const int lane = threadIdx.x & 63;
+    const int lx = q & 15;
+    const int ly = q >> 4;
+    const int px = blk.px0 + lx;
+    const int py = blk.py0 + ly;
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    const uint64_t vmask = __ballot(valid);
+    if (vmask == 0ull) return;  // no barrier in this kernel: a wave may leave early
+    const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+    const float4* __restrict__ shade = a.scene.shade;
+    const int n_surf = a.scene.n_surf;
+    const int n_tri = a.scene.n_tri;
+    const int pc = a.per_chunk;
+    float* const slots = s_ps + (size_t)(threadIdx.x >> 6) * pc * kPsFields * 64 + lane;
+    const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
+
+    // ---- candidate triangles of the wave's pixel rectangle ----
+    uint64_t cm[kPsMaxTri / 64];
+    {
+        int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
+        int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            x0 = min(x0, __shfl_xor(x0, off, 64));
+            x1 = max(x1, __shfl_xor(x1, off, 64));
+            y0 = min(y0, __shfl_xor(y0, off, 64));
+            y1 = max(y1, __shfl_xor(y1, off, 64));
+        }
+        CamRect c;
+        c.ox = a.cam_x; c.oy = a.cam_y; c.oz = a.cam_z;
+        const double cy = a.cos_y, sy = a.sin_y;
+        c.R[0][0] = cy;  c.R[0][1] = 0.0; c.R[0][2] = -sy;
+        c.R[1][0] = 0.0; c.R[1][1] = 1.0; c.R[1][2] = 0.0;
+        c.R[2][0] = sy;  c.R[2][1] = 0.0; c.R[2][2] = cy;
+        const double W = a.width, H = a.height;
+        const double xs[2] = {(double)x0 - 0.5 * W, (double)(x1 + 1) - 0.5 * W};
+        const double ys[2] = {(double)y0 - 0.5 * H, (double)(y1 + 1) - 0.5 * H};
+        double pm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            c.pc[k][0] = xs[k & 1];
+            c.pc[k][1] = ys[k >> 1];
+            c.pc[k][2] = H;
+            pm = fmax(pm, sqrt(xs[k & 1] * xs[k & 1] + ys[k >> 1] * ys[k >> 1] + H * H));
+        }
+        c.pmin = H;  // |p| >= p.z = H
+        c.pmax = pm * (1.0 + 0x1p-40);
+        c.delta = 0x1p-24 * (64.0 + 8.0 * (W + H) / H);
+        c.ets = (double)(kEps * a.t_scale);
+#pragma unroll
+        for (int g = 0; g < kPsMaxTri / 64; ++g) {
+            const int i = g * 64 + lane;
+            bool keep = false;
+            if (i < n_tri) keep = !rect_cull<RULE>(a.scene.filt + (size_t)i * kFiltF4, c);
+            cm[g] = __ballot(keep);
+        }
+    }
+
+    // ---- phase P: primary rays of the lane's samples ----
+    unsigned n_casts = 0;
+    const float nts = a.t_scale;
+    cfloat4* __restrict__ isect = as_const(a.scene.isect);
+    for (int k = 0; k < pc; ++k) {
+        const int s = chunk * pc + k;
+        float r1, r2;
+        draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        f3 d;
+        camera_ray<0>(a, px, py, r1, r2, &d);
+        const float nDx = -(d.x * nts), nDy = -(d.y * nts), nDz = -(d.z * nts);
+        Hit h;
+        h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+        h.tri = -1;
+#pragma unroll
+        for (int g = 0; g < kPsMaxTri / 64; ++g) {
+            uint64_t m = cm[g];
+            while (m != 0ull) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1ull;
+                exact_one_c<RULE>(isect, g * 64 + b, cam, nDx, nDy, nDz, h);
+            }
+        }
+        n_casts += valid ? 1u : 0u;
+        float v0 = d.x, v1 = d.y, v2 = d.z, v3 = h.t;
+        int code = h.tri;
+        if (h.tri < 0) {
+            v0 = v1 = v2 = 0.0f;  // PRESET 0: a miss contributes 0
+            code = -1;
+        } else if (h.tri >= n_surf) {
+            const float4 e = shade[h.tri * kShadeF4 + 3];
+            v0 = e.x; v1 = e.y; v2 = e.z;  // the light's emission, no surface bounce to fold
+            code = -1;
+        } else if (a.max_bounces == 0) {
+            v0 = v1 = v2 = 0.0f;
+            code = -1;
+        }
+        float* sl = slots + k * kPsFields * 64;
+        sl[0 * 64] = v0;
+        sl[1 * 64] = v1;
+        sl[2 * 64] = v2;
+        sl[3 * 64] = v3;
+        sl[4 * 64] = __int_as_float(code);
+    }
+
+    // ---- phase S: bounces ----
+    f3 acc = make3(0.0f, 0.0f, 0.0f);
+    int k = 0;          // next slot
+    int cur = 0;        // sample of the live path
+    int depth = 0;      // surface bounces of the live path so far
+    f3 o = cam, d = make3(0.0f, 0.0f, 1.0f);
+    Hit h;
+    h.t = 0.0f;
+    h.tri = 0;
+    int f_tri0 = 0;
+    float f_cos0 = 0.0f;
+    // next continuing sample of the lane (adding the values of the ended ones in order)
+    auto fetch = [&]() -> bool {
+        while (k < pc) {
+            const float* sl = slots + k * kPsFields * 64;
+            const int code = __float_as_int(sl[4 * 64]);
+            if (code < 0) {
+                acc.x = acc.x + sl[0 * 64];
+                acc.y = acc.y + sl[1 * 64];
+                acc.z = acc.z + sl[2 * 64];
+                ++k;
+                continue;
+            }
+            d = make3(sl[0 * 64], sl[1 * 64], sl[2 * 64]);
+            h.t = sl[3 * 64];
+            h.tri = code;
+            o = cam;
+            depth = 0;
+            cur = chunk * pc + k;
+            ++k;
+            return true;
+        }
+        return false;
+    };
+    bool live = valid && fetch();
+    for (;;) {
+        if (__ballot(live) == 0ull) break;
+        if (!live) continue;
+        // shade the live path's surface hit h (depth < max_bounces by construction)
+        const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+        const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+        const float4 N = shade[h.tri * kShadeF4 + 0];
+        const float4 T = shade[h.tri * kShadeF4 + 1];
+        const float4 B = shade[h.tri * kShadeF4 + 2];
+        float r1, r2;
+        draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+        float cos_theta, sin_theta;
+        if (SAMPLER == 0) {
+            cos_theta = r1;
+            sin_theta = sqrtf(1.0f - r1 * r1);
+        } else {
+            cos_theta = sqrtf(r1);
+            sin_theta = sqrtf(1.0f - r1);
+        }
+        float sphi, cphi;
+        sincos_turn(r2, &sphi, &cphi);
+        const float sx = sin_theta * cphi, sz = sin_theta * sphi;
+        const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
+                            (sx * B.y + cos_theta * N.y) + sz * T.y,
+                            (sx * B.z + cos_theta * N.z) + sz * T.z);
+        const int s_tri = h.tri;
+        const float s_cos = cos_theta;
+        if (depth == 0) {
+            f_tri0 = s_tri;
+            f_cos0 = s_cos;
+        }
+        o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
+        d = normalize(sd);
+        ++depth;
+
+        h = closest_hit_sel<RULE>(a.scene, 1, o, d, a.t_scale);
+        ++n_casts;
+
+        bool terminal = true;
+        f3 L = make3(0.0f, 0.0f, 0.0f);
+        if (h.tri < 0) {
+            // miss: 0
+        } else if (h.tri >= n_surf) {
+            const float4 e = shade[h.tri * kShadeF4 + 3];
+            L = make3(e.x, e.y, e.z);
+            // fold back through the surface bounces: depth 2 (this shading), then depth 1
+            if (depth >= 2) {
+                const float4 c = shade[s_tri * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
+                if (SAMPLER == 0) {
+                    L.x = div_rho((L.x * c.x) * s_cos);
+                    L.y = div_rho((L.y * c.y) * s_cos);
+                    L.z = div_rho((L.z * c.z) * s_cos);
+                } else {
+                    L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
+                }
+            }
+            {
+                const float4 c = shade[f_tri0 * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
+                if (SAMPLER == 0) {
+                    L.x = div_rho((L.x * c.x) * f_cos0);
+                    L.y = div_rho((L.y * c.y) * f_cos0);
+                    L.z = div_rho((L.z * c.z) * f_cos0);
+                } else {
+                    L = make3(L.x * c.x, L.y * c.y, L.z * c.z);
+                }
+            }
+        } else if (depth == a.max_bounces) {
+            // bounces == MAX_RAY_BOUNCES -> vec3(0)
+        } else {
+            terminal = false;  // shade h on the next trip
+        }
+        if (terminal) {
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+            live = fetch();
+        }
+    }
+
+    // fold the chunk sums of a pixel in chunk order: ((P0 + P1) + P2) + ...
+    const int base = lane & ~(a.split - 1);
+    f3 tot = acc;
+    for (int kk = 1; kk < a.split; ++kk) {
+        const float vx = __shfl(acc.x, base + kk, 64);
+        const float vy = __shfl(acc.y, base + kk, 64);
+        const float vz = __shfl(acc.z, base + kk, 64);
+        tot.x = tot.x + vx;
+        tot.y = tot.y + vy;
+        tot.z = tot.z + vz;
+    }
+    if (valid && chunk == 0) {
+        const float fs = (float)a.spp;
+        float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+        dst[0] = tot.x / fs;
+        dst[1] = tot.y / fs;
+        dst[2] = tot.z / fs;
+    }
+    if (a.casts != nullptr) {
+        const unsigned total = wave_sum(n_casts);
+        if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
+    }
+}
+
 // Exhaustive check of rcp_rn against IEEE division: thread g covers the
 // 4096 bit patterns [g*4096, (g+1)*4096).  Counts mismatches (ignoring NaN
 // payloads) and keeps the smallest mismatching pattern.
@@ -310,8 +579,23 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
 // Sample stealing pays where path lengths vary (GPU preset, up to 80 casts: Cornell
 // +24%, complex_light_room +32%); with the CPU preset's cap of 3 casts the lanes stay
 // in step and it costs 1%, so that preset keeps the fixed chunks.
+#ifndef RT_PS
+#define RT_PS 1  // 0: the CPU preset without the primary-ray phase (A/B builds)
+#endif
+#ifndef RT_PS_MAX_LDS
+#define RT_PS_MAX_LDS (40 * 1024)  // per workgroup: 8 samples per lane
+#endif
+
 template <int PRESET, int SAMPLER, int RULE>
 static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
+    if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= kPsMaxTri) {
+        const size_t ps_lds = (size_t)4 * a.per_chunk * kPsFields * 64 * sizeof(float);
+        if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
+            hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256),
+                               ps_lds, stream, a);
+            return;
+        }
+    }
     const size_t lds = (size_t)(256 / a.split) * (size_t)a.spp * 3 * sizeof(float);
     if (PRESET == 1 && lds <= (size_t)RT_STEAL_MAX_LDS)
         hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true>), dim3((unsigned)(a.n_blocks * a.split)),

@@ -67,6 +67,28 @@ __device__ __forceinline__ float div12(float x) {
 }
 #endif
 
+#if defined(__HIPCC__)
+// x / RHO, RHO = RN(1 / (2 RN(pi))) (GPU/constants/image_settings.h:14): q = RN(x c),
+// c = RN(1/RHO), corrected by one FMA residual step; equal to IEEE x / RHO for every
+// float x = +-0 or |x| in [2^-100, 2^100] (checked exhaustively on the host,
+// tools/check_divrho.c: 0 mismatches; zeros pass through so -0 keeps its sign).  Other
+// inputs (rare; wave-uniform test) take the division.
+__device__ __forceinline__ float div_rho(float x) {
+    constexpr float rho = 1.0f / (2.0f * 3.14159265358979323846f);
+    constexpr float c = 1.0f / rho;
+    const float q = x * c;
+    const float r = fmaf(-q, rho, x);
+    float y = (x == 0.0f) ? x : fmaf(r, c, q);
+    const float ax = fabsf(x);
+    const bool out_of_range = !(ax >= 0x1p-100f && ax <= 0x1p100f) && (x != 0.0f);
+    if (__builtin_amdgcn_ballot_w64(out_of_range) != 0ull) {
+        const float d = x / rho;
+        y = out_of_range ? d : y;
+    }
+    return y;
+}
+#endif
+
 // glm normalize: v * inversesqrt(dot(v, v)), inversesqrt(x) = 1 / sqrt(x)
 // (device: the reciprocal by rcp_rn, bit-identical to the division)
 RT_HD f3 normalize(f3 v) {
