@@ -305,6 +305,25 @@ int rt_sarsa_apply(rt_sarsa* sarsa, void* stream);
 #define RT_SELFTEST_RCP 1
 int rt_selftest(rt_ctx* ctx, int which, uint64_t* result /* 2 */);
 
+/* Host-side checks of the CPU-preset primary-ray cull (k_cull_ps; no GPU needed).
+ * rt_filter_build: the per-triangle filter records of the two-phase hit test
+ * (5 x float4 per triangle, layout rt_internal.hpp kFiltF4) for the triangle soup
+ * tri_v (n x 9, surfaces then lights: the rt_scene_create order).
+ * rt_rect_candidates: bit i of masks[i / 64] = triangle i may be the hit of a camera
+ * ray through a pixel of [px0, px1] x [py0, py1] (inclusive); the other triangles
+ * certainly fail the exact test for every such ray (RT_PRESET_CPU parameters).
+ * Replaces no reference interface: it exposes the kernel's own cull so tests can check
+ * it against the CPU restatement's hits (Ray::closest_intersection, CPU/rays/ray.cpp:14-28). */
+int rt_filter_build(const float* tri_v, int n, float* out_filt /* n x 20 */);
+int rt_rect_candidates(const float* filt, int n_tri, const rt_camera* cam, const rt_params* params,
+                       int px0, int py0, int px1, int py1, uint64_t* masks /* ceil(n_tri / 64) */);
+/* The same masks computed by the kernel (k_cull_ps) for the launch rt_render would make
+ * for the rectangle (x0, y0, w, h): 4 words per wave, waves in launch order (16x16 blocks
+ * row-major, `spp_split` workgroups each, 4 waves per workgroup).  *n_words: capacity of
+ * out on entry, words written on return. */
+int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
+                         int x0, int y0, int w, int h, uint64_t* out, int64_t* n_words);
+
 /* SDLScreen::PutPixelSDL pack rule (CPU/sdl/sdl_screen.cpp:100-112). Host arrays. */
 int rt_pack_argb(const float* rgb, int n, uint32_t* out_argb);
 

@@ -61,6 +61,9 @@ def lib():
                                      ctypes.c_int, ctypes.c_int, ctypes.c_int, _FP]
         L.orc_glibc_rand.argtypes = [ctypes.c_uint, ctypes.c_int, _IP]
         L.orc_pack_argb.argtypes = [_FP, ctypes.c_int, ctypes.POINTER(ctypes.c_uint32)]
+        L.orc_primary_hits.argtypes = [_FP, ctypes.c_int, ctypes.c_int, ctypes.POINTER(OrcCamera),
+                                       ctypes.POINTER(OrcParams), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, _IP]
         L.orc_num_threads.restype = ctypes.c_int
         L.orc_set_threads.argtypes = [ctypes.c_int]
         _LIB = L
@@ -119,6 +122,17 @@ def intersect(tri, n_surf, n_light, light_group, orig, direction, t_scale, hit_r
     lib().orc_intersect(_f(t_all), n_surf, n_light, _i(g), _f(o), _f(d), n, t_scale, hit_rule,
                         _f(out_t), _i(out_h))
     return out_t, out_h
+
+
+def primary_hits(tri, n_surf, n_light, cam, params, rect, s0, s1):
+    """Triangle index (-1 = miss) hit by the camera ray of every pixel of rect = (x, y, w, h)
+    and sample in [s0, s1): array (h, w, s1 - s0)."""
+    x, y, w, h = rect
+    t_all = np.ascontiguousarray(tri, np.float32)
+    out = np.zeros((h, w, s1 - s0), np.int32)
+    lib().orc_primary_hits(_f(t_all), n_surf, n_light, ctypes.byref(cam), ctypes.byref(params), x, y, w, h,
+                           s0, s1, _i(out))
+    return out
 
 
 def params_from(p) -> OrcParams:

@@ -587,6 +587,38 @@ ORC_API int orc_render(const float *tri, const float *albedo, int n_surf,
 }
 
 /*
+ * Primary-ray hits of the rectangle [x0,x0+w) x [y0,y0+h), samples [s0, s1) of every
+ * pixel: the triangle index (surfaces then light triangles; -1 = miss) of each camera
+ * ray, in (row, column, sample) order.  The check of the kernels' primary-ray cull
+ * (rt_rect_candidates): every triangle hit here must be a candidate of the rectangle.
+ */
+ORC_API void orc_primary_hits(const float *tri, int n_surf, int n_light, const orc_camera *cam,
+                              const orc_params *p, int x0, int y0, int w, int h, int s0, int s1,
+                              int32_t *out_tri) {
+    orc_scene sc;
+    scene_init(&sc, tri, NULL, n_surf, NULL, NULL, n_light);
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    const int ns = s1 - s0;
+    #pragma omp parallel for schedule(static)
+    for (int yy = 0; yy < h; yy++) {
+        for (int xx = 0; xx < w; xx++) {
+            int px = x0 + xx, py = y0 + yy;
+            uint32_t pix = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+            for (int s = s0; s < s1; s++) {
+                float r1, r2;
+                draw2(p->seed, pix, (uint32_t)s, 0u, &r1, &r2);
+                v3 o, d;
+                camera_ray(cam, p, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                hit_t ht = closest_hit(&sc, o, d, p->t_scale, p->hit_rule);
+                out_tri[((size_t)yy * w + xx) * ns + (s - s0)] = ht.tri;
+            }
+        }
+    }
+    free(sc.normal);
+}
+
+/*
  * The whole frame in the reference's own sampling order and random stream
  * (g_seq above): CPU preset, uniform sampler, CPU hit rule only.  out_rgb: W*H*3,
  * row-major.  srand(seed) first (seed 1 = the reference's unseeded stream).  Its

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/rtmi.h"
+#include "rt_cull.hpp"
 #include "rt_internal.hpp"
 
 namespace {
@@ -53,6 +54,10 @@ struct rt_ctx {
     rt::BlockDesc* d_blocks = nullptr;
     int n_blocks = 0;
     int blocks_cap = 0;
+    // per-wave candidate masks of the CPU-preset primary-ray phase (RenderLaunch::cull);
+    // one render at a time per context (the contexts' one-thread rule)
+    unsigned long long* d_cull = nullptr;
+    size_t cull_cap = 0;
 };
 
 struct rt_scene {
@@ -121,6 +126,22 @@ int set_device(rt_ctx* ctx) {
 }
 
 }  // namespace
+
+namespace rt {
+// The cull workspace of a render launch (grown on demand, kept by the context).
+int ctx_cull(rt_ctx* ctx, RenderLaunch* a) {
+    const size_t words = (size_t)a->n_blocks * (size_t)a->split * 4 * kRenderCullWords;
+    if (words > ctx->cull_cap) {
+        if (ctx->d_cull) RT_HIP(hipFree(ctx->d_cull));
+        ctx->d_cull = nullptr;
+        ctx->cull_cap = 0;
+        RT_HIP(hipMalloc(&ctx->d_cull, sizeof(unsigned long long) * words));
+        ctx->cull_cap = words;
+    }
+    a->cull = ctx->d_cull;
+    return RT_OK;
+}
+}  // namespace rt
 
 int rt::ensure_blocks_impl(rt_ctx* ctx, const std::vector<rt::BlockDesc>& blocks) {
     if ((int)blocks.size() > ctx->blocks_cap) {
@@ -191,6 +212,25 @@ rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const 
     a.sin_x = (float)sin((double)cam->yaw_x);
     a.use_filter = rt::filter_usable(a.scene, a.cam_x, a.cam_y, a.cam_z, a.t_scale);
     return a;
+}
+
+// Hit-test record of one triangle (v = v0, v1, v2): {v0, c0}, {e1, 0}, {e2, 0} with
+// c0 = m11*m22 - m21*m12 of [-D | e1 | e2] (rt_internal.hpp, kIsectF4).
+void isect_record(const float* v, float4* out) {
+    const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+    const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+    const float c0 = e1y * e2z - e2y * e1z;
+    out[0] = make_float4(v[0], v[1], v[2], c0);
+    out[1] = make_float4(e1x, e1y, e1z, 0.0f);
+    out[2] = make_float4(e2x, e2y, e2z, 0.0f);
+}
+
+// Origin bound of the filter records of a scene: every surface point, plus room for a
+// camera outside the scene (a camera beyond it gets the single-phase scan).
+double filter_origin_bound(const float* v, size_t n_floats) {
+    double vmax = 0.0;
+    for (size_t k = 0; k < n_floats; ++k) vmax = fmax(vmax, fabs((double)v[k]));
+    return fmax(8.0, 2.0 * vmax + 1.0);
 }
 
 // float >= x (x finite, >= 0)
@@ -307,6 +347,7 @@ int rt_ctx_destroy(rt_ctx* ctx) {
     (void)hipSetDevice(ctx->device);
     rt::release_dqn_workspace(ctx);
     if (ctx->d_blocks) (void)hipFree(ctx->d_blocks);
+    if (ctx->d_cull) (void)hipFree(ctx->d_cull);
     delete ctx;
     return RT_OK;
 }
@@ -347,14 +388,11 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
         const bool is_light = i >= n_surf;
         const int j = is_light ? i - n_surf : i;
         const float* v = is_light ? light_v + (size_t)j * 9 : tri_v + (size_t)j * 9;
-        const f3 v0 = make3(v[0], v[1], v[2]), v1 = make3(v[3], v[4], v[5]), v2 = make3(v[6], v[7], v[8]);
-        const f3 e1 = make3(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
-        const f3 e2 = make3(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
-        // c0 = m11*m22 - m21*m12 of [-D | e1 | e2]
-        const float c0 = e1.y * e2.z - e2.y * e1.z;
-        isect[(size_t)i * 3 + 0] = make_float4(v0.x, v0.y, v0.z, c0);
-        isect[(size_t)i * 3 + 1] = make_float4(e1.x, e1.y, e1.z, 0.0f);
-        isect[(size_t)i * 3 + 2] = make_float4(e2.x, e2.y, e2.z, 0.0f);
+        isect_record(v, &isect[(size_t)i * 3]);
+        const f3 v0 = make3(v[0], v[1], v[2]);
+        const f3 e1 = make3(isect[(size_t)i * 3 + 1].x, isect[(size_t)i * 3 + 1].y, isect[(size_t)i * 3 + 1].z);
+        const f3 e2 = make3(isect[(size_t)i * 3 + 2].x, isect[(size_t)i * 3 + 2].y, isect[(size_t)i * 3 + 2].z);
+        (void)v0;
         // Triangle::compute_and_set_normal: normalize(cross(e2, e1))
         const f3 N = rt::normalize(rt::cross(e2, e1));
         f3 T, B;
@@ -381,9 +419,7 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     }
     // Filter records (two-phase hit test).  Origin bound: every surface point, plus room
     // for a camera outside the scene (a camera beyond it gets the single-phase scan).
-    double vmax = 0.0;
-    for (float v : sc->tri) vmax = fmax(vmax, fabs((double)v));
-    const double obound = fmax(8.0, 2.0 * vmax + 1.0);
+    const double obound = filter_origin_bound(sc->tri.data(), sc->tri.size());
     // padded to an even triangle count (phase 1 runs in pairs; the pad is masked off)
     std::vector<float4> filt((size_t)((n + 1) & ~1) * rt::kFiltF4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     bool filt_ok = true;
@@ -522,7 +558,9 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
         a.out_pitch = w;
         a.out = d_out;
         a.casts = d_casts;
-        e = rt::launch_render(a, 0);
+        rc = rt::ctx_cull(ctx, &a);
+        if (rc != RT_OK) e = hipErrorOutOfMemory;
+        if (e == hipSuccess) e = rt::launch_render(a, 0);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, out_bytes, hipMemcpyDeviceToHost);
@@ -565,6 +603,8 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     a.out_pitch = tile_size;
     a.out = d_out;
     a.casts = reinterpret_cast<unsigned long long*>(d_casts);
+    rc = rt::ctx_cull(ctx, &a);
+    if (rc != RT_OK) return rc;
     RT_HIP(rt::launch_render(a, (hipStream_t)stream));
     return RT_OK;
 }
@@ -591,6 +631,90 @@ int rt_selftest(rt_ctx* ctx, int which, uint64_t* result) {
     if (e != hipSuccess) return fail(RT_E_HIP, "rt_selftest: %s", hipGetErrorString(e));
     result[0] = m;
     result[1] = f;
+    return RT_OK;
+}
+
+
+// ---- checks of the primary-ray cull (k_cull_ps) on the host ----
+
+int rt_filter_build(const float* tri_v, int n, float* out_filt) {
+    if (!tri_v || !out_filt || n <= 0) return fail(RT_E_INVALID, "bad arguments");
+    const double obound = filter_origin_bound(tri_v, (size_t)n * 9);
+    for (int i = 0; i < n; ++i) {
+        float4 rec[3];
+        isect_record(tri_v + (size_t)i * 9, rec);
+        float4 f[rt::kFiltF4];
+        if (!build_filter(rec[0], rec[1], rec[2], obound, f))
+            return fail(RT_E_UNSUPPORTED, "no filter record for triangle %d (coordinates too large)", i);
+        memcpy(out_filt + (size_t)i * 4 * rt::kFiltF4, f, sizeof(f));
+    }
+    return RT_OK;
+}
+
+int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
+                         int x0, int y0, int w, int h, uint64_t* out, int64_t* n_words) {
+    if (!ctx || !scene || !cam || !out || !n_words) return fail(RT_E_INVALID, "NULL argument");
+    int rc = check_params(params);
+    if (rc != RT_OK) return rc;
+    if (w <= 0 || h <= 0 || x0 < 0 || y0 < 0 || x0 + w > params->width || y0 + h > params->height)
+        return fail(RT_E_INVALID, "rectangle outside the image");
+    rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    std::vector<rt::BlockDesc> blocks;
+    for (int by = 0; by < h; by += 16)
+        for (int bx = 0; bx < w; bx += 16) blocks.push_back({x0 + bx, y0 + by, bx, by});
+    rt::RenderLaunch a = make_launch(scene, cam, params);
+    if (!a.use_filter) return fail(RT_E_UNSUPPORTED, "no filter records for this scene and camera");
+    a.n_blocks = (int)blocks.size();
+    a.clip_x1 = x0 + w;
+    a.clip_y1 = y0 + h;
+    const int64_t words = (int64_t)a.n_blocks * a.split * 4 * rt::kRenderCullWords;
+    if (*n_words < words) {
+        *n_words = words;
+        return fail(RT_E_INVALID, "out holds %lld words, %lld needed", (long long)*n_words, (long long)words);
+    }
+    rt::BlockDesc* d_blocks = nullptr;
+    hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(d_blocks, blocks.data(), sizeof(rt::BlockDesc) * blocks.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        a.blocks = d_blocks;
+        rc = rt::ctx_cull(ctx, &a);
+        if (rc != RT_OK) e = hipErrorOutOfMemory;
+    }
+    if (e == hipSuccess) e = rt::launch_cull(a, 0);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, a.cull, sizeof(uint64_t) * (size_t)words, hipMemcpyDeviceToHost);
+    (void)hipFree(d_blocks);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_cull_masks_device: %s", hipGetErrorString(e));
+    *n_words = words;
+    return RT_OK;
+}
+
+// debugging aid: the context's cull workspace as the last render left it
+int rt_debug_cull_workspace(rt_ctx* ctx, uint64_t* out, int64_t n_words) {
+    if (!ctx || !out) return fail(RT_E_INVALID, "NULL argument");
+    if ((size_t)n_words > ctx->cull_cap) return fail(RT_E_INVALID, "workspace holds %zu words", ctx->cull_cap);
+    RT_HIP(hipDeviceSynchronize());
+    RT_HIP(hipMemcpy(out, ctx->d_cull, sizeof(uint64_t) * (size_t)n_words, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_rect_candidates(const float* filt, int n_tri, const rt_camera* cam, const rt_params* p, int px0, int py0,
+                       int px1, int py1, uint64_t* masks) {
+    if (!filt || !cam || !p || !masks || n_tri <= 0) return fail(RT_E_INVALID, "bad arguments");
+    if (p->preset != RT_PRESET_CPU) return fail(RT_E_UNSUPPORTED, "the primary-ray phase is CPU-preset only");
+    if (px0 > px1 || py0 > py1) return fail(RT_E_INVALID, "empty rectangle");
+    const rt::CamRect c = rt::make_cam_rect(cam->pos[0], cam->pos[1], cam->pos[2], (float)cos((double)cam->yaw_y),
+                                            (float)sin((double)cam->yaw_y), p->width, p->height, p->t_scale,
+                                            px0, px1, py0, py1);
+    const float4* f = reinterpret_cast<const float4*>(filt);
+    for (int g = 0; g < (n_tri + 63) / 64; ++g) masks[g] = 0;
+    for (int i = 0; i < n_tri; ++i) {
+        const bool cull = (p->hit_rule == RT_HIT_RULE_CPU) ? rt::rect_cull<0>(f + (size_t)i * rt::kFiltF4, c)
+                                                           : rt::rect_cull<1>(f + (size_t)i * rt::kFiltF4, c);
+        if (!cull) masks[i / 64] |= 1ull << (i % 64);
+    }
     return RT_OK;
 }
 

@@ -75,7 +75,11 @@ struct RenderLaunch {
     unsigned long long* casts;
     uint32_t sample_base;  // first RNG sample index (SARSA: frame * spp); 0 elsewhere
     int use_filter;        // 1: two-phase closest hit (filter records valid for this launch)
+    // CPU-preset primary-ray phase (k_render_ps): workspace of kRenderCullWords 64-bit
+    // candidate masks per wave (n_blocks * split * 4 waves); nullptr: no primary phase
+    unsigned long long* cull;
 };
+constexpr int kRenderCullWords = 4;  // candidate masks per wave: scenes of <= 256 triangles
 
 // 1 if the filter records of `s` hold for rays from a camera at (cx, cy, cz) (and
 // from surface points) at this t_scale.  Host side, once per launch.
@@ -232,5 +236,7 @@ int read_locations(const char* path, std::vector<float>* loc, std::vector<float>
 
 // returns hipErrorInvalidValue for combinations the kernels do not instantiate
 hipError_t launch_render(const RenderLaunch& a, hipStream_t stream);
+// k_cull_ps alone (the primary-ray candidate masks into a.cull)
+hipError_t launch_cull(const RenderLaunch& a, hipStream_t stream);
 
 }  // namespace rt

@@ -278,10 +278,67 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
 // LDS: per wave and sample slot k, five 64-lane rows (lane-contiguous: conflict-free):
 //   continuing: d.x, d.y, d.z, t, triangle;  ended: L.x, L.y, L.z, -, -1.
 constexpr int kPsFields = 5;
-constexpr int kPsMaxTri = 256;
 
+// the bits of 64-triangle group g that are triangles of an n-triangle scene
+__device__ __forceinline__ uint64_t tri_mask(int n, int g) {
+    const int k = n - 64 * g;
+    return k >= 64 ? ~0ull : (k <= 0 ? 0ull : ((1ull << k) - 1ull));
+}
+
+// Candidate masks of the primary-ray phase: wave w of workgroup b writes
+// cull[(b * 4 + w) * kRenderCullWords + g], bit j = triangle 64 g + j may be the hit of a
+// camera ray through the wave's pixel rectangle (rect_cull, rt_trace.hpp).  Same grid
+// and lane -> pixel mapping as k_render_ps.
+template <int RULE>
+__global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    const int part = blockIdx.x & (a.split - 1);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int lane = threadIdx.x & 63;
+    const int px = blk.px0 + (q & 15);
+    const int py = blk.py0 + (q >> 4);
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
+    int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        x0 = min(x0, __shfl_xor(x0, off, 64));
+        x1 = max(x1, __shfl_xor(x1, off, 64));
+        y0 = min(y0, __shfl_xor(y0, off, 64));
+        y1 = max(y1, __shfl_xor(y1, off, 64));
+    }
+    unsigned long long* w = a.cull + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRenderCullWords;
+    if (x1 < 0) {  // no pixel of the image in this wave
+        if (lane < kRenderCullWords) w[lane] = 0ull;
+        return;
+    }
+    const CamRect c = make_cam_rect(a.cam_x, a.cam_y, a.cam_z, a.cos_y, a.sin_y, a.width, a.height, a.t_scale,
+                                    x0, x1, y0, y1);
+    const int n_tri = a.scene.n_tri;
+    unsigned long long mine = 0ull;
+#pragma unroll
+    for (int g = 0; g < kRenderCullWords; ++g) {
+        const int i = g * 64 + lane;
+        const bool in_range = i < n_tri;
+#ifdef RT_TIMING_NO_CULL
+        const bool keep = in_range;
+#else
+        // every lane tests a real record (triangle 0 past the end), the range masks after
+        const bool cull = rect_cull<RULE>(a.scene.filt + (size_t)(in_range ? i : 0) * kFiltF4, c);
+        const bool keep = in_range && !cull;
+#endif
+        const unsigned long long m = __ballot(keep) & tri_mask(n_tri, g);
+        if (lane == g) mine = m;
+    }
+    if (lane < kRenderCullWords) w[lane] = mine;
+}
+
+#ifndef RT_PS_MIN_WAVES
+#define RT_PS_MIN_WAVES 1
+#endif
 template <int SAMPLER, int RULE>
-__global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
+__global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
     extern __shared__ float s_ps[];
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -299,51 +356,25 @@ __global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
     const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
     const float4* __restrict__ shade = a.scene.shade;
     const int n_surf = a.scene.n_surf;
-    const int n_tri = a.scene.n_tri;
     const int pc = a.per_chunk;
     float* const slots = s_ps + (size_t)(threadIdx.x >> 6) * pc * kPsFields * 64 + lane;
     const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
 
-    // ---- candidate triangles of the wave's pixel rectangle ----
-    uint64_t cm[kPsMaxTri / 64];
+#ifdef RT_DEBUG_POISON_LDS
+    for (int k = 0; k < pc * kPsFields; ++k) slots[k * 64] = __int_as_float(RT_DEBUG_POISON_LDS);
+#endif
+    // ---- candidate triangles of the wave's pixel rectangle (k_cull_ps) ----
+    uint64_t cm[kRenderCullWords];
     {
-        int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
-        int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
+#ifdef RT_DEBUG_ACQUIRE_CULL
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#endif
+        const unsigned long long* w = a.cull + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRenderCullWords;
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            x0 = min(x0, __shfl_xor(x0, off, 64));
-            x1 = max(x1, __shfl_xor(x1, off, 64));
-            y0 = min(y0, __shfl_xor(y0, off, 64));
-            y1 = max(y1, __shfl_xor(y1, off, 64));
-        }
-        CamRect c;
-        c.ox = a.cam_x; c.oy = a.cam_y; c.oz = a.cam_z;
-        const double cy = a.cos_y, sy = a.sin_y;
-        c.R[0][0] = cy;  c.R[0][1] = 0.0; c.R[0][2] = -sy;
-        c.R[1][0] = 0.0; c.R[1][1] = 1.0; c.R[1][2] = 0.0;
-        c.R[2][0] = sy;  c.R[2][1] = 0.0; c.R[2][2] = cy;
-        const double W = a.width, H = a.height;
-        const double xs[2] = {(double)x0 - 0.5 * W, (double)(x1 + 1) - 0.5 * W};
-        const double ys[2] = {(double)y0 - 0.5 * H, (double)(y1 + 1) - 0.5 * H};
-        double pm = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            c.pc[k][0] = xs[k & 1];
-            c.pc[k][1] = ys[k >> 1];
-            c.pc[k][2] = H;
-            pm = fmax(pm, sqrt(xs[k & 1] * xs[k & 1] + ys[k >> 1] * ys[k >> 1] + H * H));
-        }
-        c.pmin = H;  // |p| >= p.z = H
-        c.pmax = pm * (1.0 + 0x1p-40);
-        c.delta = 0x1p-24 * (64.0 + 8.0 * (W + H) / H);
-        c.ets = (double)(kEps * a.t_scale);
-#pragma unroll
-        for (int g = 0; g < kPsMaxTri / 64; ++g) {
-            const int i = g * 64 + lane;
-            bool keep = false;
-            if (i < n_tri) keep = !rect_cull<RULE>(a.scene.filt + (size_t)i * kFiltF4, c);
-            cm[g] = __ballot(keep);
-        }
+        for (int g = 0; g < kRenderCullWords; ++g)
+            cm[g] = (__builtin_amdgcn_readfirstlane((uint32_t)w[g]) |
+                     ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w[g] >> 32)) << 32)) &
+                    tri_mask(a.scene.n_tri, g);  // never a triangle past the scene
     }
 
     // ---- phase P: primary rays of the lane's samples ----
@@ -361,12 +392,16 @@ __global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
         h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
         h.tri = -1;
 #pragma unroll
-        for (int g = 0; g < kPsMaxTri / 64; ++g) {
+        for (int g = 0; g < kRenderCullWords; ++g) {
             uint64_t m = cm[g];
             while (m != 0ull) {
                 const int b = __builtin_ctzll(m);
                 m &= m - 1ull;
+#ifdef RT_DEBUG_VECTOR_ISECT
+                exact_one<RULE>(a.scene.isect, g * 64 + b, cam, nDx, nDy, nDz, h);
+#else
                 exact_one_c<RULE>(isect, g * 64 + b, cam, nDx, nDy, nDz, h);
+#endif
             }
         }
         n_casts += valid ? 1u : 0u;
@@ -391,6 +426,9 @@ __global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
         sl[4 * 64] = __int_as_float(code);
     }
 
+#ifdef RT_DEBUG_OUT
+    const unsigned n_p = n_casts;
+#endif
     // ---- phase S: bounces ----
     f3 acc = make3(0.0f, 0.0f, 0.0f);
     int k = 0;          // next slot
@@ -519,9 +557,17 @@ __global__ __launch_bounds__(256) void k_render_ps(const RenderLaunch a) {
     if (valid && chunk == 0) {
         const float fs = (float)a.spp;
         float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+#ifdef RT_DEBUG_OUT
+        int codes = 0;
+        for (int kk = 0; kk < pc; ++kk) codes = codes * 41 + (__float_as_int(slots[(kk * kPsFields + 4) * 64]) + 1);
+        dst[0] = (float)(uint32_t)(cm[0] & 0xffffffu);
+        dst[1] = (float)(uint32_t)((cm[0] >> 24) & 0xffffffu);
+        dst[2] = (float)(codes & 0xffffff) + 0.0f * (float)n_p;
+#else
         dst[0] = tot.x / fs;
         dst[1] = tot.y / fs;
         dst[2] = tot.z / fs;
+#endif
     }
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
@@ -588,9 +634,13 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
 
 template <int PRESET, int SAMPLER, int RULE>
 static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
-    if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= kPsMaxTri) {
+    if (PRESET == 0 && RT_PS && a.use_filter && a.cull != nullptr && a.scene.n_tri <= 64 * kRenderCullWords) {
         const size_t ps_lds = (size_t)4 * a.per_chunk * kPsFields * 64 * sizeof(float);
         if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
+            hipLaunchKernelGGL((k_cull_ps<RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a);
+#ifdef RT_DEBUG_SYNC_CULL
+            (void)hipStreamSynchronize(stream);
+#endif
             hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256),
                                ps_lds, stream, a);
             return;
@@ -603,6 +653,15 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     else
         hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false>), dim3((unsigned)(a.n_blocks * a.split)),
                            dim3(256), 0, stream, a);
+}
+
+hipError_t launch_cull(const RenderLaunch& a, hipStream_t stream) {
+    if (a.n_blocks <= 0 || a.cull == nullptr || a.scene.filt == nullptr) return hipErrorInvalidValue;
+    if (a.hit_rule == 0)
+        hipLaunchKernelGGL((k_cull_ps<0>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a);
+    else
+        hipLaunchKernelGGL((k_cull_ps<1>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a);
+    return hipGetLastError();
 }
 
 hipError_t launch_render(const RenderLaunch& a, hipStream_t stream) {

@@ -6,6 +6,7 @@
 
 #include <float.h>
 
+#include "rt_cull.hpp"
 #include "rt_internal.hpp"
 
 namespace rt {
@@ -247,64 +248,7 @@ __device__ __forceinline__ void exact_one_c(cfloat4* __restrict__ tri, int i, f3
 // test fails (build_filter, rt_capi.cpp).  So a culled triangle cannot be the hit of any
 // primary ray of the rectangle, and testing the others in index order gives the
 // reference's hit bit for bit.
-struct CamRect {
-    double ox, oy, oz;        // camera position
-    double R[3][3];           // d = R p (the float rotation entries of camera_ray)
-    double pc[4][3];          // p at the 4 corners of the rectangle
-    double pmin, pmax;        // bounds of |p| over the rectangle
-    double delta;             // bound of |d_float - R p/|p|| per component
-    double ets;               // eps * t_scale as the filter computes it (RULE 0)
-};
-
-// bounds of a.d over the rectangle (a in world space)
-__device__ __forceinline__ void form_bounds(const CamRect& c, double ax, double ay, double az, double* lo,
-                                            double* hi) {
-    const double bx = c.R[0][0] * ax + c.R[1][0] * ay + c.R[2][0] * az;  // b = R^T a
-    const double by = c.R[0][1] * ax + c.R[1][1] * ay + c.R[2][1] * az;
-    const double bz = c.R[0][2] * ax + c.R[1][2] * ay + c.R[2][2] * az;
-    double l = 1e300, h = -1e300;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const double v = bx * c.pc[k][0] + by * c.pc[k][1] + bz * c.pc[k][2];
-        l = fmin(l, v);
-        h = fmax(h, v);
-    }
-    const double slack = c.delta * (fabs(ax) + fabs(ay) + fabs(az));
-    *lo = l / (l >= 0.0 ? c.pmax : c.pmin) - slack;
-    *hi = h / (h >= 0.0 ? c.pmin : c.pmax) + slack;
-}
-
-// true if filter record `f` certainly rejects every camera ray of the rectangle
-template <int RULE>
-__device__ __forceinline__ bool rect_cull(const float4* __restrict__ f, const CamRect& c) {
-    const float4 F0 = f[0], F1 = f[1], F2 = f[2], F3 = f[3], F4 = f[4];
-    const double eA = 2.0 * (double)F1.w, EW = 2.0 * (double)F2.w, ET = 2.0 * (double)F3.w;
-    const double nx = F0.x, ny = F0.y, nz = F0.z;
-    double alo, ahi;
-    form_bounds(c, nx, ny, nz, &alo, &ahi);
-    double sg;
-    if (alo > eA) sg = 1.0;
-    else if (ahi < -eA) sg = -1.0;
-    else return false;  // the sign of the determinant is not certain
-    // U = (o x e2 + F2).d, e2 = F1
-    const double ux = (c.oy * F1.z - c.oz * F1.y) + F2.x;
-    const double uy = (c.oz * F1.x - c.ox * F1.z) + F2.y;
-    const double uz = (c.ox * F1.y - c.oy * F1.x) + F2.z;
-    // V = (o x F3 + F4).d, F3 = -e1
-    const double vx = (c.oy * F3.z - c.oz * F3.y) + F4.x;
-    const double vy = (c.oz * F3.x - c.ox * F3.z) + F4.y;
-    const double vz = (c.ox * F3.y - c.oy * F3.x) + F4.z;
-    double lo, hi;
-    form_bounds(c, ux, uy, uz, &lo, &hi);
-    if ((sg > 0.0 ? hi : -lo) < -EW) return true;  // u < 0
-    form_bounds(c, vx, vy, vz, &lo, &hi);
-    if ((sg > 0.0 ? hi : -lo) < -EW) return true;  // v < 0
-    form_bounds(c, nx - ux - vx, ny - uy - vy, nz - uz - vz, &lo, &hi);
-    if ((sg > 0.0 ? hi : -lo) < -EW) return true;  // u + v > 1
-    const double cT = (double)F0.w - (c.ox * nx + c.oy * ny + c.oz * nz);
-    const double tmax = (RULE == 0) ? (sg > 0.0 ? cT - c.ets * alo : -cT + c.ets * ahi) : sg * cT;
-    return tmax < -ET;  // t <= eps (RULE 0) / t < 0 (RULE 1)
-}
+// CamRect, rect_cull: rt_cull.hpp (shared with the host for tests)
 
 // Two-phase closest hit: the same Hit as closest_hit, bit for bit.
 //
@@ -441,6 +385,13 @@ __device__ __forceinline__ Hit closest_hit_sel(const DeviceScene& s, int use_fil
 // two uniforms of event `ev` of sample `smp` of pixel `pix`
 __device__ __forceinline__ void draw2(uint32_t pix, uint32_t smp, uint32_t ev, uint32_t k0,
                                       uint32_t k1, float* a, float* b) {
+#ifdef RT_TIMING_CHEAP_RNG
+    // timing-only build (wrong images): what the Philox rounds cost
+    const uint32_t h = (pix * 0x9E3779B9u) ^ (smp * 0x85EBCA6Bu) ^ (ev * 0xC2B2AE35u) ^ k0;
+    *a = u01(h * 0x27D4EB2Fu);
+    *b = u01((h ^ (h >> 15)) * 0x165667B1u);
+    return;
+#endif
     uint32_t o[4];
     philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
     *a = u01(o[0]);

@@ -8,15 +8,15 @@ from ._lib import (LIB_PATH, RT_HIT_NONE, RT_HIT_RULE_CPU, RT_HIT_RULE_GPU, RT_H
                    RT_HIT_TYPE_SURFACE, RT_PRESET_CPU, RT_PRESET_GPU, RT_SAMPLER_COSINE,
                    RT_SAMPLER_UNIFORM, RtCamera, RtError, RtParams, lib)
 from .api import (CAMERAS, OBJ_KINDS, Context, Geometry, Scene, camera, cornell_geometry,
-                  default_params, intersect, intersect_device, obj_geometry, pack_argb, render,
-                  render_tiles_device, save_bmp, save_png)
+                  default_params, filter_records, intersect, intersect_device, obj_geometry, pack_argb,
+                  rect_candidates, render, render_tiles_device, save_bmp, save_png)
 from . import dist, dqn, metrics, sarsa, tiles
 
 __all__ = [
     "LIB_PATH", "RT_HIT_NONE", "RT_HIT_RULE_CPU", "RT_HIT_RULE_GPU", "RT_HIT_TYPE_LIGHT",
     "RT_HIT_TYPE_SURFACE", "RT_PRESET_CPU", "RT_PRESET_GPU", "RT_SAMPLER_COSINE",
     "RT_SAMPLER_UNIFORM", "RtCamera", "RtError", "RtParams", "lib", "CAMERAS", "OBJ_KINDS",
-    "Context", "Geometry", "Scene", "camera", "cornell_geometry", "default_params", "intersect",
-    "intersect_device", "obj_geometry", "pack_argb", "render", "render_tiles_device", "save_bmp", "save_png",
+    "Context", "Geometry", "Scene", "camera", "cornell_geometry", "default_params", "filter_records", "intersect",
+    "intersect_device", "obj_geometry", "pack_argb", "rect_candidates", "render", "render_tiles_device", "save_bmp", "save_png",
     "dist", "dqn", "metrics", "sarsa", "tiles",
 ]

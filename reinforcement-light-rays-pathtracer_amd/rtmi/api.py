@@ -226,6 +226,27 @@ def render_tiles_device(ctx: Context, scene: Scene, cam: RtCamera, params: RtPar
                                        ctypes.c_void_p(stream)))
 
 
+def filter_records(tri_all: np.ndarray) -> np.ndarray:
+    """Filter records of the two-phase hit test for a triangle soup (n, 9): (n, 20) float32."""
+    t = np.ascontiguousarray(tri_all, np.float32).reshape(-1, 9)
+    out = np.zeros((t.shape[0], 20), np.float32)
+    check(lib().rt_filter_build(_fp(t), t.shape[0], _fp(out)))
+    return out
+
+
+def rect_candidates(filt: np.ndarray, cam: RtCamera, params: RtParams, px0: int, py0: int, px1: int,
+                    py1: int) -> np.ndarray:
+    """Boolean (n_tri,) mask: the triangles the CPU-preset primary-ray phase keeps for camera
+    rays through pixels [px0, px1] x [py0, py1] (the cull of k_cull_ps, run on the host)."""
+    f = np.ascontiguousarray(filt, np.float32)
+    n = f.shape[0]
+    words = np.zeros((n + 63) // 64, np.uint64)
+    check(lib().rt_rect_candidates(_fp(f), n, ctypes.byref(cam), ctypes.byref(params), px0, py0, px1, py1,
+                                   words.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+    bits = np.unpackbits(words.view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)
+
+
 def pack_argb(rgb: np.ndarray) -> np.ndarray:
     a = np.ascontiguousarray(rgb, np.float32)
     n = a.size // 3
