@@ -1,27 +1,34 @@
 #!/usr/bin/env python3
-"""Benchmark: Mrays/s on the Cornell box 512x512, 256 spp (BASELINE.json config 2).
+"""Benchmark: ray casts per second of the path tracer's hot path on BASELINE.json's configs.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cornell|door_room_sarsa|
+                    archway_dqn|complex_light] [--width .. --height .. --spp .. --spp-split ..]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step renders one full 512x512 / 256-spp frame of the reference's Cornell
-box (CPU-engine preset: cap 2 bounces, hit rule of the prebuilt CPU object,
-uniform hemisphere sampling).  The frame is cut into 32x32 tiles dealt to the
-ranks by diagonals (rtmi.tiles; one process per GPU); each rank renders its
-tiles with the HIP megakernel, and the per-rank tile buffers are all-gathered
-over RCCL into the full image -- asynchronously, into one of two buffers, so
-frame i+1 renders while frame i is exchanged.  The frame is fixed as N grows:
+Default workload (the driver's bench line): BASELINE config 2, the reference's Cornell box,
+512x512, 256 spp, CPU-engine preset (cap 2 bounces, hit rule of the prebuilt CPU object,
+uniform hemisphere sampling).  A step renders one full frame.  The other workloads are
+BASELINE configs 3-5 for torchrun runs at more GPUs (a step = one frame; SARSA frames learn,
+so their TD sums are all-reduced between ranks every step).
+
+Multi-GPU: the frame is cut into 32x32 tiles dealt to the ranks by diagonals (rtmi.tiles; one
+process per GPU); each rank renders its tiles with the HIP kernels, and the per-rank tile
+buffers are all-gathered over RCCL into the full image -- asynchronously, into one of two
+buffers, so frame i+1 renders while frame i is exchanged.  The frame is fixed as N grows:
 strong scaling.
 
-value = total ray casts (all ranks) / max-over-ranks wall time of the K
-timed steps, in Mrays/s.  rank 0 prints one JSON line with the roofline of
-the render kernel (HIP events on the launch stream), the per-pixel MAPE vs the
-CPU restatement on a checked window, and the CPU baseline (oracle/, timed on
-this host's cores on a bounded sample).
+value = total ray casts (all ranks) / max-over-ranks wall time of the K timed steps, in
+Mrays/s.  rank 0 prints one JSON line with the roofline of the render kernels (HIP events on
+the launch stream; instruction and HBM counts from the committed rocprofv3 profile of the
+same build, profiles/*_bench_pmc.json), the bit-exactness of 8 full 32x32 tiles (image and
+ray casts) vs the CPU restatement, and the CPU baseline (oracle/, this host's cores, bounded
+sample, best of 3).
 """
 from __future__ import annotations
 
 import argparse
+import glob
+import hashlib
 import json
 import os
 import sys
@@ -37,13 +44,23 @@ import torch.distributed as dist  # noqa: E402
 
 import rtmi  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-VALU_PEAK_TFLOPS = 157.3  # FP32 vector spec
+MODELS = os.path.join(ROOT, "assets", "models")
 TILE = 32
-# HBM traffic of k_render<0,0,0> on this workload from the PMC passes of tools/gpu_profile.sh
-# (rocprofv3 FETCH_SIZE x 2 per MI355X_MICROARCH.md + WRITE_SIZE, per launch)
-PMC_PROFILE = os.path.join("profiles", "r1v9_pmc.json")
-DEFAULT_WORKLOAD = (512, 512, 256, 64)
+# MI355X peaks (MI355X_MICROARCH.md): 1024 SIMD-32 units, one wave64 VALU instruction per
+# 2 cycles each at the 2.4 GHz maximum clock; FP32 vector 157.3 TFLOP/s; HBM3E 8 TB/s.
+VALU_ISSUE_PEAK_G = 1024 * 2.4 / 2.0  # G wave-instructions / s
+VALU_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+# the committed rocprofv3 profile of the default workload (tools/gpu_bench_pmc.sh)
+PMC_GLOB = os.path.join(ROOT, "profiles", "*_bench_pmc.json")
+
+WORKLOADS = {
+    # name: (scene, preset, sampler, width, height, spp, spp_split, BASELINE config)
+    "cornell": ("cornell", rtmi.RT_PRESET_CPU, "uniform", 512, 512, 256, 64, 2),
+    "door_room_sarsa": ("door_room", rtmi.RT_PRESET_GPU, "sarsa", 512, 512, 256, 8, 3),
+    "archway_dqn": ("archway", rtmi.RT_PRESET_GPU, "dqn", 1024, 1024, 512, 1, 4),
+    "complex_light": ("complex_light_room", rtmi.RT_PRESET_GPU, "uniform", 2048, 2048, 1024, 8, 5),
+}
 
 
 def parse():
@@ -51,48 +68,80 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--width", type=int, default=512)
-    ap.add_argument("--height", type=int, default=512)
-    ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--spp-split", type=int, default=64)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
-                    help="target CPU-baseline sample duration (0 disables)")
+    ap.add_argument("--workload", default="cornell", choices=sorted(WORKLOADS))
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--spp-split", type=int, default=None)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
+                    help="target duration of one CPU-baseline run (best of 3; 0 disables)")
     ap.add_argument("--no-parity", action="store_true")
     return ap.parse_args()
 
 
-def pmc_traffic(params):
-    """(bytes per launch, source) of the committed PMC profile for the default workload."""
-    if (params.width, params.height, params.spp, params.spp_split) != DEFAULT_WORKLOAD:
-        return None, None
-    try:
-        prof = json.load(open(os.path.join(ROOT, PMC_PROFILE)))
-    except (OSError, ValueError):
-        return None, None
-    for name, e in prof.get("selected", {}).items():
-        if "k_render<0, 0, 0" in name and "traffic_bytes_per_launch" in e:
-            return int(e["traffic_bytes_per_launch"]), PMC_PROFILE
-    return None, None
+def lib_sha256() -> str:
+    return hashlib.sha256(open(rtmi.LIB_PATH, "rb").read()).hexdigest()
 
 
-SQ_PROFILE = os.path.join("profiles", "r1v9_sq_summary.json")
+def load_profile():
+    """The newest bench PMC profile whose library hash equals the loaded librtmi.so."""
+    sha = lib_sha256()
+    newest = None
+    for path in sorted(glob.glob(PMC_GLOB), key=os.path.getmtime):
+        try:
+            prof = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        newest = (os.path.relpath(path, ROOT), prof)
+        if prof.get("lib_sha256") == sha:
+            return newest[0], prof, True
+    return (newest[0], newest[1], False) if newest else (None, None, False)
 
 
-def pmc_valu_issue(params):
-    """Fraction of the VALU issue slots k_render used on this workload (SQ_INSTS_VALU of
-    the committed PMC pass over 1024 SIMDs x one wave-instruction per 2 cycles)."""
-    if (params.width, params.height, params.spp, params.spp_split) != DEFAULT_WORKLOAD:
-        return None
-    try:
-        c = json.load(open(os.path.join(ROOT, SQ_PROFILE)))["per_dispatch"]
-        cycles = c["GRBM_GUI_ACTIVE"] / 8.0  # summed over the 8 XCDs
-        return round(c["SQ_INSTS_VALU"] / (1024 * cycles / 2.0), 3)
-    except (OSError, ValueError, KeyError):
-        return None
+def roofline(geom, casts_per_launch: float, kernel_ms: float, default_workload: bool, kernel: str):
+    """VALU-issue roofline of the render kernel (k_render_ps on the default workload).
+
+    frac = VALU wave-instructions per launch (SQ_INSTS_VALU of the committed profile of the
+    same build and workload) / (kernel time from this run's HIP events x the chip's issue
+    peak: 1024 SIMDs x one wave-instruction per 2 cycles at 2.4 GHz).  The kernel is bound by
+    VALU issue: its HBM traffic is the 3 MB frame (profile), the triangle records are
+    scalar-cache resident.  Informational: the reference's brute-force flops (71 per
+    ray-triangle test) per second, and the HBM-algorithmic ratio the north
+    star names (36 B per triangle per cast as if streamed: not a bound on this kernel)."""
+    t = kernel_ms * 1e-3
+    n_tri = geom.n_tri
+    path, prof, match = load_profile() if default_workload else (None, None, False)
+    line = {"bound": "valu", "achieved": None, "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU wave-instr/s",
+            "frac": None, "traffic": None, "kernel": kernel,
+            "kernel_ms": round(kernel_ms, 4), "profile": path, "profile_matches_build": match}
+    if prof is not None and match:
+        ks = [k for k in prof["kernels"] if "k_render_ps" in k]
+        valu = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_INSTS_VALU", 0.0) for k in ks)
+        hbm = sum(prof["kernels"][k].get("hbm_bytes_per_dispatch", 0.0) for k in ks)
+        ren = [prof["kernels"][k] for k in ks if "k_render_ps" in k]
+        achieved = valu / t / 1e9
+        line.update({
+            "achieved": round(achieved, 1), "frac": round(achieved / VALU_ISSUE_PEAK_G, 4),
+            "traffic": int(hbm) if hbm else None,
+            "valu_insts_per_launch": valu,
+            "valu_insts_per_cast": round(valu / casts_per_launch, 1),
+            "pmc_clock_ghz": round(ren[0]["clock_ghz"], 3) if ren and "clock_ghz" in ren[0] else None,
+            "pmc_kernel_ms": round(sum(prof["kernels"][k].get("avg_ns", 0.0) for k in ks) * 1e-6, 4),
+        })
+        if line["pmc_clock_ghz"]:
+            line["frac_at_pmc_clock"] = round(valu / (1024 * line["pmc_clock_ghz"] * 1e9 * t / 2.0), 4)
+    useful = casts_per_launch * 71.0 * n_tri / t / 1e12
+    line["brute_force_tflops"] = round(useful, 2)
+    line["brute_force_frac_of_fp32"] = round(useful / VALU_PEAK_TFLOPS, 4)
+    b_cast = 36 * n_tri + 32
+    line["hbm_algorithmic_bytes_per_cast"] = b_cast
+    line["hbm_algorithmic_ratio"] = round(casts_per_launch * b_cast / t / 1e9 / HBM_PEAK_GBS, 3)
+    return line
 
 
 def cpu_baseline(geom, params, cam_pos, seconds):
-    """Time the CPU restatement (oracle/, OpenMP) on a bounded strip of the same frame."""
+    """Time the CPU restatement (oracle/, OpenMP) on a bounded strip of the same frame,
+    best of 3, and one thread on a 2-row strip."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
 
@@ -104,19 +153,16 @@ def cpu_baseline(geom, params, cam_pos, seconds):
     rows, y0 = 4, params.height // 2 - 2
     t0 = time.perf_counter()
     _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
-    dt = time.perf_counter() - t0
-    rate = casts / max(dt, 1e-9)
-    # scale the strip so that the timed sample takes about `seconds`
+    rate = casts / max(time.perf_counter() - t0, 1e-9)
     per_row = casts / rows
     rows = int(max(4, min(params.height, seconds * rate / max(per_row, 1.0))))
     y0 = max(0, params.height // 2 - rows // 2)
     best = None
-    for _ in range(1):
+    for _ in range(3):
         t0 = time.perf_counter()
         _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
-    # the 1-thread figure on a 2-row strip of the same frame
     oracle.set_threads(1)
     y1 = params.height // 2 - 1
     t0 = time.perf_counter()
@@ -129,10 +175,52 @@ def cpu_baseline(geom, params, cam_pos, seconds):
         "cores": threads,
         "kind": "port",
         "sample": f"rows {y0}..{y0 + rows - 1} of the {w}x{params.height}/{params.spp}-spp frame "
-                  f"({casts} ray casts, {best:.1f} s, OpenMP over rows)",
+                  f"({casts} ray casts, best of 3: {best:.2f} s, OpenMP over rows)",
         "value_1thread": round(casts1 / max(dt1, 1e-9) / 1e6, 3),
         "sample_1thread": f"rows {y1}..{y1 + 1} ({casts1} ray casts, {dt1:.2f} s, 1 thread)",
     }
+
+
+def parity_tiles(ctx, scene, geom, params, cam, cam_pos, image):
+    """8 full 32x32 tiles spread over the frame: the frame's pixels bit-exact vs the CPU
+    restatement, and the tile's ray casts (a separate GPU render of the tile) equal to its."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    op = oracle.params_from(params)
+    ocam = oracle.camera(cam_pos)
+    W, H = params.width, params.height
+    fx = [0.08, 0.45, 0.8, 0.25, 0.6, 0.92, 0.1, 0.5]
+    fy = [0.1, 0.15, 0.3, 0.45, 0.55, 0.7, 0.85, 0.95]
+    worst, exact, casts_ok, px = 0.0, True, True, 0
+    for a, b in zip(fx, fy):
+        x = min(W - TILE, int(a * W) // TILE * TILE)
+        y = min(H - TILE, int(b * H) // TILE * TILE)
+        ref, ref_casts = oracle.render(geom, ocam, op, (x, y, TILE, TILE))
+        got = image[y:y + TILE, x:x + TILE]
+        _, gpu_casts = rtmi.render(ctx, scene, cam, params, (x, y, TILE, TILE))
+        worst = max(worst, rtmi.metrics.mape_f(ref, got))
+        exact = exact and bool(np.array_equal(ref.view(np.uint32), got.view(np.uint32)))
+        casts_ok = casts_ok and gpu_casts == ref_casts
+        px += TILE * TILE
+    return {"mape_vs_cpu": worst, "bit_exact": exact, "ray_casts_equal": casts_ok, "tiles": len(fx),
+            "pixels": px, "frac_of_frame": round(px / (W * H), 4)}
+
+
+def make_workload(args, ctx):
+    scene_kind, preset, sampler, W, H, spp, split, cfg = WORKLOADS[args.workload]
+    W = args.width or W
+    H = args.height or H
+    spp = args.spp or spp
+    split = args.spp_split or split
+    if scene_kind == "cornell":
+        geom = rtmi.cornell_geometry(preset)
+        cam_pos = rtmi.CAMERAS["cornell"]
+    else:
+        geom = rtmi.obj_geometry(os.path.join(MODELS, scene_kind + ".obj"), scene_kind)
+        cam_pos = rtmi.CAMERAS[scene_kind]
+    params = rtmi.default_params(preset, width=W, height=H, spp=spp, spp_split=split)
+    return scene_kind, sampler, cfg, geom, cam_pos, params
 
 
 def main():
@@ -146,21 +234,36 @@ def main():
     dev = torch.device("cuda", local_rank)
 
     ctx = rtmi.Context(local_rank)
-    geom = rtmi.cornell_geometry(rtmi.RT_PRESET_CPU)
+    scene_kind, sampler, cfg, geom, cam_pos, params = make_workload(args, ctx)
     scene = rtmi.Scene(ctx, geom)
-    params = rtmi.default_params(rtmi.RT_PRESET_CPU, width=args.width, height=args.height,
-                                 spp=args.spp, spp_split=args.spp_split)
-    cam_pos = rtmi.CAMERAS["cornell"]
     cam = rtmi.camera(cam_pos)
 
     tiles = rtmi.tiles.rank_tiles(params.width, params.height, TILE, rank, world)
+    n_real = rtmi.tiles.rank_tile_count(params.width, params.height, TILE, rank, world)
     k = tiles.shape[0]
     casts = torch.zeros(1, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream(dev)
+    extra = []  # objects to close
 
-    def render(out):
-        rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(), casts.data_ptr(),
-                                 stream.cuda_stream)
+    if sampler == "sarsa":
+        rmap = rtmi.sarsa.RadianceMap(ctx, scene, 1984)
+        extra.append(rmap)
+        td = rtmi.dist.td_tensors(rmap, dev) if world > 1 else None
+
+        def render(out):
+            rtmi.dist.sarsa_frame(rmap, cam, params, tiles, n_real, TILE, out, casts, td)
+    elif sampler == "dqn":
+        Ws, bs = rtmi.dqn.synthetic_weights(geom.nn_vertices.size)
+        net = rtmi.dqn.Dqn(ctx, geom.nn_vertices, Ws, bs)
+        extra.append(net)
+
+        def render(out):
+            rtmi.dqn.render_tiles_device(ctx, scene, net, cam, params, tiles, TILE, out.data_ptr(),
+                                         casts.data_ptr(), stream.cuda_stream)
+    else:
+        def render(out):
+            rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(), casts.data_ptr(),
+                                     stream.cuda_stream)
 
     # two frame buffers: frame i+1 renders while frame i is all-gathered over RCCL
     pipe = rtmi.dist.FramePipeline(render, (k, TILE, TILE, 3), world, dev)
@@ -189,31 +292,23 @@ def main():
 
     kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_casts = int(casts.item())
-    stats = torch.tensor([elapsed, float(rank_casts), kernel_ms, float(rank_casts)],
-                         dtype=torch.float64, device=dev)
     if world > 1:
-        t_max = stats[0:1].clone()
+        t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        tot = stats[1:2].clone()
+        tot = torch.tensor([rank_casts], dtype=torch.int64, device=dev)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed, total_casts = float(t_max.item()), int(tot.item())
     else:
         total_casts = rank_casts
 
     frame = pipe.frame(args.steps - 1)
-    image = None
     if rank == 0:
         image = rtmi.tiles.assemble(frame.cpu().numpy(), params.width, params.height, TILE, world)
-
-    if rank == 0:
-        n_tri = geom.n_tri
-        b_cast = 36 * n_tri + 32  # algorithmic bytes per ray cast
-        casts_per_launch = rank_casts / args.steps
-        achieved_gbs = casts_per_launch * b_cast / (kernel_ms * 1e-3) / 1e9
-        valu_tflops = casts_per_launch * n_tri * 71 / (kernel_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic(params)
+        default = args.workload == "cornell" and (params.width, params.height, params.spp, params.spp_split) == (
+            512, 512, 256, 64)
         line = {
-            "metric": "Mrays/sec (Cornell 512^2 256spp ray casts)",
+            "metric": f"Mrays/sec ({WORKLOADS[args.workload][0]} {params.width}^2 {params.spp}spp ray casts)"
+            if params.width == params.height else f"Mrays/sec ({args.workload} ray casts)",
             "value": round(total_casts / elapsed / 1e6, 2),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -224,62 +319,37 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "procedural Cornell box of the reference (CPU-engine preset), Philox RNG seed 1984",
+            "data": ("procedural Cornell box of the reference (CPU-engine preset)" if scene_kind == "cornell"
+                     else f"Models/{scene_kind}.obj of the reference (GPU-engine preset)")
+            + ", Philox RNG seed 1984" + (", synthetic He-normal DQN weights" if sampler == "dqn" else ""),
             "config": {
-                "workload": "cornell_512x512_256spp",
+                "workload": f"{scene_kind}_{params.width}x{params.height}_{params.spp}spp"
+                + ("" if sampler == "uniform" else f"_{sampler}"),
+                "baseline_config": cfg,
                 "width": params.width, "height": params.height, "spp": params.spp,
-                "max_bounces": params.max_bounces, "hit_rule": "cpu_object", "sampler": "uniform",
-                "spp_split": params.spp_split, "tile": TILE, "parallelism": f"tiles{world}",
-                "triangles": n_tri,
+                "max_bounces": params.max_bounces,
+                "hit_rule": "cpu_object" if params.hit_rule == rtmi.RT_HIT_RULE_CPU else "gpu_engine",
+                "sampler": sampler, "spp_split": params.spp_split, "tile": TILE, "parallelism": f"tiles{world}",
+                "triangles": geom.n_tri,
             },
             "ray_casts_per_step": total_casts // args.steps,
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved_gbs, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel": "k_render<0,0,0>",
-                "kernel_ms": round(kernel_ms, 4),
-                "bytes_per_cast": b_cast,
-                "valu_tflops_est": round(valu_tflops, 2),
-                "valu_frac_est": round(valu_tflops / VALU_PEAK_TFLOPS, 4),
-                "valu_issue_frac_pmc": pmc_valu_issue(params),
-                "valu_issue_source": SQ_PROFILE,
-            },
+            "roofline": roofline(geom, rank_casts / args.steps, kernel_ms, default, {
+                "uniform": "k_render_ps<0,0>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal>",
+                "sarsa": "k_sarsa_render + k_sarsa_apply", "dqn": "k_dqn_mlp + k_dqn_bounce (wavefront)"}[sampler]),
         }
-        if not args.no_parity:
-            line["parity"] = parity_window(geom, params, cam_pos, image)
-        if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
+        if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
+            line["parity"] = parity_tiles(ctx, scene, geom, params, cam, cam_pos, image)
+        if args.cpu_seconds > 0 and world == 1 and sampler == "uniform":  # the CPU baseline is an N=1 figure
             line["cpu_baseline"] = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
         print(json.dumps(line), flush=True)
 
+    for o in extra:
+        o.close()
     scene.close()
     ctx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def parity_window(geom, params, cam_pos, image):
-    """MAPE and bit-exactness of the GPU frame vs the CPU restatement on 4 windows."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle
-
-    op = oracle.params_from(params)
-    ocam = oracle.camera(cam_pos)
-    wins = [(96, 64, 16, 16), (248, 248, 16, 16), (400, 300, 16, 16), (40, 440, 16, 16)]
-    worst, exact = 0.0, True
-    for (x, y, w, h) in wins:
-        if x + w > params.width or y + h > params.height:
-            continue
-        ref, _ = oracle.render(geom, ocam, op, (x, y, w, h))
-        got = image[y:y + h, x:x + w]
-        worst = max(worst, rtmi.metrics.mape_f(ref, got))
-        exact = exact and bool(np.array_equal(ref.view(np.uint32), got.view(np.uint32)))
-    return {"mape_vs_cpu": worst, "bit_exact": exact, "windows": len(wins), "window_px": 16}
 
 
 if __name__ == "__main__":

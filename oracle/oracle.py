@@ -309,6 +309,9 @@ class Sarsa:
         L.orc_sarsa_nearest.argtypes = [VP, _FP, _FP, ctypes.c_int, _IP]
         L.orc_render_sarsa.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
                                        _FP, ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_sarsa_td_rect.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_uint32)]
         get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
         self._keep = [np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32),
                       np.ascontiguousarray(get("albedo"), np.float32),
@@ -352,6 +355,17 @@ class Sarsa:
         out = np.zeros(p.shape[0], np.int32)
         self._L.orc_sarsa_nearest(self._h, _f(p), _f(n_), p.shape[0], _i(out))
         return out
+
+    def td_rect(self, cam: OrcCamera, params: OrcParams, rect):
+        """(int64 sums, uint32 counts), each (n_volumes * 144,): the TD accumulators that the
+        rectangle (x, y, w, h) of the current frame adds (the frame is not applied)."""
+        n = self.n_volumes * 144
+        s = np.zeros(n, np.int64)
+        c = np.zeros(n, np.uint32)
+        self._L.orc_sarsa_td_rect(self._h, ctypes.byref(cam), ctypes.byref(params), *rect,
+                                  s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                  c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
+        return s, c
 
     def render(self, cam: OrcCamera, params: OrcParams, frames: int = 1):
         out = np.zeros((params.height, params.width, 3), np.float32)

@@ -1424,6 +1424,41 @@ static void sarsa_apply(orc_sarsa *m) {
     }
 }
 
+/* The TD accumulators one rectangle of the current frame adds (the frame is not applied):
+ * out_sum/out_cnt get this rectangle's n_vol x 144 fixed-point target sums and counts, and
+ * the map's accumulators are cleared again.  The rectangles of a frame's tiles add up to the
+ * whole frame's accumulators (the multi-GPU exchange, rtmi.dist.sum_td). */
+ORC_API int orc_sarsa_td_rect(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int x0, int y0, int w,
+                              int h, int64_t *out_sum, uint32_t *out_cnt) {
+    float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    orc_params pg = *p;
+    pg.preset = 1;
+    uint32_t base = m->frames * (uint32_t)p->spp;
+    uint64_t total = 0;
+    #pragma omp parallel for schedule(dynamic, 1) reduction(+:total)
+    for (int py = y0; py < y0 + h; py++) {
+        for (int px = x0; px < x0 + w; px++) {
+            uint32_t pix = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+            uint64_t casts = 0;
+            for (int s = 0; s < p->spp; s++) {
+                float r1, r2;
+                draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
+                v3 o, d;
+                camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                (void)sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
+            }
+            total += casts;
+        }
+    }
+    size_t n = (size_t)m->n_vol * 144;
+    memcpy(out_sum, m->sum, sizeof(int64_t) * n);
+    memcpy(out_cnt, m->cnt, sizeof(uint32_t) * n);
+    memset(m->sum, 0, sizeof(int64_t) * n);
+    memset(m->cnt, 0, sizeof(uint32_t) * n);
+    return (int)(total > 0);
+}
+
 /* `frames` frames of the whole width x height image (GPU-engine preset); out_rgb = last frame */
 ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int frames, float *out_rgb,
                              uint64_t *out_casts) {

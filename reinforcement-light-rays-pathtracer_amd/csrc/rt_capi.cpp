@@ -54,8 +54,7 @@ struct rt_ctx {
     rt::BlockDesc* d_blocks = nullptr;
     int n_blocks = 0;
     int blocks_cap = 0;
-    // per-wave candidate masks of the CPU-preset primary-ray phase (RenderLaunch::cull);
-    // one render at a time per context (the contexts' one-thread rule)
+    // per-wave candidate masks of rt_cull_masks_device (RenderLaunch::cull)
     unsigned long long* d_cull = nullptr;
     size_t cull_cap = 0;
 };
@@ -558,9 +557,7 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
         a.out_pitch = w;
         a.out = d_out;
         a.casts = d_casts;
-        rc = rt::ctx_cull(ctx, &a);
-        if (rc != RT_OK) e = hipErrorOutOfMemory;
-        if (e == hipSuccess) e = rt::launch_render(a, 0);
+        e = rt::launch_render(a, 0);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, out_bytes, hipMemcpyDeviceToHost);
@@ -603,8 +600,6 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     a.out_pitch = tile_size;
     a.out = d_out;
     a.casts = reinterpret_cast<unsigned long long*>(d_casts);
-    rc = rt::ctx_cull(ctx, &a);
-    if (rc != RT_OK) return rc;
     RT_HIP(rt::launch_render(a, (hipStream_t)stream));
     return RT_OK;
 }
@@ -688,15 +683,6 @@ int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* ca
     (void)hipFree(d_blocks);
     if (e != hipSuccess) return fail(RT_E_HIP, "rt_cull_masks_device: %s", hipGetErrorString(e));
     *n_words = words;
-    return RT_OK;
-}
-
-// debugging aid: the context's cull workspace as the last render left it
-int rt_debug_cull_workspace(rt_ctx* ctx, uint64_t* out, int64_t n_words) {
-    if (!ctx || !out) return fail(RT_E_INVALID, "NULL argument");
-    if ((size_t)n_words > ctx->cull_cap) return fail(RT_E_INVALID, "workspace holds %zu words", ctx->cull_cap);
-    RT_HIP(hipDeviceSynchronize());
-    RT_HIP(hipMemcpy(out, ctx->d_cull, sizeof(uint64_t) * (size_t)n_words, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

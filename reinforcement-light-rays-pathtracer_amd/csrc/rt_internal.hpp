@@ -75,8 +75,8 @@ struct RenderLaunch {
     unsigned long long* casts;
     uint32_t sample_base;  // first RNG sample index (SARSA: frame * spp); 0 elsewhere
     int use_filter;        // 1: two-phase closest hit (filter records valid for this launch)
-    // CPU-preset primary-ray phase (k_render_ps): workspace of kRenderCullWords 64-bit
-    // candidate masks per wave (n_blocks * split * 4 waves); nullptr: no primary phase
+    // k_cull_ps (diagnostic): kRenderCullWords 64-bit candidate masks per wave
+    // (n_blocks * split * 4 waves); unused by the renders
     unsigned long long* cull;
 };
 constexpr int kRenderCullWords = 4;  // candidate masks per wave: scenes of <= 256 triangles

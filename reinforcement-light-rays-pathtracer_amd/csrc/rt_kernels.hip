@@ -289,16 +289,12 @@ __device__ __forceinline__ uint64_t tri_mask(int n, int g) {
 // cull[(b * 4 + w) * kRenderCullWords + g], bit j = triangle 64 g + j may be the hit of a
 // camera ray through the wave's pixel rectangle (rect_cull, rt_trace.hpp).  Same grid
 // and lane -> pixel mapping as k_render_ps.
+// Candidate masks of the wave's pixel rectangle (the valid lanes' pixels): bit j of
+// cm[g] = triangle 64 g + j may be the hit of a camera ray through the rectangle
+// (rect_cull); never a bit past the scene.  All lanes of the wave take part.
 template <int RULE>
-__global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
-    const int lg = a.split_log2;
-    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
-    const int part = blockIdx.x & (a.split - 1);
-    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
-    const int lane = threadIdx.x & 63;
-    const int px = blk.px0 + (q & 15);
-    const int py = blk.py0 + (q >> 4);
-    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+__device__ __forceinline__ void wave_candidates(const RenderLaunch& a, bool valid, int px, int py, int lane,
+                                                uint64_t* cm) {
     int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
     int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
 #pragma unroll
@@ -308,15 +304,10 @@ __global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
         y0 = min(y0, __shfl_xor(y0, off, 64));
         y1 = max(y1, __shfl_xor(y1, off, 64));
     }
-    unsigned long long* w = a.cull + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRenderCullWords;
-    if (x1 < 0) {  // no pixel of the image in this wave
-        if (lane < kRenderCullWords) w[lane] = 0ull;
-        return;
-    }
     const CamRect c = make_cam_rect(a.cam_x, a.cam_y, a.cam_z, a.cos_y, a.sin_y, a.width, a.height, a.t_scale,
-                                    x0, x1, y0, y1);
+                                    __builtin_amdgcn_readfirstlane(x0), __builtin_amdgcn_readfirstlane(x1),
+                                    __builtin_amdgcn_readfirstlane(y0), __builtin_amdgcn_readfirstlane(y1));
     const int n_tri = a.scene.n_tri;
-    unsigned long long mine = 0ull;
 #pragma unroll
     for (int g = 0; g < kRenderCullWords; ++g) {
         const int i = g * 64 + lane;
@@ -328,14 +319,39 @@ __global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
         const bool cull = rect_cull<RULE>(a.scene.filt + (size_t)(in_range ? i : 0) * kFiltF4, c);
         const bool keep = in_range && !cull;
 #endif
-        const unsigned long long m = __ballot(keep) & tri_mask(n_tri, g);
-        if (lane == g) mine = m;
+        cm[g] = __ballot(keep) & tri_mask(n_tri, g);
     }
-    if (lane < kRenderCullWords) w[lane] = mine;
+}
+
+// The masks alone, as k_render_ps computes them, into a.cull (wave w of workgroup b at
+// words (b * 4 + w) * kRenderCullWords ..): the diagnostic rt_cull_masks_device.
+template <int RULE>
+__global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    const int part = blockIdx.x & (a.split - 1);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int lane = threadIdx.x & 63;
+    const int px = blk.px0 + (q & 15);
+    const int py = blk.py0 + (q >> 4);
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    uint64_t cm[kRenderCullWords];
+    if (__ballot(valid) == 0ull) {
+        for (int g = 0; g < kRenderCullWords; ++g) cm[g] = 0ull;
+    } else {
+        wave_candidates<RULE>(a, valid, px, py, lane, cm);
+    }
+    unsigned long long* w = a.cull + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRenderCullWords;
+    if (lane < kRenderCullWords) {
+        uint64_t v = cm[0];
+#pragma unroll
+        for (int g = 1; g < kRenderCullWords; ++g) v = (lane == g) ? cm[g] : v;
+        w[lane] = v;
+    }
 }
 
 #ifndef RT_PS_MIN_WAVES
-#define RT_PS_MIN_WAVES 1
+#define RT_PS_MIN_WAVES 7  // 72 VGPRs: 7 waves per SIMD (4.84 vs 4.91 ms at 75 VGPRs, profiles/r2c_ab.log)
 #endif
 template <int SAMPLER, int RULE>
 __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
@@ -360,22 +376,9 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
     float* const slots = s_ps + (size_t)(threadIdx.x >> 6) * pc * kPsFields * 64 + lane;
     const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
 
-#ifdef RT_DEBUG_POISON_LDS
-    for (int k = 0; k < pc * kPsFields; ++k) slots[k * 64] = __int_as_float(RT_DEBUG_POISON_LDS);
-#endif
-    // ---- candidate triangles of the wave's pixel rectangle (k_cull_ps) ----
+    // ---- candidate triangles of the wave's pixel rectangle (rect_cull, rt_cull.hpp) ----
     uint64_t cm[kRenderCullWords];
-    {
-#ifdef RT_DEBUG_ACQUIRE_CULL
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#endif
-        const unsigned long long* w = a.cull + ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * kRenderCullWords;
-#pragma unroll
-        for (int g = 0; g < kRenderCullWords; ++g)
-            cm[g] = (__builtin_amdgcn_readfirstlane((uint32_t)w[g]) |
-                     ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(w[g] >> 32)) << 32)) &
-                    tri_mask(a.scene.n_tri, g);  // never a triangle past the scene
-    }
+    wave_candidates<RULE>(a, valid, px, py, lane, cm);
 
     // ---- phase P: primary rays of the lane's samples ----
     unsigned n_casts = 0;
@@ -397,11 +400,7 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
             while (m != 0ull) {
                 const int b = __builtin_ctzll(m);
                 m &= m - 1ull;
-#ifdef RT_DEBUG_VECTOR_ISECT
-                exact_one<RULE>(a.scene.isect, g * 64 + b, cam, nDx, nDy, nDz, h);
-#else
                 exact_one_c<RULE>(isect, g * 64 + b, cam, nDx, nDy, nDz, h);
-#endif
             }
         }
         n_casts += valid ? 1u : 0u;
@@ -426,9 +425,6 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
         sl[4 * 64] = __int_as_float(code);
     }
 
-#ifdef RT_DEBUG_OUT
-    const unsigned n_p = n_casts;
-#endif
     // ---- phase S: bounces ----
     f3 acc = make3(0.0f, 0.0f, 0.0f);
     int k = 0;          // next slot
@@ -557,17 +553,9 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
     if (valid && chunk == 0) {
         const float fs = (float)a.spp;
         float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
-#ifdef RT_DEBUG_OUT
-        int codes = 0;
-        for (int kk = 0; kk < pc; ++kk) codes = codes * 41 + (__float_as_int(slots[(kk * kPsFields + 4) * 64]) + 1);
-        dst[0] = (float)(uint32_t)(cm[0] & 0xffffffu);
-        dst[1] = (float)(uint32_t)((cm[0] >> 24) & 0xffffffu);
-        dst[2] = (float)(codes & 0xffffff) + 0.0f * (float)n_p;
-#else
         dst[0] = tot.x / fs;
         dst[1] = tot.y / fs;
         dst[2] = tot.z / fs;
-#endif
     }
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
@@ -634,13 +622,9 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
 
 template <int PRESET, int SAMPLER, int RULE>
 static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
-    if (PRESET == 0 && RT_PS && a.use_filter && a.cull != nullptr && a.scene.n_tri <= 64 * kRenderCullWords) {
+    if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= 64 * kRenderCullWords) {
         const size_t ps_lds = (size_t)4 * a.per_chunk * kPsFields * 64 * sizeof(float);
         if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
-            hipLaunchKernelGGL((k_cull_ps<RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a);
-#ifdef RT_DEBUG_SYNC_CULL
-            (void)hipStreamSynchronize(stream);
-#endif
             hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256),
                                ps_lds, stream, a);
             return;
