@@ -107,7 +107,18 @@ int rt_cornell_geometry(int variant, float* tri_v /* n_surf x 9 */, float* albed
  * GPU/objects/object_importer.cu:8-412 (scale 2, (v1,v3,v2) order, per-scene materials and
  * lights, lights_in_obj for complex_light_room).  `scene_kind` selects the hard-coded
  * material/light block: 0 generic (white 0.75, no lights), 1 door_room, 2 archway,
- * 3 complex_light_room.  Two-pass: call with NULL arrays to get counts. */
+ * 3 complex_light_room.  Two-pass: call with NULL arrays to get counts.
+ * door_room variants: scene_kind = 1 | (bits << 8), the blocks the reference comments in
+ * and out by hand (object_importer.cu).  0 = the door-room lights of :214-237, the red
+ * material of :152-155 on triangles 24-35 and the blue of :161-163 on 12-23: the scene of
+ * the thesis's door-room comparison renders (Images/door_room/default_128spp_50avg.png:
+ * image mean and average path length match, tools/door_variants.py).  RT_DOOR_WHITE_DOOR
+ * drops the red material (commented at HEAD), RT_DOOR_NO_BLUE the blue (active at HEAD),
+ * RT_DOOR_ARCHWAY_LIGHTS uses the lights active at HEAD (:240-271, the archway's, outside
+ * this room: a black image) instead of the door-room lights (commented at HEAD). */
+#define RT_DOOR_WHITE_DOOR 1
+#define RT_DOOR_NO_BLUE 2
+#define RT_DOOR_ARCHWAY_LIGHTS 4
 int rt_obj_geometry(const char* path, int scene_kind, float* tri_v, float* albedo, int* n_surf,
                     float* light_v, float* emission, int32_t* light_group, int* n_light,
                     float* nn_vertices /* Scene::vertices order, may be NULL */, int* n_nn_floats);

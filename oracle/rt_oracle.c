@@ -719,6 +719,11 @@ typedef struct {
     int n_in, h1, h2, h3, n_out;
     const float *W[4], *b[4]; /* row-major [out][in] */
     const float *verts;       /* n_in: Scene::vertices */
+    /* bf16 arithmetic, computed once per network by dqn_prepare (the same values the
+     * per-call evaluation gives): the folded layer 0 {c0, S0, S1, S2} per output and the
+     * bf16-rounded weights of layers 1-3 */
+    float *fold;
+    float *Wb[4];
 } orc_dqn;
 
 static float bf16_round(float f) {
@@ -731,19 +736,44 @@ static float bf16_round(float f) {
     return r;
 }
 
+/* the bf16 path's per-network constants (orc_dqn.fold, .Wb) */
+static void dqn_prepare(orc_dqn *net) {
+    net->fold = (float *)malloc(sizeof(float) * 4 * (size_t)net->h1);
+    for (int o = 0; o < net->h1; o++) {
+        const float *w = net->W[0] + (size_t)o * net->n_in;
+        double c0 = (double)net->b[0][o], S[3] = {0.0, 0.0, 0.0};
+        for (int i = 0; i < net->n_in; i++) {
+            c0 += (double)w[i] * (double)net->verts[i];
+            S[i % 3] += (double)w[i];
+        }
+        net->fold[4 * o + 0] = (float)c0;
+        net->fold[4 * o + 1] = (float)S[0];
+        net->fold[4 * o + 2] = (float)S[1];
+        net->fold[4 * o + 3] = (float)S[2];
+    }
+    int dims[5] = {net->n_in, net->h1, net->h2, net->h3, net->n_out};
+    net->Wb[0] = NULL;
+    for (int l = 1; l < 4; l++) {
+        size_t n = (size_t)dims[l] * dims[l + 1];
+        float *w = (float *)malloc(sizeof(float) * n);
+        for (size_t i = 0; i < n; i++) w[i] = bf16_round(net->W[l][i]);
+        net->Wb[l] = w;
+    }
+}
+
+static void dqn_release(orc_dqn *net) {
+    free(net->fold);
+    for (int l = 1; l < 4; l++) free(net->Wb[l]);
+}
+
 static void dqn_forward_one(const orc_dqn *net, const float *loc, int bf16, float *q_out, float *scratch) {
     int dims[5] = {net->n_in, net->h1, net->h2, net->h3, net->n_out};
     float *in = scratch, *out = scratch + 1024;
     int l0 = 0;
     if (bf16) {
         for (int o = 0; o < net->h1; o++) {
-            const float *w = net->W[0] + (size_t)o * net->n_in;
-            double c0 = (double)net->b[0][o], S[3] = {0.0, 0.0, 0.0};
-            for (int i = 0; i < net->n_in; i++) {
-                c0 += (double)w[i] * (double)net->verts[i];
-                S[i % 3] += (double)w[i];
-            }
-            const float cf = (float)c0, s0 = (float)S[0], s1 = (float)S[1], s2 = (float)S[2];
+            const float cf = net->fold[4 * o], s0 = net->fold[4 * o + 1], s1 = net->fold[4 * o + 2],
+                        s2 = net->fold[4 * o + 3];
             float h = cf - fmaf(s2, loc[2], fmaf(s1, loc[1], s0 * loc[0]));
             h = h > 0.0f ? h : 0.0f;
             in[o] = bf16_round(h);
@@ -756,11 +786,8 @@ static void dqn_forward_one(const orc_dqn *net, const float *loc, int bf16, floa
         const float *W = net->W[l], *b = net->b[l];
         for (int o = 0; o < dims[l + 1]; o++) {
             double acc = 0.0;
-            const float *w = W + (size_t)o * dims[l];
-            for (int i = 0; i < dims[l]; i++) {
-                float wv = bf16 ? bf16_round(w[i]) : w[i];
-                acc += (double)wv * (double)in[i];
-            }
+            const float *w = (bf16 ? net->Wb[l] : W) + (size_t)o * dims[l];
+            for (int i = 0; i < dims[l]; i++) acc += (double)w[i] * (double)in[i];
             float v = (float)acc + b[o];
             v = v > 0.0f ? v : 0.0f;
             out[o] = (bf16 && l < 3) ? bf16_round(v) : v;
@@ -773,7 +800,9 @@ static void dqn_forward_one(const orc_dqn *net, const float *loc, int bf16, floa
 ORC_API void orc_dqn_forward(int n_in, int h1, int h2, int h3, int n_out, const float *const *W,
                              const float *const *b, const float *verts, const float *loc, int n, int bf16,
                              float *q) {
-    orc_dqn net = {n_in, h1, h2, h3, n_out, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts};
+    orc_dqn net = {n_in, h1, h2, h3, n_out, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts,
+                   NULL, {NULL, NULL, NULL, NULL}};
+    if (bf16) dqn_prepare(&net);
     #pragma omp parallel
     {
         float *scratch = (float *)malloc(sizeof(float) * 2048);
@@ -781,6 +810,7 @@ ORC_API void orc_dqn_forward(int n_in, int h1, int h2, int h3, int n_out, const 
         for (int r = 0; r < n; r++) dqn_forward_one(&net, loc + (size_t)r * 3, bf16, q + (size_t)r * n_out, scratch);
         free(scratch);
     }
+    if (bf16) dqn_release(&net);
 }
 
 static void chiu_map_t(float x, float y, float *xr, float *yr, float *zr) {
@@ -929,7 +959,9 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
                            float *out_rgb, uint64_t *out_casts) {
     orc_scene sc;
     scene_init(&sc, tri, albedo, n_surf, emission, light_group, n_light);
-    orc_dqn net = {n_in, h1, h2, h3, 144, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts};
+    orc_dqn net = {n_in, h1, h2, h3, 144, {W[0], W[1], W[2], W[3]}, {b[0], b[1], b[2], b[3]}, verts,
+                   NULL, {NULL, NULL, NULL, NULL}};
+    if (bf16) dqn_prepare(&net);
     float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
     float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
     uint64_t total_casts = 0;
@@ -978,6 +1010,7 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
         free(scratch);
     }
     free(sc.normal);
+    if (bf16) dqn_release(&net);
     if (out_casts) *out_casts = total_casts;
     return 0;
 }

@@ -180,7 +180,10 @@ void add_light(Built& b, V4 p, V4 q, V4 r, float e) {
 
 // build_surfaces / build_area_lights / build_surfaces_and_lights
 // (GPU/objects/object_importer.cu:93-185, 210-314, 318-412)
-int build_obj(const ObjData& o, int kind, Built* b) {
+// kind: 0 generic, 1 door_room, 2 archway, 3 complex_light_room; for door_room the bits
+// of `variant` select among the blocks the reference leaves commented or active at HEAD
+// (RT_DOOR_* in rtmi.h).
+int build_obj(const ObjData& o, int kind, int variant, Built* b) {
     const int nv = (int)(o.v.size() / 3);
     float max_pos[3] = {0.f, 0.f, 0.f}, min_pos[3] = {0.f, 0.f, 0.f};  // start at 0 as the reference
     for (int i = 0; i < 3; ++i)
@@ -213,8 +216,16 @@ int build_obj(const ObjData& o, int kind, Built* b) {
             if (kind == 2) {  // archway materials active at HEAD (:157-163)
                 if (i > 80) { col[0] = 0.75f; col[1] = 0.15f; col[2] = 0.15f; }
                 if (11 < i && i < 24) { col[0] = 0.15f; col[1] = 0.15f; col[2] = 0.75f; }
-            } else if (kind == 1) {  // door_room: the blue block of :161-163
-                if (11 < i && i < 24) { col[0] = 0.15f; col[1] = 0.15f; col[2] = 0.75f; }
+            } else if (kind == 1) {  // door_room
+                // red door (:152-155, commented at HEAD), then the blue block (:161-163, active).
+                // Both on: the scene of the thesis's 128-spp comparison renders
+                // (Images/door_room/default_128spp_50avg.png: mean and path length match).
+                if (!(variant & RT_DOOR_WHITE_DOOR) && i > 23 && i < 36) {
+                    col[0] = 0.75f; col[1] = 0.15f; col[2] = 0.15f;
+                }
+                if (!(variant & RT_DOOR_NO_BLUE) && 11 < i && i < 24) {
+                    col[0] = 0.15f; col[1] = 0.15f; col[2] = 0.75f;
+                }
             } else if (kind == 3) {  // complex_light_room (:382-389)
                 col[0] = col[1] = col[2] = 0.9f;
                 if (i >= 0 && i <= 7) col[0] = col[1] = col[2] = 0.1f;
@@ -233,7 +244,7 @@ int build_obj(const ObjData& o, int kind, Built* b) {
     if (kind == 1 || kind == 2) {
         const float l = 2.f;
         std::vector<V4> quad;
-        if (kind == 1) {  // door room block, commented at HEAD (:216-237)
+        if (kind == 1 && !(variant & RT_DOOR_ARCHWAY_LIGHTS)) {  // door room block, commented at HEAD (:216-237)
             V4 I = v4((6.3f * l) / 8, (l * 6.f) / 8, 1.499f * l);
             V4 J = v4((6.3f * l) / 8, 0, 1.499f * l);
             V4 K = v4((2.58f * l) / 8, (l * 6.f) / 8, 1.499f * l);
@@ -322,12 +333,14 @@ int rt_obj_geometry(const char* path, int scene_kind, float* tri_v, float* albed
                     float* light_v, float* emission, int32_t* light_group, int* n_light,
                     float* nn_vertices, int* n_nn_floats) {
     if (!path || !n_surf || !n_light) return rt::set_error(RT_E_INVALID, "NULL argument");
-    if (scene_kind < 0 || scene_kind > 3) return rt::set_error(RT_E_INVALID, "bad scene_kind");
+    const int kind = scene_kind & 0xff, variant = scene_kind >> 8;
+    if (kind < 0 || kind > 3) return rt::set_error(RT_E_INVALID, "bad scene_kind");
+    if (variant != 0 && (kind != 1 || (variant & ~7) != 0)) return rt::set_error(RT_E_INVALID, "bad variant bits");
     ObjData o;
     int rc = parse_obj(path, &o);
     if (rc != RT_OK) return rc;
     Built b;
-    rc = build_obj(o, scene_kind, &b);
+    rc = build_obj(o, kind, variant, &b);
     if (rc != RT_OK) return rc;
     const int ns = (int)(b.tri.size() / 9), nl = (int)(b.light.size() / 9);
     if (tri_v || albedo || light_v || emission || light_group) {

@@ -2,7 +2,9 @@
 // default path tracing) written against the drop-in facade: Cornell box,
 // Camera(0,0,-3,1), draw_default_path_tracing, SDL_SaveImage.
 //
-//   ./build/cornell_demo [out.bmp] [spp]
+//   ./build/cornell_demo [out.bmp] [spp] [frames]
+// With frames > 1 the frame loop of CPU/main.cpp:85-131 runs that many times (same
+// camera): the facade keeps one context and device scene for all of them.
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -18,6 +20,7 @@ using namespace rtmi;
 int main(int argc, char** argv) {
     const char* out = argc > 1 ? argv[1] : "render.bmp";
     const int spp = argc > 2 ? atoi(argv[2]) : 16;
+    const int frames = argc > 3 ? atoi(argv[3]) : 1;
     SDLScreen screen(512, 512, false);
 
     std::vector<Surface> surfaces_load;
@@ -31,12 +34,15 @@ int main(int argc, char** argv) {
     for (auto& l : light_planes_load) light_planes.push_back(&l);
 
     try {
-        draw_default_path_tracing(screen, camera, light_planes, surfaces, spp);
+        for (int f = 0; f < frames && screen.NoQuitMessageSDL(); ++f) {
+            draw_default_path_tracing(screen, camera, light_planes, surfaces, spp);
+            screen.SDL_Renderframe();
+        }
     } catch (const std::exception& e) {
         fprintf(stderr, "render failed: %s\n", e.what());
         return 1;
     }
-    screen.SDL_Renderframe();
+    printf("frames %d, scene uploads %d\n", screen.frames_presented, default_path_tracer().scene_uploads());
     screen.SDL_SaveImage(out);
     screen.kill_screen();
     printf("wrote %s\n", out);

@@ -38,6 +38,7 @@ class PathTracer {
         if (rt_scene_create(ctx_, a.tri.data(), a.albedo.data(), a.n_surf(), a.light.data(), a.emission.data(),
                             a.light_group.data(), a.n_light(), &scene_) != RT_OK)
             throw std::runtime_error(rt_last_error());
+        ++uploads_;
     }
 
     // renders the whole frame into screen.buffer; returns the number of ray casts
@@ -53,19 +54,37 @@ class PathTracer {
     }
 
     const std::vector<float>& radiance() const { return rgb_; }
+    int scene_uploads() const { return uploads_; }
 
    private:
     rt_ctx* ctx_ = nullptr;
     rt_scene* scene_ = nullptr;
     std::vector<float> rgb_;
+    int uploads_ = 0;
 };
 
 // The CPU engine's entry point: CPU preset semantics (cap 2, emission of the plane,
 // hit rule of the CPU object), SAMPLES_PER_PIXEL 16, FOCAL_LENGTH = screen height.
+// The reference calls it once per frame (CPU/main.cpp:85-131, `while NoQuitMessageSDL`):
+// one PathTracer (context + device scene) lives for the process and the scene is
+// uploaded again only when the surfaces or lights passed in change.
+inline PathTracer& default_path_tracer() {
+    // never destroyed: a device context must not outlive the HIP runtime's own teardown
+    static PathTracer* pt = new PathTracer(0);
+    return *pt;
+}
+
 inline void draw_default_path_tracing(SDLScreen screen, Camera& camera, std::vector<AreaLightPlane*> light_planes,
                                       std::vector<Surface*> surfaces, int spp = 16) {
-    PathTracer pt(0);
-    pt.set_scene(flatten(surfaces, light_planes));
+    static SceneArrays uploaded;
+    static bool have_scene = false;
+    PathTracer& pt = default_path_tracer();
+    SceneArrays a = flatten(surfaces, light_planes);
+    if (!have_scene || !a.same_as(uploaded)) {
+        pt.set_scene(a);
+        uploaded = std::move(a);
+        have_scene = true;
+    }
     rt_params p;
     rt_params_default(RT_PRESET_CPU, &p);
     p.width = screen.width;

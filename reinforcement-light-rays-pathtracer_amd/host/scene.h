@@ -90,6 +90,10 @@ struct SceneArrays {
     std::vector<int32_t> light_group;
     int n_surf() const { return (int)(tri.size() / 9); }
     int n_light() const { return (int)(light.size() / 9); }
+    bool same_as(const SceneArrays& o) const {
+        return tri == o.tri && albedo == o.albedo && light == o.light && emission == o.emission &&
+               light_group == o.light_group;
+    }
 };
 
 inline void push_tri(std::vector<float>& dst, const Triangle& t) {

@@ -103,14 +103,21 @@ def scene_image_stats(ref):
     except ImportError:
         return
     stats = {}
-    for scene in ("door_room", "archway", "complex_light"):
-        p = os.path.join(ref, "Images", scene, "reference.png")
+    # (key, file): the 4096-spp reference of each scene, and the door room's 128-spp
+    # default render (the thesis's comparison renders of that room were made of this scene;
+    # its reference.png was made with other settings)
+    files = [(s, f"Images/{s}/reference.png") for s in ("door_room", "archway", "complex_light")]
+    files += [("door_room_default_128spp", "Images/door_room/default_128spp_50avg.png"),
+              ("door_room_sarsa_128spp", "Images/door_room/sarsa_128_spp_avg_pl_5_max_pl_80.png")]
+    for key, rel in files:
+        p = os.path.join(ref, rel)
+        if not os.path.exists(p):
+            continue
         a = np.asarray(Image.open(p).convert("RGB"), np.float64)
         h, w, _ = a.shape
         b = 45
         blocks = a[: h // b * b, : w // b * b].reshape(h // b, b, w // b, b, 3).mean(axis=(1, 3))
-        stats[scene] = {"file": f"Images/{scene}/reference.png", "shape": [h, w], "block": b,
-                        "means": blocks.round(4).tolist()}
+        stats[key] = {"file": rel, "shape": [h, w], "block": b, "means": blocks.round(4).tolist()}
     with open(os.path.join(HERE, "scenes_ref_stats.json"), "w") as f:
         json.dump(stats, f)
 

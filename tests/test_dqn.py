@@ -127,7 +127,7 @@ def test_sampler_bit_exact(rtmi_mod, oracle_mod, gpu_ctx):
 def test_dqn_render_statistical(rtmi_mod, oracle_mod, gpu_ctx):
     g = door(rtmi_mod)
     W, b = trained(rtmi_mod)
-    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16, max_bounces=20)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16)  # 80 bounces
     rect = (48, 48, 32, 32)
     cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
     with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
@@ -136,13 +136,74 @@ def test_dqn_render_statistical(rtmi_mod, oracle_mod, gpu_ctx):
     assert np.array_equal(img, img2) and casts == casts2  # deterministic
     ocam = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"])
     ref, rc = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p), rect, bf16=True)
-    p2 = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16, max_bounces=20, seed=7)
+    p2 = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=16, seed=7)
     alt, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p2), rect, bf16=True)
     noise = rtmi_mod.metrics.mape_f(ref, alt)
     m = rtmi_mod.metrics.mape_f(ref, img)
     assert m <= noise, (m, noise)
     assert abs(casts - rc) <= 0.05 * rc
     assert img.mean() > 0
+
+
+def zscores(a, b):
+    """per-channel z-score of the mean per-pixel difference a - b"""
+    d = (a.astype(np.float64) - b.astype(np.float64)).reshape(-1, 3)
+    se = d.std(axis=0) / np.sqrt(d.shape[0])
+    return np.abs(d.mean(axis=0)) / np.maximum(se, 1e-30)
+
+
+@pytest.mark.gpu
+def test_config4_archway_dqn_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx):
+    """BASELINE config 4 at its own workload: archway (102 triangles, 918 network inputs),
+    the GPU-engine preset (80 bounces), Q-weighted sampling from the fc_layer network
+    (synthetic He-normal weights: the archway model is not in the reference), a 64x64
+    window of the 1024x1024 frame, against the oracle's render with the kernel's bf16
+    arithmetic (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491;
+    importance_sample_direction, nn_rendering_helpers.cu:391-489)."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=4)
+    assert p.max_bounces == 80
+    rect = (448, 448, 64, 64)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["archway"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        img, casts = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+    ocam = oracle_mod.camera(rtmi_mod.CAMERAS["archway"])
+    ref, rc = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p), rect, bf16=True)
+    p2 = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=4, seed=7)
+    alt, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, oracle_mod.params_from(p2), rect, bf16=True)
+    assert np.isfinite(img).all() and img.mean() > 0
+    z = zscores(img, ref)
+    assert np.all(z < 3.0), z
+    assert abs(casts - rc) <= 0.01 * rc, (casts, rc)
+    noise = rtmi_mod.metrics.mape_f(ref, alt)
+    assert rtmi_mod.metrics.mape_f(ref, img) <= noise, (rtmi_mod.metrics.mape_f(ref, img), noise)
+
+
+@pytest.mark.gpu
+def test_config4_full_frame_properties(rtmi_mod, gpu_ctx):
+    """The whole 1024x1024 config-4 frame (2 spp): deterministic, the tile-list render equals
+    the rectangle render, finite, and the ray casts per sample in the archway band."""
+    torch = pytest.importorskip("torch")
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=2)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["archway"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        img, casts = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p)
+        img2, casts2 = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p)
+        tiles = rtmi_mod.tiles.tile_origins(1024, 1024, 32)
+        out = torch.zeros((len(tiles), 32, 32, 3), dtype=torch.float32, device="cuda")
+        tc = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rtmi_mod.dqn.render_tiles_device(gpu_ctx, sc, net, cam, p, tiles, 32, out.data_ptr(), tc.data_ptr(),
+                                         torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        timg = rtmi_mod.tiles.assemble(out.cpu().numpy()[None], 1024, 1024, 32, 1)
+    assert np.array_equal(img, img2) and casts == casts2
+    assert np.array_equal(img, timg) and int(tc.item()) == casts
+    assert np.isfinite(img).all() and img.mean() > 0
+    per_sample = casts / (1024 * 1024 * 2)
+    assert 30.0 < per_sample < 45.0, per_sample  # 37.5 at 512 spp (profiles/r1_configs_full.json c4)
 
 
 @pytest.mark.gpu
