@@ -166,8 +166,9 @@ typedef struct rt_dqn rt_dqn;
 
 /* DyNet TextFileSaver format reader (the reference loads RMD/<scene>.model with
  * dynet::TextFileLoader, GPU/deep_learning/pre_trained_pathtracer.cu:45-53).  Parameters in
- * file order; each returned row-major [rows][cols] (DyNet stores column-major).  Call with
- * values = NULL to size: *n_params, *n_values. */
+ * file order; each returned row-major [rows][cols] (DyNet stores column-major); a vector
+ * ("{rows}" header) is returned with cols = 0 and holds rows values.  Call with values = NULL
+ * to size: *n_params, *n_values. */
 int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols, float* values,
                   int* n_params, int64_t* n_values);
 
@@ -176,8 +177,10 @@ int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols
  * NN_Q_Value_Trainer/Source/main.cu:290, into Radiance_Map_Data/<name>.model):
  * "#Parameter# /_<k> {rows,cols} <bytes> ZERO_GRAD" (vectors "{rows}") then one line of
  * column-major "%+.8e " values; <bytes> counts that line with its newline.  values: the
- * n_params parameters concatenated, each row-major [rows][cols] (the rt_dynet_read layout),
- * so a write -> read round trip returns the same floats bit for bit. */
+ * n_params parameters concatenated, each row-major [rows][cols] (the rt_dynet_read layout;
+ * cols = 0: a vector of rows values, "{rows}" header; cols = 1: an (rows, 1) matrix), so a
+ * write -> read round trip returns the same floats and shapes bit for bit.  Non-finite
+ * values are refused (RT_E_INVALID): DyNet's loader cannot parse them. */
 int rt_dynet_write(const char* path, int n_params, const int32_t* rows, const int32_t* cols,
                    const float* values);
 

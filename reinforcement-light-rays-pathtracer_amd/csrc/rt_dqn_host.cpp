@@ -79,7 +79,8 @@ int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols
             rc = err(RT_E_IO, "bad #Parameter# header");
             break;
         }
-        if (!strchr(br, ',') || strchr(br, ',') > strchr(br, '}')) c = 1;  // vector {r}
+        const bool vec = !strchr(br, ',') || strchr(br, ',') > strchr(br, '}');  // vector {r}
+        if (vec) c = 1;
         if (r <= 0 || c <= 0) {
             rc = err(RT_E_IO, "bad parameter shape");
             break;
@@ -109,7 +110,7 @@ int rt_dynet_read(const char* path, int max_params, int32_t* rows, int32_t* cols
             if (rc != RT_OK) break;
         }
         if (rows && np < max_params) rows[np] = r;
-        if (cols && np < max_params) cols[np] = c;
+        if (cols && np < max_params) cols[np] = vec ? 0 : c;  // 0: a vector of r values
         ++np;
         nv += cnt;
     }
@@ -124,14 +125,21 @@ int rt_dynet_write(const char* path, int n_params, const int32_t* rows, const in
                    const float* values) {
     if (!path || n_params < 0 || (n_params > 0 && (!rows || !cols || !values)))
         return err(RT_E_INVALID, "NULL argument");
-    for (int p = 0; p < n_params; ++p)
-        if (rows[p] <= 0 || cols[p] <= 0) return err(RT_E_INVALID, "bad parameter shape");
+    int64_t total = 0;
+    for (int p = 0; p < n_params; ++p) {
+        if (rows[p] <= 0 || cols[p] < 0) return err(RT_E_INVALID, "bad parameter shape");
+        total += (int64_t)rows[p] * (cols[p] ? cols[p] : 1);
+    }
+    // DyNet's loader reads values with operator>>(float), which cannot parse nan/inf
+    for (int64_t k = 0; k < total; ++k)
+        if (!std::isfinite(values[k])) return err(RT_E_INVALID, "non-finite parameter value");
     FILE* f = fopen(path, "w");
     if (!f) return err(RT_E_IO, std::string("cannot open ") + path);
     std::string line;
     const float* src = values;
     for (int p = 0; p < n_params && f; ++p) {
-        const int r = rows[p], c = cols[p];
+        const bool vec = cols[p] == 0;
+        const int r = rows[p], c = vec ? 1 : cols[p];
         // values line first: the header carries its byte count (newline included)
         line.clear();
         char num[32];
@@ -141,7 +149,7 @@ int rt_dynet_write(const char* path, int n_params, const int32_t* rows, const in
             line += num;
         }
         line += '\n';
-        if (c == 1)
+        if (vec)
             fprintf(f, "#Parameter# /_%d {%d} %zu ZERO_GRAD\n", p, r, line.size());
         else
             fprintf(f, "#Parameter# /_%d {%d,%d} %zu ZERO_GRAD\n", p, r, c, line.size());

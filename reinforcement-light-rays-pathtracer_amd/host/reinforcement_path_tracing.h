@@ -13,6 +13,7 @@
 // is already part of it and kept as a no-op for source compatibility.
 #pragma once
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -136,9 +137,9 @@ class PretrainedPathtracer {
         size_t off = 0;
         for (int l = 0; l < 4; ++l) {
             W[l] = values.data() + off;
-            off += (size_t)rows[2 * l] * cols[2 * l];
+            off += (size_t)rows[2 * l] * std::max(cols[2 * l], 1);  // cols 0: a vector
             b[l] = values.data() + off;
-            off += (size_t)rows[2 * l + 1] * cols[2 * l + 1];
+            off += (size_t)rows[2 * l + 1] * std::max(cols[2 * l + 1], 1);
         }
         const int32_t hidden[3] = {rows[0], rows[2], rows[4]};
         const std::vector<float>& v = ds.vertices();

@@ -37,23 +37,24 @@ def read_dynet(path: str) -> List[np.ndarray]:
     check(L.rt_dynet_read(path.encode(), n_params.value, _ip(rows), _ip(cols), _fp(vals),
                           ctypes.byref(n_params), ctypes.byref(n_values)))
     out, off = [], 0
-    for r, c in zip(rows, cols):
-        n = int(r) * int(c)
-        a = vals[off:off + n].reshape(int(r), int(c))
-        out.append(a[:, 0].copy() if c == 1 else a.copy())
+    for r, c in zip(rows, cols):  # cols 0: a vector ("{rows}" header)
+        n = int(r) * max(int(c), 1)
+        a = vals[off:off + n]
+        out.append(a.copy() if c == 0 else a.reshape(int(r), int(c)).copy())
         off += n
     return out
 
 
 def write_dynet(path: str, params: Sequence[np.ndarray]) -> None:
     """DyNet TextFileSaver model (neural_q_pathtracer.cu:193) of `params` in order: matrices
-    row-major [rows][cols], vectors [rows]; read_dynet(path) returns them bit for bit."""
+    row-major [rows][cols], vectors [rows]; read_dynet(path) returns them bit for bit, shapes
+    included (an (n, 1) matrix stays one).  Non-finite values raise (DyNet cannot load them)."""
     arrs = [np.ascontiguousarray(p, np.float32) for p in params]
     for a in arrs:
         if a.ndim not in (1, 2) or a.size == 0:
             raise ValueError(f"DyNet parameters are non-empty vectors or matrices, got {a.shape}")
     rows = np.array([a.shape[0] for a in arrs], np.int32)
-    cols = np.array([a.shape[1] if a.ndim == 2 else 1 for a in arrs], np.int32)
+    cols = np.array([a.shape[1] if a.ndim == 2 else 0 for a in arrs], np.int32)  # 0: vector
     vals = np.concatenate([a.ravel() for a in arrs]) if arrs else np.zeros(1, np.float32)
     check(lib().rt_dynet_write(os.fsencode(path), len(arrs), _ip(rows), _ip(cols), _fp(vals)))
 

@@ -448,3 +448,16 @@ def test_dynet_write_read_round_trip(rtmi_mod, tmp_path):
         assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
     with pytest.raises(ValueError):
         rtmi_mod.dqn.write_dynet(out, [np.zeros((2, 2, 2), np.float32)])
+    # an (n, 1) matrix stays a matrix, a vector a vector
+    col = np.arange(5, dtype=np.float32).reshape(5, 1)
+    rtmi_mod.dqn.write_dynet(out, [col, col[:, 0]])
+    text = open(out).read()
+    assert "{5,1}" in text and "{5}" in text
+    back = rtmi_mod.dqn.read_dynet(out)
+    assert back[0].shape == (5, 1) and back[1].shape == (5,)
+    # a diverged trainer's nan / inf cannot be written: DyNet's loader cannot parse them
+    for bad in (np.nan, np.inf):
+        x = np.ones(3, np.float32)
+        x[1] = bad
+        with pytest.raises(RuntimeError):
+            rtmi_mod.dqn.write_dynet(out, [x])
