@@ -272,6 +272,24 @@ int rt_sarsa_info(const rt_sarsa* sarsa, int32_t* n_volumes, int32_t* n_nodes, u
 #define RT_SARSA_SEARCH_KD 0
 #define RT_SARSA_SEARCH_GRID 1
 int rt_sarsa_set_search(rt_sarsa* sarsa, int mode);
+/* Direction sampling at a surface with a radiance volume:
+ * RT_SARSA_SAMPLE_CDF (default) RadianceVolume::sample_direction_from_radiance_distribution
+ *   (radiance_volume.cu:191-244), the CDF by inverse transform;
+ * RT_SARSA_SAMPLE_MAX sample_max_direction_from_radiance_distribution (:246-278): the first
+ *   sector of largest Q (of the previous frame), uniform within it, pdf = RHO x its CDF step
+ *   / GRID_RHO -- 0 for sector 0, as the reference computes it (the path's throughput is
+ *   then infinite).  TD learning is the same in both modes. */
+#define RT_SARSA_SAMPLE_CDF 0
+#define RT_SARSA_SAMPLE_MAX 1
+int rt_sarsa_set_sampling(rt_sarsa* sarsa, int mode);
+/* Training statistics of the last frame rendered (GPU/main.cu:321-339, one line of
+ * Radiance_Map_Data/sarsa_training_stats.txt per frame): path_floor_sum = the sum over the
+ * frame's pixels of int(path lengths / spp) (path_trace_reinforcement,
+ * reinforcement_path_tracing.cu:27-44; a path's length is its ray casts), zero_paths = the
+ * paths whose mean radiance (r + g + b) / 3 < THROUGHPUT_THRESHOLD.  The reference's line is
+ * "<path_floor_sum / pixels, integer division> 0 <zero_paths>".  For rt_render_sarsa_tiles_device
+ * the sums cover the call's tiles (add them over ranks). */
+int rt_sarsa_frame_stats(const rt_sarsa* sarsa, uint64_t* path_floor_sum, uint64_t* zero_paths);
 /* On-disk formats of the reference's Q-tables.
  * rt_sarsa_save_q: RadianceMap::save_q_vals_to_file (GPU/radiance_volumes/radiance_map.cu:236-266):
  *   "144\n", then one line per volume in map order: "x y z Q0 .. Q143" (ostream defaults,
@@ -282,6 +300,15 @@ int rt_sarsa_set_search(rt_sarsa* sarsa, int mode);
  *   distribution (the CDF differenced: convert_radiance_distribution, radiance_volume.cu:332-336);
  *   out_path is replaced.  Both return RT_E_IO on file errors. */
 int rt_sarsa_save_q(const rt_sarsa* sarsa, const char* path);
+/* The Q-table back into a map: a file of rt_sarsa_save_q / save_q_vals_to_file, whose
+ * volume positions must be this map's (same scene and seed: RT_E_INVALID otherwise).  Q is
+ * set from the file (std::stof of the printed values), the irradiance estimate recomputed
+ * as initialise_radiance_grid does for a Q grid (radiance_volume.cu:46-63), the CDF as
+ * update_radiance_distribution (:148-188); visits are kept.  The reference reads its
+ * per-volume files back only to draw them (read_radiance_volumes_from_file,
+ * radiance_volume.cu:377-440); this resumes training or renders from a saved map.
+ * save_q -> load_q -> save_q reproduces the file byte for byte. */
+int rt_sarsa_load_q(rt_sarsa* sarsa, const char* path);
 int rt_sarsa_save_selected(rt_ctx* ctx, const rt_sarsa* sarsa, const char* to_select_path,
                            const char* out_path);
 int rt_sarsa_search_stats(const rt_sarsa* sarsa, int32_t* mode, int32_t* n_classes, int64_t* grid_cells,

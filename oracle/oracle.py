@@ -309,6 +309,9 @@ class Sarsa:
         L.orc_sarsa_nearest.argtypes = [VP, _FP, _FP, ctypes.c_int, _IP]
         L.orc_render_sarsa.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
                                        _FP, ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_sarsa_set_sampling.argtypes = [VP, ctypes.c_int]
+        L.orc_sarsa_stats.argtypes = [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_sarsa_load_q.argtypes = [VP, _FP]
         L.orc_sarsa_td_rect.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
                                         ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_uint32)]
@@ -355,6 +358,20 @@ class Sarsa:
         out = np.zeros(p.shape[0], np.int32)
         self._L.orc_sarsa_nearest(self._h, _f(p), _f(n_), p.shape[0], _i(out))
         return out
+
+    def set_sampling(self, mode: int):
+        """0: CDF importance sampling, 1: sample_max_direction_from_radiance_distribution"""
+        self._L.orc_sarsa_set_sampling(self._h, mode)
+
+    def stats(self):
+        """(sum over pixels of int(path length mean), zero-contribution paths) of the last frame"""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._L.orc_sarsa_stats(self._h, ctypes.byref(a), ctypes.byref(b))
+        return int(a.value), int(b.value)
+
+    def load_q(self, q):
+        q = np.ascontiguousarray(q, np.float32).reshape(self.n_volumes, 144)
+        self._L.orc_sarsa_load_q(self._h, _f(q))
 
     def td_rect(self, cam: OrcCamera, params: OrcParams, rect):
         """(int64 sums, uint32 counts), each (n_volumes * 144,): the TD accumulators that the

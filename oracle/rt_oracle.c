@@ -1062,6 +1062,8 @@ typedef struct {
     float *tri_lum;
     uint32_t frames;
     uint64_t seed;
+    int sample_max;                 /* 1: sample_max_direction_from_radiance_distribution */
+    uint64_t stat_paths, stat_zero; /* last frame: sum of per-pixel floor(path length mean), zero paths */
     /* scene (copied) */
     int n_surf, n_light;
     float *tri, *albedo, *emission, *normal;
@@ -1340,6 +1342,33 @@ static int sarsa_sample(const orc_sarsa *m, int rv, float r, float rx, float ry,
     return 1;
 }
 
+/* sample_max_direction_from_radiance_distribution (radiance_volume.cu:246-278): the first
+ * sector of largest Q (strict <, scanned from sector 0), uniform within it; pdf from the
+ * CDF step of that sector, which is 0 for sector 0 (last_pdf = cdf[0] there, :274). */
+static void sarsa_sample_max(const orc_sarsa *m, int rv, float rx, float ry, int *sector, v3 *dir, float *pdf) {
+    const float *q = m->Q + (size_t)rv * 144, *cdf = m->cdf + (size_t)rv * 144;
+    const float RHO = 1.0f / (2.0f * 3.1415926535f);
+    const float GRID_RHO = 1.0f / (12.0f * 12.0f);
+    int mi = 0;
+    float mq = q[0];
+    for (int i = 0; i < 144; i++)
+        if (mq < q[i]) { mq = q[i]; mi = i; }
+    int sx = mi / 12, sy = mi - sx * 12;
+    *sector = mi;
+    float last = mi == 0 ? cdf[mi] : cdf[mi - 1];
+    *pdf = RHO * ((cdf[mi] - last) / GRID_RHO);
+    const float *f = m->frame + 9 * (size_t)rv;
+    *dir = grid_dir((float)sx + rx, (float)sy + ry, mk(f[0], f[1], f[2]), mk(f[3], f[4], f[5]), mk(f[6], f[7], f[8]),
+                    mk(m->pos[4 * rv], m->pos[4 * rv + 1], m->pos[4 * rv + 2]));
+}
+
+ORC_API void orc_sarsa_set_sampling(orc_sarsa *m, int mode) { m->sample_max = mode == 1; }
+
+ORC_API void orc_sarsa_stats(const orc_sarsa *m, uint64_t *path_floor_sum, uint64_t *zero_paths) {
+    *path_floor_sum = m->stat_paths;
+    *zero_paths = m->stat_zero;
+}
+
 static void td_add(orc_sarsa *m, int rv, int sector, float target) {
     int64_t v = (int64_t)llrintf(target * 4294967296.0f);
     size_t k = (size_t)rv * 144 + sector;
@@ -1400,6 +1429,8 @@ static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t 
             float ct;
             sd = sample_dir(nrm, u01(rn[0]), u01(rn[1]), 0, &ct);
             pdf = RHO;
+        } else if (m->sample_max) {
+            sarsa_sample_max(m, cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
         } else if (!sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf)) {
             if (i + 1 >= p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
             (*casts)++; /* the zero direction is traced and misses */
@@ -1415,6 +1446,25 @@ static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t 
         d = normalize3(sd);
     }
     return mk(0.0f, 0.0f, 0.0f);
+}
+
+/* update_radiance_distribution (radiance_volume.cu:148-188) of volume v */
+static void sarsa_rebuild_cdf(orc_sarsa *m, int v) {
+    size_t b = (size_t)v * 144;
+    float total = 0.0000000001f;
+    for (int k = 0; k < 144; k++) {
+        float t = m->Q[b + k] * m->cc[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        total += t;
+    }
+    float prev = 0.0f;
+    for (int k = 0; k < 144; k++) {
+        float t = m->Q[b + k] * m->cc[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        float rad = t / total + prev;
+        m->cdf[b + k] = rad;
+        prev = rad;
+    }
 }
 
 /* update_radiance_distribution + the frame's TD fold */
@@ -1440,20 +1490,24 @@ static void sarsa_apply(orc_sarsa *m) {
             m->sum[b + k] = 0;
         }
         m->accum[v] = accum;
-        float total = 0.0000000001f;
-        for (int k = 0; k < 144; k++) {
-            float t = m->Q[b + k] * m->cc[b + k];
-            t = t > 0.0f ? t : 0.0f;
-            total += t;
-        }
-        float prev = 0.0f;
-        for (int k = 0; k < 144; k++) {
-            float t = m->Q[b + k] * m->cc[b + k];
-            t = t > 0.0f ? t : 0.0f;
-            float rad = t / total + prev;
-            m->cdf[b + k] = rad;
-            prev = rad;
-        }
+        sarsa_rebuild_cdf(m, v);
+    }
+}
+
+/* Q-table loader (rt_sarsa_load_q): Q from radiance_map_data.txt values, the irradiance
+ * estimate of initialise_radiance_grid (radiance_volume.cu:46-63) over that Q, the CDF of
+ * update_radiance_distribution; visits kept. */
+ORC_API void orc_sarsa_load_q(orc_sarsa *m, const float *q) {
+    memcpy(m->Q, q, sizeof(float) * (size_t)m->n_vol * 144);
+    for (int v = 0; v < m->n_vol; v++) {
+        size_t b = (size_t)v * 144;
+        float lum = lum3(m->albedo + 3 * m->surf[v]);
+        float irr = 0.0f;
+        for (int k = 0; k < 144; k++)
+            irr = (float)((double)irr + ((double)m->cc[b + k] * ((double)lum / 3.14159265358979323846)) *
+                                            (double)m->Q[b + k]);
+        m->accum[v] = irr;
+        sarsa_rebuild_cdf(m, v);
     }
 }
 
@@ -1505,7 +1559,8 @@ ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_para
     int per = p->spp / S;
     for (int f = 0; f < frames; f++) {
         uint32_t base = m->frames * (uint32_t)p->spp;
-        #pragma omp parallel for schedule(dynamic, 1) reduction(+:total)
+        uint64_t paths = 0, zero = 0;
+        #pragma omp parallel for schedule(dynamic, 1) reduction(+:total, paths, zero)
         for (int py = 0; py < H; py++) {
             for (int px = 0; px < W; px++) {
                 uint32_t pix = (uint32_t)py * (uint32_t)W + (uint32_t)px;
@@ -1520,6 +1575,9 @@ ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_para
                         camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
                         v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
                         part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
+                        /* path_trace_reinforcement (reinforcement_path_tracing.cu:28-41): a
+                         * zero-contribution path; its path length is its ray casts */
+                        if ((L.x + L.y + L.z) / 3.f < 0.0001f) zero++;
                     }
                     if (c == 0) acc = part;
                     else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }
@@ -1528,8 +1586,11 @@ ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_para
                 float *dst = out_rgb + ((size_t)py * W + px) * 3;
                 dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
                 total += casts;
+                paths += casts / (uint64_t)p->spp; /* int(total_path_lengths / SAMPLES_PER_PIXEL) */
             }
         }
+        m->stat_paths = paths;
+        m->stat_zero = zero;
         sarsa_apply(m);
         m->frames++;
     }

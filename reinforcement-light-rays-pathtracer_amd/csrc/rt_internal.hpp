@@ -216,11 +216,17 @@ struct SarsaMap {
     float grid_cs = 0.f;                   // cell size (cell centres: org + (i + 0.5) cs)
     float grid_h = 0.f;                    // accept radius: sqrt(MAX_DIST) * 0.999
     unsigned long long* grid_fallbacks = nullptr;  // optional count of KD fallbacks
+    // sampling rule: 0 = the CDF (sample_direction_from_radiance_distribution), 1 = the
+    // sector of largest Q (sample_max_direction_from_radiance_distribution)
+    int sample_max = 0;
+    int32_t* qmax = nullptr;               // [n] first sector of largest Q (k_sarsa_apply)
+    unsigned long long* stats = nullptr;   // [2] launch: sum of per-pixel int(mean path length), zero paths
 };
 constexpr int kKdStack = 32;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
 
 hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);
+hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream);  // CDF + argmax from Q
 hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float* nrm, int n, int32_t* out,
                                 hipStream_t stream);
 

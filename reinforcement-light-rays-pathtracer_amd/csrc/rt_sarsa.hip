@@ -47,6 +47,7 @@ namespace {
 constexpr float kGridRhoS = 1.0f / ((float)kGridRes * (float)kGridRes);             // GRID_RHO
 constexpr float kRadianceThreshold = (1.f / ((float)kGridRes * (float)kGridRes)) * 0.8f;  // RADIANCE_THRESHOLD
 constexpr float kIrrScale = (2.f * kPi) / ((float)(kGridRes * kGridRes));          // get_irradiance_estimate
+constexpr float kThroughputThreshold = 0.0001f;  // THROUGHPUT_THRESHOLD (constants/monte_carlo_settings.h:11)
 
 __device__ __forceinline__ float len3(float x, float y, float z) { return sqrtf((x * x + y * y) + z * z); }
 
@@ -255,6 +256,24 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     return true;
 }
 
+// sample_max_direction_from_radiance_distribution (radiance_volume.cu:246-278): the first
+// sector of largest Q (qmax, kept by k_sarsa_apply), uniform within it; the pdf is the CDF
+// step of that sector, 0 for sector 0 (the reference's last_pdf is cdf[0] there, :274)
+__device__ void sarsa_sample_max(const SarsaMap& m, int rv, float rx, float ry, int* sector, f3* dir,
+                                 float* pdf) {
+    const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
+    const int mi = m.qmax[rv];
+    const float mv = cdf[mi];
+    const float last = cdf[mi > 0 ? mi - 1 : 0];
+    const int sx = mi / kGridRes;
+    const int sy = mi - sx * kGridRes;
+    *sector = mi;
+    *pdf = kRho * ((mv - last) / kGridRhoS);
+    const float4 N4 = m.vol_frame[rv * 3 + 0], T4 = m.vol_frame[rv * 3 + 1], B4 = m.vol_frame[rv * 3 + 2];
+    *dir = grid_direction((float)sx + rx, (float)sy + ry, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                          make3(B4.x, B4.y, B4.z), make3(N4.w, T4.w, B4.w));
+}
+
 __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, float target) {
     if (RT_SARSA_NO_TD) return;
     const long long v = __float2ll_rn(target * 4294967296.0f);
@@ -288,7 +307,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     float cur_brdf = 0.0f;
     f3 o = make3(a.cam_x, a.cam_y, a.cam_z), d = make3(0.f, 0.f, 1.f);
     f3 tp = make3(1.f, 1.f, 1.f), acc = make3(0.f, 0.f, 0.f);
-    unsigned n_casts = 0;
+    unsigned n_casts = 0, n_zero = 0;
     if (s < s_end) {
         float r1, r2;
         draw2(pix, a.sample_base + (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
@@ -356,6 +375,8 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
                 sd = make3((sx * B4.x + c * nrm.x) + sz * T4.x, (sx * B4.y + c * nrm.y) + sz * T4.y,
                            (sx * B4.z + c * nrm.z) + sz * T4.z);
                 pdf = kRho;
+            } else if (m.sample_max) {
+                sarsa_sample_max(m, cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
             } else {
                 ok = sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
             }
@@ -384,6 +405,8 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
+            // a zero-contribution light path (reinforcement_path_tracing.cu:36-40)
+            n_zero += ((L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
             ++s;
             depth = 0;
             cur_rv = -1;
@@ -399,13 +422,24 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     }
     const int base = lane & ~(a.split - 1);
     f3 tot = acc;
+    unsigned pix_casts = n_casts;  // a sample's path length is its ray casts
     for (int k = 1; k < a.split; ++k) {
         const float vx = __shfl(acc.x, base + k, 64);
         const float vy = __shfl(acc.y, base + k, 64);
         const float vz = __shfl(acc.z, base + k, 64);
+        pix_casts += (unsigned)__shfl((int)n_casts, base + k, 64);
         tot.x = tot.x + vx;
         tot.y = tot.y + vy;
         tot.z = tot.z + vz;
+    }
+    if (m.stats != nullptr) {
+        // main.cu:321-339 statistics: int(total_path_lengths / SAMPLES_PER_PIXEL) per pixel
+        const unsigned pf = (valid && chunk == 0) ? pix_casts / (unsigned)a.spp : 0u;
+        const unsigned sp = wave_sum(pf), sz = wave_sum(n_zero);
+        if (lane == 0) {
+            atomicAdd(&m.stats[0], (unsigned long long)sp);
+            atomicAdd(&m.stats[1], (unsigned long long)sz);
+        }
     }
     if (valid && chunk == 0) {
         const float fs = (float)a.spp;
@@ -418,6 +452,39 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
         const unsigned total = wave_sum(n_casts);
         if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
     }
+}
+
+// update_radiance_distribution (radiance_volume.cu:148-188) of volume v, its row ends, and
+// the first sector of largest Q (the max-direction sampler's scan, radiance_volume.cu:251-257)
+__device__ void rebuild_volume(const SarsaMap& m, int v) {
+    const size_t b = (size_t)v * kSarsaSectors;
+    float total = 0.0000000001f;
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        float t = m.Q[b + k] * m.cos_center[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        total += t;
+    }
+    float prev = 0.0f;
+    float* top = reinterpret_cast<float*>(m.cdf_top + (size_t)v * 4);
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        float t = m.Q[b + k] * m.cos_center[b + k];
+        t = t > 0.0f ? t : 0.0f;
+        const float rad = t / total + prev;
+        m.cdf[b + k] = rad;
+        if (k == 0) top[0] = rad;
+        if (k % kGridRes == kGridRes - 1) top[1 + k / kGridRes] = rad;
+        prev = rad;
+    }
+    int mi = 0;
+    float mq = m.Q[b];
+    for (int k = 0; k < kSarsaSectors; ++k) {
+        const float q = m.Q[b + k];
+        if (mq < q) {
+            mq = q;
+            mi = k;
+        }
+    }
+    m.qmax[v] = mi;
 }
 
 // End of frame, one lane per volume: fold the frame's TD targets (the running
@@ -447,23 +514,14 @@ __global__ __launch_bounds__(256) void k_sarsa_apply(const SarsaMap m) {
         m.acc_sum[b + k] = 0ull;
     }
     m.accum[v] = accum;
-    float total = 0.0000000001f;
-    for (int k = 0; k < kSarsaSectors; ++k) {
-        float t = m.Q[b + k] * m.cos_center[b + k];
-        t = t > 0.0f ? t : 0.0f;
-        total += t;
-    }
-    float prev = 0.0f;
-    float* top = reinterpret_cast<float*>(m.cdf_top + (size_t)v * 4);
-    for (int k = 0; k < kSarsaSectors; ++k) {
-        float t = m.Q[b + k] * m.cos_center[b + k];
-        t = t > 0.0f ? t : 0.0f;
-        const float rad = t / total + prev;
-        m.cdf[b + k] = rad;
-        if (k == 0) top[0] = rad;
-        if (k % kGridRes == kGridRes - 1) top[1 + k / kGridRes] = rad;
-        prev = rad;
-    }
+    rebuild_volume(m, v);
+}
+
+// CDF and argmax of Q after a load (rt_sarsa_load_q)
+__global__ __launch_bounds__(256) void k_sarsa_rebuild(const SarsaMap m) {
+    const int v = blockIdx.x * 256 + threadIdx.x;
+    if (v >= m.n_vol) return;
+    rebuild_volume(m, v);
 }
 
 // nearest-volume queries alone (KD parity): pos/nrm [n][3]
@@ -492,6 +550,12 @@ hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStre
         hipLaunchKernelGGL(k_sarsa_render<0>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
     else
         hipLaunchKernelGGL(k_sarsa_render<1>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
+    return hipGetLastError();
+}
+
+hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream) {
+    if (m.n_vol <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sarsa_rebuild, dim3((unsigned)((m.n_vol + 255) / 256)), dim3(256), 0, stream, m);
     return hipGetLastError();
 }
 

@@ -8,12 +8,15 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <array>
 #include <fstream>
 #include <map>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -350,6 +353,8 @@ struct rt_sarsa {
     std::vector<float> nrm;   // [n][3]
     std::vector<int32_t> surf;  // [n] surface index
     std::vector<rt::KdNode> kd;
+    std::vector<float> lum;         // [n] luminance of the volume's surface
+    std::vector<float> cos_center;  // [n*144] (rt_sarsa_load_q's irradiance)
     int64_t grid_cells = 0;   // nearest-volume grid (0: none, every search walks the KD tree)
     rt::SarsaMap m;
     std::vector<void*> allocs;
@@ -368,6 +373,15 @@ struct rt_sarsa {
 };
 
 namespace {
+
+// initialise_radiance_grid (radiance_volume.cu:46-63): cos * (luminance / M_PI) * Q in
+// double, summed in float
+float initial_irradiance(const float* cc, const float* q, float lum) {
+    float irr = 0.f;
+    for (int k = 0; k < rt::kSarsaSectors; ++k)
+        irr = (float)((double)irr + ((double)cc[k] * ((double)lum / M_PI)) * (double)q[k]);
+    return irr;
+}
 
 int check_sarsa_params(const rt_params* p) {
     if (!p) return err(RT_E_INVALID, "params is NULL");
@@ -396,6 +410,7 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
     a.out = d_out;
     a.casts = d_casts;
     a.sample_base = sa->frames * (uint32_t)p->spp;
+    RT_HIPE(hipMemsetAsync(sa->m.stats, 0, 2 * sizeof(unsigned long long), stream));
     RT_HIPE(rt::launch_sarsa_render(a, sa->m, stream));
     if (apply) RT_HIPE(rt::launch_sarsa_apply(sa->m, stream));
     sa->frames += 1;
@@ -461,7 +476,6 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         memcpy(&frame[(size_t)12 * i], f, sizeof(f));
         const float lum = luminance(albedo + 3 * sa->surf[i]);
         brdf[i] = lum / rt::kPi;
-        float irr = 0.f;
         for (int x = 0; x < rt::kGridRes; ++x)
             for (int y = 0; y < rt::kGridRes; ++y) {
                 const int k = x * rt::kGridRes + y;
@@ -471,12 +485,12 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
                 ck[(size_t)i * S + k] = rt::dot(dk, N);
                 Q[(size_t)i * S + k] = kInitialRadiance;
                 cdf[(size_t)i * S + k] = (float)k * (1.f / ((float)rt::kGridRes * (float)rt::kGridRes));
-                // initialise_radiance_grid: cos * (luminance / M_PI) * Q in double, summed in float
-                irr = (float)((double)irr + ((double)cc[(size_t)i * S + k] * ((double)lum / M_PI)) *
-                                                (double)kInitialRadiance);
             }
-        accum[i] = irr;
+        accum[i] = initial_irradiance(&cc[(size_t)i * S], &Q[(size_t)i * S], lum);
     }
+    sa->lum.resize(n);
+    for (int i = 0; i < n; ++i) sa->lum[i] = luminance(albedo + 3 * sa->surf[i]);
+    sa->cos_center = cc;
     std::vector<float> tri_lum(n_surf + n_light);
     for (int j = 0; j < n_surf; ++j) tri_lum[j] = luminance(albedo + 3 * j);
     for (int j = 0; j < n_light; ++j) tri_lum[n_surf + j] = luminance(emission + 3 * j);
@@ -539,6 +553,10 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     uint32_t* d_cstart = nullptr;
     unsigned long long* d_fb = nullptr;
     if (e == hipSuccess) e = sa->alloc(&d_fb, 1);
+    unsigned long long* d_stats = nullptr;
+    int32_t* d_qmax = nullptr;
+    if (e == hipSuccess) e = sa->alloc(&d_stats, 2);
+    if (e == hipSuccess) e = sa->alloc(&d_qmax, n);
     if (have_grid) {
         if (e == hipSuccess) e = sa->alloc(&d_tcls, grid.tri_class.size());
         if (e == hipSuccess) e = sa->alloc(&d_corg, grid.org.size());
@@ -578,6 +596,8 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         up(d_leaf, grid.leaf.data(), sizeof(float4) * grid.leaf.size());
     }
     if (e == hipSuccess) e = hipMemset(d_fb, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_stats, 0, 2 * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_qmax, 0, sizeof(int32_t) * n);  // every Q equal: sector 0
     if (e == hipSuccess) e = hipMemset(d_vis, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_cnt, 0, sizeof(uint32_t) * nS);
     if (e == hipSuccess) e = hipMemset(d_sum, 0, sizeof(unsigned long long) * nS);
@@ -620,6 +640,8 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         sa->grid_cells = (int64_t)grid.start.size() - 1;
     }
     m.grid_fallbacks = d_fb;
+    m.stats = d_stats;
+    m.qmax = d_qmax;
     *out = sa;
     return RT_OK;
 }
@@ -721,6 +743,72 @@ int rt_sarsa_save_q(const rt_sarsa* sa, const char* path) {
     }
     f.close();
     if (f.fail()) return err(RT_E_IO, std::string("write failed: ") + path);
+    return RT_OK;
+}
+
+int rt_sarsa_load_q(rt_sarsa* sa, const char* path) {
+    if (!sa || !path) return err(RT_E_INVALID, "NULL argument");
+    const int S = rt::kSarsaSectors;
+    FILE* f = fopen(path, "r");
+    if (!f) return err(RT_E_IO, std::string("cannot open ") + path);
+    std::vector<float> q((size_t)sa->n_vol * S);
+    int rc = RT_OK;
+    int actions = 0;
+    if (fscanf(f, "%d", &actions) != 1 || actions != S) rc = err(RT_E_IO, "first line must be the action count 144");
+    char tok[64];
+    auto next = [&](float* v) {  // std::stof semantics
+        if (fscanf(f, "%63s", tok) != 1) return false;
+        char* end = nullptr;
+        *v = strtof(tok, &end);
+        return end != tok && *end == '\0';
+    };
+    for (int i = 0; rc == RT_OK && i < sa->n_vol; ++i) {
+        for (int c = 0; c < 3 && rc == RT_OK; ++c) {
+            float v;
+            if (!next(&v)) {
+                rc = err(RT_E_IO, "truncated or malformed Q-table file");
+                break;
+            }
+            // the position must be this map's volume i as save_q prints it
+            std::ostringstream os;
+            os << sa->pos[4 * i + c];
+            if (strtof(os.str().c_str(), nullptr) != v)
+                rc = err(RT_E_INVALID, "volume " + std::to_string(i) + ": position differs from this map's "
+                                       "(another scene or seed)");
+        }
+        for (int k = 0; k < S && rc == RT_OK; ++k)
+            if (!next(&q[(size_t)i * S + k])) rc = err(RT_E_IO, "truncated or malformed Q-table file");
+    }
+    if (rc == RT_OK && fscanf(f, "%63s", tok) == 1) rc = err(RT_E_INVALID, "more volumes in the file than in the map");
+    fclose(f);
+    if (rc != RT_OK) return rc;
+    std::vector<float> accum(sa->n_vol);
+    for (int i = 0; i < sa->n_vol; ++i)
+        accum[i] = initial_irradiance(&sa->cos_center[(size_t)i * S], &q[(size_t)i * S], sa->lum[i]);
+    RT_HIPE(hipSetDevice(sa->device));
+    RT_HIPE(hipDeviceSynchronize());
+    RT_HIPE(hipMemcpy(sa->m.Q, q.data(), sizeof(float) * q.size(), hipMemcpyHostToDevice));
+    RT_HIPE(hipMemcpy(sa->m.accum, accum.data(), sizeof(float) * accum.size(), hipMemcpyHostToDevice));
+    RT_HIPE(rt::launch_sarsa_rebuild(sa->m, 0));
+    RT_HIPE(hipDeviceSynchronize());
+    return RT_OK;
+}
+
+int rt_sarsa_set_sampling(rt_sarsa* sa, int mode) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (mode != RT_SARSA_SAMPLE_CDF && mode != RT_SARSA_SAMPLE_MAX) return err(RT_E_INVALID, "bad sampling mode");
+    sa->m.sample_max = mode == RT_SARSA_SAMPLE_MAX;
+    return RT_OK;
+}
+
+int rt_sarsa_frame_stats(const rt_sarsa* sa, uint64_t* path_floor_sum, uint64_t* zero_paths) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    unsigned long long v[2] = {0, 0};
+    RT_HIPE(hipSetDevice(sa->device));
+    RT_HIPE(hipDeviceSynchronize());
+    RT_HIPE(hipMemcpy(v, sa->m.stats, sizeof(v), hipMemcpyDeviceToHost));
+    if (path_floor_sum) *path_floor_sum = v[0];
+    if (zero_paths) *zero_paths = v[1];
     return RT_OK;
 }
 

@@ -43,7 +43,8 @@ EXPORTS = (
     "rt_sarsa_create", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
-    "rt_sarsa_save_selected", "rt_dqn_save_selected",
+    "rt_sarsa_save_selected", "rt_sarsa_load_q", "rt_sarsa_set_sampling", "rt_sarsa_frame_stats",
+    "rt_dqn_save_selected",
     "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
     "rt_dqn_td_targets_device",
 )
@@ -131,6 +132,9 @@ def _declare(lib):
         "rt_sarsa_destroy": (i, [_P]),
         "rt_sarsa_info": (i, [_P, _IP, _IP, _UP]),
         "rt_sarsa_set_search": (i, [_P, i]),
+        "rt_sarsa_set_sampling": (i, [_P, i]),
+        "rt_sarsa_load_q": (i, [_P, ctypes.c_char_p]),
+        "rt_sarsa_frame_stats": (i, [_P, _U64P, _U64P]),
         "rt_sarsa_save_q": (i, [_P, ctypes.c_char_p]),
         "rt_dqn_save_selected": (i, [_P, _P, ctypes.c_char_p, ctypes.c_char_p]),
         "rt_sarsa_save_selected": (i, [_P, _P, ctypes.c_char_p, ctypes.c_char_p]),

@@ -6,6 +6,9 @@
   .render_tiles_device(...)       one frame over a tile list; apply=False leaves the frame's TD
                                   sums for a cross-GPU sum (rtmi.dist.sarsa_frame)
   .read() / .volumes() / .nearest(pos, nrm)   Q-table, placement, KD queries (parity)
+  .save_q(path) / .load_q(path)   radiance_map_data.txt out and back in (resume a trained map)
+  .set_sampling(SAMPLE_MAX)       sample_max_direction_from_radiance_distribution
+  .frame_stats() / .append_stats_line(path)   sarsa_training_stats.txt (GPU/main.cu:321-339)
 """
 from __future__ import annotations
 
@@ -16,9 +19,12 @@ import numpy as np
 
 from ._lib import check, lib
 
+from .api import Context, Scene, _fp, _ip
+
 SEARCH_KD = 0    # RT_SARSA_SEARCH_KD
 SEARCH_GRID = 1  # RT_SARSA_SEARCH_GRID
-from .api import Context, Scene, _fp, _ip
+SAMPLE_CDF = 0   # RT_SARSA_SAMPLE_CDF
+SAMPLE_MAX = 1   # RT_SARSA_SAMPLE_MAX
 
 SECTORS = 144  # GRID_RESOLUTION^2
 
@@ -62,6 +68,32 @@ class RadianceMap:
     def save_q(self, path: str) -> None:
         """radiance_map_data.txt format (RadianceMap::save_q_vals_to_file)."""
         check(lib().rt_sarsa_save_q(self._h, os.fsencode(path)))
+
+    def load_q(self, path: str) -> None:
+        """A radiance_map_data.txt of this map (same scene and seed) back into the device map:
+        Q from the file, irradiance estimate and CDF recomputed, visits kept (rt_sarsa_load_q)."""
+        check(lib().rt_sarsa_load_q(self._h, os.fsencode(path)))
+
+    def set_sampling(self, mode: int) -> None:
+        """SAMPLE_CDF (default) or SAMPLE_MAX (the sector of largest Q, radiance_volume.cu:246-278)."""
+        check(lib().rt_sarsa_set_sampling(self._h, mode))
+
+    def frame_stats(self):
+        """(sum over pixels of int(mean path length), zero-contribution paths) of the last frame."""
+        a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(lib().rt_sarsa_frame_stats(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return int(a.value), int(b.value)
+
+    def append_stats_line(self, path: str, pixels: int, sums=None) -> str:
+        """One line of sarsa_training_stats.txt (GPU/main.cu:330-339): the average path length
+        (integer division over `pixels`, printed as the float it is stored in), 0.0, the
+        zero-contribution paths.  sums: (path_floor_sum, zero_paths) summed over ranks, else
+        this map's frame_stats()."""
+        paths, zero = self.frame_stats() if sums is None else sums
+        line = stats_line(paths, zero, pixels)
+        with open(path, "a") as fh:
+            fh.write(line)
+        return line
 
     def save_selected(self, to_select: str, out: str) -> None:
         """selected_sarsa.txt format for the locations of to_select.txt."""
@@ -128,6 +160,12 @@ class RadianceMap:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def stats_line(path_floor_sum: int, zero_paths: int, pixels: int) -> str:
+    """`avg << " " << 0.0 << " " << zero` with ostream defaults: avg = float(int / int)."""
+    avg = np.float32(path_floor_sum // pixels)
+    return f"{float(avg):g} {0.0:g} {zero_paths}\n"
 
 
 def read_q_file(path: str):

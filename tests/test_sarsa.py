@@ -52,6 +52,24 @@ def leaves_under(kd, i, out):
 
 # ---------------------------------------------------------------- CPU ----------
 
+def test_stats_line_format(rtmi_mod):
+    """GPU/main.cu:330-339: `avg << " " << 0.0 << " " << zero` with avg = total / pixels in
+    integer arithmetic, stored in a float: the reference's own lines read "41 0 266689"."""
+    f = rtmi_mod.sarsa.stats_line
+    assert f(41 * 720 * 720 + 719, 266689, 720 * 720) == "41 0 266689\n"
+    assert f(0, 0, 4) == "0 0 0\n"
+
+
+def test_oracle_stats_bound_casts(rtmi_mod, oracle_mod):
+    """per-pixel floors sum to at most casts / spp and more than casts / spp - pixels"""
+    g = geometry(rtmi_mod, "cornell")
+    m = oracle_mod.Sarsa(g, 1984)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=24, height=16, spp=4)
+    _, casts = m.render(oracle_mod.camera(rtmi_mod.CAMERAS["cornell"]), oracle_mod.params_from(p), 1)
+    paths, zero = m.stats()
+    assert casts // 4 - 24 * 16 < paths <= casts // 4
+    assert 0 <= zero <= 24 * 16 * 4
+
 @pytest.mark.parametrize("scene", SCENES)
 def test_oracle_volume_placement(rtmi_mod, oracle_mod, scene):
     g = geometry(rtmi_mod, scene)
@@ -296,9 +314,122 @@ def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, sce
             assert np.array_equal(img_g, img_o)
             for a, b in zip(rm.read(), om.read()):
                 assert np.array_equal(a, b)
+            assert rm.frame_stats() == om.stats()  # the last frame's training statistics
         assert rm.frames == 3
     finally:
         rm.close()
+        sc.close()
+
+
+def _same_bits_nan_aware(a, b):
+    """bit-exact, except that NaN payloads may differ between the GPU and x86"""
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,split", [("door_room", 4), ("cornell", 1), ("complex_light_room", 2)])
+def test_gpu_max_direction_sampling_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, split):
+    """sample_max_direction_from_radiance_distribution (radiance_volume.cu:246-278) after two
+    frames of CDF-sampled learning: image, casts, Q, CDF, visits, irradiance and the frame
+    statistics bit-exact with the restatement over two frames in max mode."""
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    try:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=40, spp=8, spp_split=split)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+        ocam, op = oracle_mod.camera(rtmi_mod.CAMERAS[scene]), oracle_mod.params_from(p)
+        rm.render(cam, p, 2)
+        om.render(ocam, op, 2)
+        rm.set_sampling(rtmi_mod.sarsa.SAMPLE_MAX)
+        om.set_sampling(1)
+        for _ in range(2):
+            img_g, casts_g = rm.render(cam, p, 1)
+            img_o, casts_o = om.render(ocam, op, 1)
+            assert casts_g == casts_o
+            assert _same_bits_nan_aware(img_g, img_o)
+            for a, b in zip(rm.read(), om.read()):
+                assert np.array_equal(a, b)
+            assert rm.frame_stats() == om.stats()
+        # and back to CDF sampling on the greedily trained map
+        rm.set_sampling(rtmi_mod.sarsa.SAMPLE_CDF)
+        om.set_sampling(0)
+        img_g, _ = rm.render(cam, p, 1)
+        img_o, _ = om.render(ocam, op, 1)
+        assert np.array_equal(img_g, img_o)
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_max_direction_sector0_pdf_is_zero(rtmi_mod, oracle_mod, gpu_ctx):
+    """Frame 0 in max mode: every Q equal, so every volume's first largest sector is 0, whose
+    pdf the reference computes as cdf[0] - cdf[0] = 0 (radiance_volume.cu:274): paths that
+    bounce off a surface with a volume get an infinite throughput, as in the reference;
+    GPU and restatement agree on which pixels are non-finite and on all the others."""
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, "cornell")
+    try:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=32, height=32, spp=4)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
+        rm.set_sampling(rtmi_mod.sarsa.SAMPLE_MAX)
+        om.set_sampling(1)
+        img_g, casts_g = rm.render(cam, p, 1)
+        img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS["cornell"]), oracle_mod.params_from(p), 1)
+        assert casts_g == casts_o
+        assert not np.isfinite(img_g).all()
+        assert _same_bits_nan_aware(img_g, img_o)
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_q_table_load_round_trip(rtmi_mod, oracle_mod, gpu_ctx, tmp_path):
+    """rt_sarsa_save_q -> rt_sarsa_load_q into a fresh map of the same scene and seed ->
+    rt_sarsa_save_q: the same bytes; Q is the file's values, visits kept (zero), irradiance
+    and CDF as the restatement derives them from that Q, and the next frame renders and
+    learns bit-exactly like the restatement loaded with the same Q.  A map of another seed,
+    a truncated file and a file with a wrong action count are refused."""
+    S = rtmi_mod.sarsa
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, "door_room")
+    maps = [rm]
+    try:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=48, spp=8, spp_split=2)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+        rm.render(cam, p, 2)
+        f1, f2 = str(tmp_path / "q1.txt"), str(tmp_path / "q2.txt")
+        rm.save_q(f1)
+        fresh = S.RadianceMap(gpu_ctx, sc, 1984)
+        maps.append(fresh)
+        fresh.load_q(f1)
+        fresh.save_q(f2)
+        assert open(f1, "rb").read() == open(f2, "rb").read()
+        q, cdf, vis, acc = fresh.read()
+        _, fq = S.read_q_file(f1)
+        assert np.array_equal(q, fq.astype(np.float32))
+        assert not vis.any()
+        om.load_q(q)
+        _, ocdf, _, oacc = om.read()
+        assert np.array_equal(cdf, ocdf) and np.array_equal(acc, oacc)
+        img_g, casts_g = fresh.render(cam, p, 1)
+        img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS["door_room"]), oracle_mod.params_from(p), 1)
+        assert casts_g == casts_o and np.array_equal(img_g, img_o)
+        for a, b in zip(fresh.read(), om.read()):
+            assert np.array_equal(a, b)
+        other = S.RadianceMap(gpu_ctx, sc, 7)
+        maps.append(other)
+        with pytest.raises(rtmi_mod.RtError):
+            other.load_q(f1)
+        lines = open(f1).read().splitlines()
+        (tmp_path / "short.txt").write_text("\n".join(lines[:-1]) + "\n")
+        with pytest.raises(rtmi_mod.RtError):
+            fresh.load_q(str(tmp_path / "short.txt"))
+        (tmp_path / "bad.txt").write_text("\n".join(["100"] + lines[1:]) + "\n")
+        with pytest.raises(rtmi_mod.RtError):
+            fresh.load_q(str(tmp_path / "bad.txt"))
+    finally:
+        for m in maps:
+            m.close()
         sc.close()
 
 
@@ -357,12 +488,17 @@ def test_gpu_full_size_door_room_properties(rtmi_mod, gpu_ctx):
     try:
         p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=512, height=512, spp=256, spp_split=8)
         cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
-        lens = []
+        lens, logged = [], []
         for _ in range(3):
             img, casts = rm.render(cam, p, 1)
             lens.append(casts / (512 * 512 * 256))
+            paths, zero = rm.frame_stats()
+            logged.append(int(rm.append_stats_line(os.devnull, 512 * 512, (paths, zero)).split()[0]))
+            assert paths <= casts // 256 and 0 < zero < 512 * 512 * 256
             assert np.isfinite(img).all() and (img >= 0).all()
         assert ref[0] - 0.5 <= lens[0] <= ref[0] + 2.5
+        # the statistic the reference logs (floor of per-pixel floors), frame 0: 41 in its log
+        assert abs(logged[0] - ref[0]) <= 1, (logged, ref[:3])
         assert lens[2] < lens[0] * 0.6, lens
         q, cdf, vis, acc = rm.read()
         assert np.all(q >= np.float32(1 / np.float32(144)) * np.float32(0.8))
