@@ -1,7 +1,8 @@
 // reinforcement_main.cpp — the GPU engine's learned-sampling main loops
 // (GPU/main.cu:260-350 Expected SARSA, :420-470 pre-trained DQN) written against
-// the drop-in facade: load a scene, render frames, log the per-frame average path
-// length (the statistic of Radiance_Map_Data/sarsa_*.txt), save the last frame.
+// the drop-in facade: load a scene, render frames, log the per-frame statistics and
+// append them to sarsa_training_stats.txt (the format of Radiance_Map_Data/sarsa_*.txt),
+// save the Q-table (radiance_map_data.txt) and the last frame, in the working directory.
 //
 //   ./build/reinforcement_demo sarsa <scene.obj> <kind> [frames] [spp] [out.bmp]
 //   ./build/reinforcement_demo dqn <scene.obj> <kind> <model> [frames] [spp] [out.bmp]
@@ -62,10 +63,18 @@ int main(int argc, char** argv) {
             printf("radiance volumes: %d (KD array %d)\n", map.radiance_volumes_count, map.radiance_array_size);
             for (int f = 0; f < frames; ++f) {
                 const uint64_t casts = draw_reinforcement_path_tracing(screen, camera, map, spp);
-                update_radiance_volume_distributions(map);
                 printf("frame %d: average path length %.3f\n", f,
                        (double)casts / ((double)screen.width * screen.height * spp));
+                // GPU/main.cu:321-339: the logged statistics and the training-stats line
+                float avg = 0.f;
+                uint64_t zero = 0;
+                map.frame_stats(screen.width * screen.height, &avg, &zero);
+                printf("Average Path Length: %.3f\n", avg);
+                printf("Zero contribution light paths: %llu\n", (unsigned long long)zero);
+                map.append_training_stats("sarsa_training_stats.txt", screen.width * screen.height);
+                update_radiance_volume_distributions(map);
             }
+            map.save_q_vals_to_file("radiance_map_data.txt");  // SAVE_RADIANCE_MAP (main.cu:353-369)
         }
     } catch (const std::exception& e) {
         fprintf(stderr, "render failed: %s\n", e.what());

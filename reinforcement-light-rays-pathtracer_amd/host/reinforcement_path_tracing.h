@@ -14,6 +14,7 @@
 #pragma once
 
 #include <algorithm>
+#include <fstream>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -79,6 +80,31 @@ class RadianceMap {
         std::vector<float> q((size_t)radiance_volumes_count * 144);
         detail::check(rt_sarsa_read(map_, q.data(), nullptr, nullptr, nullptr));
         return q;
+    }
+
+    // RadianceMap::save_q_vals_to_file (radiance_map.cu:236-266) to `path`
+    void save_q_vals_to_file(const std::string& path) const { detail::check(rt_sarsa_save_q(map_, path.c_str())); }
+    // a saved Q-table back into this map (same scene and seed): resume training / render greedily
+    void read_q_vals_from_file(const std::string& path) { detail::check(rt_sarsa_load_q(map_, path.c_str())); }
+    // sample_max_direction_from_radiance_distribution (radiance_volume.cu:246-278) instead of the CDF
+    void set_sample_max_direction(bool on) {
+        detail::check(rt_sarsa_set_sampling(map_, on ? RT_SARSA_SAMPLE_MAX : RT_SARSA_SAMPLE_CDF));
+    }
+    // GPU/main.cu:321-339 after a frame: the average path length as the reference computes it
+    // (int(sum over pixels of int(path lengths / spp)) / pixels)) and the zero-contribution
+    // paths; append_training_stats writes its "avg 0 zero" line.
+    void frame_stats(int pixels, float* avg_path_length, uint64_t* zero_paths) const {
+        uint64_t paths = 0;
+        detail::check(rt_sarsa_frame_stats(map_, &paths, zero_paths));
+        *avg_path_length = (float)(paths / (uint64_t)pixels);
+    }
+    void append_training_stats(const std::string& path, int pixels) const {
+        float avg = 0.f;
+        uint64_t zero = 0;
+        frame_stats(pixels, &avg, &zero);
+        std::ofstream f(path, std::ios::app);
+        f << avg << " " << 0.0 << " " << zero << "\n";
+        if (!f) throw std::runtime_error("cannot append to " + path);
     }
 
     int radiance_volumes_count = 0;

@@ -48,14 +48,20 @@ def test_reinforcement_demo_sarsa_equals_c_abi(rtmi_mod, gpu_ctx, tmp_path):
     out = str(tmp_path / "sarsa.bmp")
     obj = os.path.join(MODELS, "door_room.obj")
     log = run(["reinforcement_demo", "sarsa", obj, "1", "2", "4", out], tmp_path)
-    assert log.count("average path length") == 2
+    assert log.count("average path length") == 2 and log.count("Zero contribution light paths") == 2
     got = read_bmp(out, 512, 512)
     geom = rtmi_mod.obj_geometry(obj, "door_room")
     p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=512, height=512, spp=4)
+    lines = []
     with rtmi_mod.Scene(gpu_ctx, geom) as sc, rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) as rm:
-        rm.render(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p, 1)
-        img, _ = rm.render(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p, 1)
+        for _ in range(2):
+            img, _ = rm.render(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p, 1)
+            lines.append(rtmi_mod.sarsa.stats_line(*rm.frame_stats(), 512 * 512))
+        rm.save_q(str(tmp_path / "q_abi.txt"))
     assert np.array_equal(got, rtmi_mod.pack_argb(img))
+    # the training-stats lines and the saved Q-table of the facade's loop
+    assert open(tmp_path / "sarsa_training_stats.txt").read() == "".join(lines)
+    assert open(tmp_path / "radiance_map_data.txt").read() == open(tmp_path / "q_abi.txt").read()
 
 
 def test_reinforcement_demo_dqn_equals_c_abi(rtmi_mod, gpu_ctx, tmp_path):
