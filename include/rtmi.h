@@ -193,6 +193,13 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
                   int n_out, const float* const* W /* 4 */, const float* const* b /* 4 */,
                   rt_dqn** out);
 int rt_dqn_destroy(rt_dqn* dqn);
+/* Kernel of the forward pass (same Q bit for bit; for A/B measurement):
+ * RT_DQN_MLP_AUTO (default) the weight-stationary kernel (weights resident in registers,
+ * one workgroup per CU) when the network has the reference's 200-300-200 shape, else the
+ * weight-streaming one; RT_DQN_MLP_STREAM always the weight-streaming kernel. */
+#define RT_DQN_MLP_AUTO 0
+#define RT_DQN_MLP_STREAM 1
+int rt_dqn_set_mlp(rt_dqn* dqn, int mode);
 /* DQNetwork::network_inference on n ray positions (host arrays): q = n x 144. */
 int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc /* n x 3 */, int n, float* q);
 /* Same on device buffers, asynchronous on `stream`. */

@@ -536,6 +536,15 @@ __global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, fl
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
                           int max_rows, float* q, int ldq, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
+    // the weight-stationary kernel (rt_dqn_ws.hip) for the reference's 200-300-200 network,
+    // this file's weight-streaming kernel for other widths (or when asked: rt_dqn_set_mlp)
+    if (net.mlp_mode != kMlpStream && dqn_mlp_ws_fits(net)) {
+        int dev = 0, n_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        return launch_dqn_mlp_ws(net, loc, list, count, max_rows, q, ldq, n_cu, stream);
+    }
     const int blocks = (max_rows + kTileM - 1) / kTileM;
     if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc, list, count,

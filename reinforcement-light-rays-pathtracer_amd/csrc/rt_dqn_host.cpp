@@ -249,6 +249,15 @@ int rt_dqn_destroy(rt_dqn* dqn) {
     return RT_OK;
 }
 
+static_assert(RT_DQN_MLP_STREAM == rt::kMlpStream, "MLP mode constants");
+
+int rt_dqn_set_mlp(rt_dqn* dqn, int mode) {
+    if (!dqn) return err(RT_E_INVALID, "NULL argument");
+    if (mode != RT_DQN_MLP_AUTO && mode != RT_DQN_MLP_STREAM) return err(RT_E_INVALID, "bad MLP kernel mode");
+    dqn->net.mlp_mode = mode;
+    return RT_OK;
+}
+
 int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc, int n, float* q) {
     if (!ctx || !dqn || (n > 0 && (!loc || !q))) return err(RT_E_INVALID, "NULL argument");
     if (n < 0) return err(RT_E_INVALID, "n < 0");

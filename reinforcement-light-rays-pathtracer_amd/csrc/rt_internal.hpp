@@ -101,6 +101,7 @@ inline int filter_usable(const DeviceScene& s, float cx, float cy, float cz, flo
 constexpr int kDqnActions = 144;  // GRID_RESOLUTION^2 (GPU/constants/radiance_volumes_settings.h:9)
 constexpr int kDqnGrid = 12;
 
+constexpr int kMlpStream = 1;  // RT_DQN_MLP_STREAM
 struct DqnNet {
     // layer 0 folded: [N[0]] x {-S0, -S1, -S2, c0}; h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x)))
     const float4* l0 = nullptr;
@@ -110,6 +111,7 @@ struct DqnNet {
     const float* b[4] = {nullptr, nullptr, nullptr, nullptr};      // fp32, padded (b[0] unused)
     int K[4] = {0, 0, 0, 0};      // padded input width of each layer (K[0] = n_in, unpadded)
     int N[4] = {0, 0, 0, 0};      // padded output width of each layer (multiple of 32; last = 144)
+    int mlp_mode = 0;             // RT_DQN_MLP_* (rtmi.h rt_dqn_set_mlp): kMlpStream = weight streaming
 };
 
 // Ray state of the DQN wavefront renderer (SoA over the rays of a frame part).
@@ -154,6 +156,10 @@ struct DqnLaunch {
 // ldq a multiple of 64 covering every launched row (the renderer's, coalesced per action)
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
                           const int32_t* count, int max_rows, float* q, int ldq, hipStream_t stream);
+// weight-stationary forward (rt_dqn_ws.hip): one workgroup per CU, the 200-300-200 shape
+bool dqn_mlp_ws_fits(const DqnNet& net);
+hipError_t launch_dqn_mlp_ws(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
+                             int max_rows, float* q, int ldq, int n_cu, hipStream_t stream);
 hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream);
 hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream);  // samples s0 .. s0 + n/n_pix - 1
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream);

@@ -37,7 +37,7 @@ EXPORTS = (
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
     "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
     "rt_pack_argb", "rt_save_bmp", "rt_save_png", "rt_selftest", "rt_filter_build", "rt_rect_candidates", "rt_cull_masks_device",
-    "rt_dynet_read", "rt_dynet_write", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_forward", "rt_dqn_forward_device",
+    "rt_dynet_read", "rt_dynet_write", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_set_mlp", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
     "rt_sarsa_create", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
@@ -112,6 +112,7 @@ def _declare(lib):
         "rt_dynet_read": (i, [ctypes.c_char_p, i, _IP, _IP, _FP, ctypes.POINTER(i),
                               ctypes.POINTER(ctypes.c_int64)]),
         "rt_dynet_write": (i, [ctypes.c_char_p, i, _IP, _IP, _FP]),
+        "rt_dqn_set_mlp": (i, [_P, i]),
         "rt_dqn_create": (i, [_P, _FP, i, _IP, i, ctypes.POINTER(_FP), ctypes.POINTER(_FP),
                               ctypes.POINTER(_P)]),
         "rt_dqn_destroy": (i, [_P]),

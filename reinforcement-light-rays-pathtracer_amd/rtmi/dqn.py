@@ -105,6 +105,12 @@ class Dqn:
     def handle(self):
         return self._h
 
+    MLP_AUTO, MLP_STREAM = 0, 1  # RT_DQN_MLP_*
+
+    def set_mlp(self, mode: int) -> None:
+        """forward kernel: MLP_AUTO (weight-stationary for the 200-300-200 shape) or MLP_STREAM"""
+        check(lib().rt_dqn_set_mlp(self._h, mode))
+
     def forward(self, loc: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(loc, np.float32).reshape(-1, 3)
         q = np.zeros((x.shape[0], ACTIONS), np.float32)

@@ -15,6 +15,7 @@ HIP events on the launch stream), written as one JSON document.
   c5  complex_light_room 2048^2, 8-GPU tile split: the tile set of every rank r of
       P = 8 rendered alone on this GPU at `--c5-spp` samples: max_r is the kernel
       part of one 8-GPU frame, the sum the 1-GPU frame.
+  cpu the CPU restatement's ray-cast rate on bounded samples of c3-c5 (this host).
 """
 import argparse
 import json
@@ -146,6 +147,46 @@ def c5(ctx, stream, spp, world=8):
             "ms_1024spp_8gpu_extrapolated": round(max(per) * 1024 / spp, 0)}
 
 
+def cpu_configs(which):
+    """The CPU restatement (oracle/, OpenMP over rows, this host's cores) on a bounded sample
+    of configs 3-5: ray casts per second, to set beside the GPU's.  Per-sample cost does not
+    depend on spp within a frame, so a few spp stand for the configs' 256/512/1024."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # the CPU restatement: CPU baseline only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    oracle.set_threads(threads)
+    out = {}
+    if "c3" in which:  # frame 0 of Expected SARSA (TD accumulation and the end-of-frame update)
+        g = rtmi.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+        m = oracle.Sarsa(g, 1984)
+        p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=512, height=512, spp=2)
+        t0 = time.perf_counter()
+        _, c = m.render(oracle.camera(rtmi.CAMERAS["door_room"]), oracle.params_from(p), 1)
+        dt = time.perf_counter() - t0
+        out["c3"] = {"sample": "door_room 512^2 x 2 spp, frame 0", "ray_casts": c, "s": round(dt, 2),
+                     "cpu_mrays_s": round(c / dt / 1e6, 2), "threads": threads}
+    if "c4" in which:  # DQN sampling with the bf16-emulating forward (prepared weights)
+        g = rtmi.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+        W, b = rtmi.dqn.synthetic_weights(g.nn_vertices.size)
+        p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=1024, height=1024, spp=1)
+        t0 = time.perf_counter()
+        _, c = oracle.render_dqn(g, W, b, g.nn_vertices, oracle.camera(rtmi.CAMERAS["archway"]),
+                                 oracle.params_from(p), (448, 448, 64, 64), bf16=True)
+        dt = time.perf_counter() - t0
+        out["c4"] = {"sample": "archway 1024^2 window 64^2 at (448, 448) x 1 spp", "ray_casts": c,
+                     "s": round(dt, 2), "cpu_mrays_s": round(c / dt / 1e6, 3), "threads": threads}
+    if "c5" in which:
+        g = rtmi.obj_geometry(os.path.join(MODELS, "complex_light_room.obj"), "complex_light_room")
+        p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=2048, height=2048, spp=4)
+        t0 = time.perf_counter()
+        _, c = oracle.render(g, oracle.camera(rtmi.CAMERAS["complex_light_room"]), oracle.params_from(p),
+                             (0, 1008, 2048, 32))
+        dt = time.perf_counter() - t0
+        out["c5"] = {"sample": "complex_light_room 2048^2 rows 1008..1039 x 4 spp", "ray_casts": c,
+                     "s": round(dt, 2), "cpu_mrays_s": round(c / dt / 1e6, 2), "threads": threads}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "configs.json"))
@@ -153,6 +194,8 @@ def main():
     ap.add_argument("--dqn-spp", type=int, default=16)
     ap.add_argument("--c5-spp", type=int, default=64)
     ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--cpu", nargs="*", default=["c3", "c4", "c5"],
+                    help="configs whose CPU-restatement rate to measure (empty: none)")
     args = ap.parse_args()
     stream = torch.cuda.current_stream()
     res = {"device": torch.cuda.get_device_name(0)}
@@ -165,6 +208,9 @@ def main():
                 continue
             res[k] = fn()
             print(k, json.dumps(res[k]), flush=True)
+    if args.cpu:
+        res["cpu"] = cpu_configs(args.cpu)
+        print("cpu", json.dumps(res["cpu"]), flush=True)
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as fh:
         json.dump(res, fh, indent=1)
