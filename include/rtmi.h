@@ -193,12 +193,14 @@ int rt_dqn_create(rt_ctx* ctx, const float* nn_vertices, int n_in, const int32_t
                   int n_out, const float* const* W /* 4 */, const float* const* b /* 4 */,
                   rt_dqn** out);
 int rt_dqn_destroy(rt_dqn* dqn);
-/* Kernel of the forward pass (same Q bit for bit; for A/B measurement):
- * RT_DQN_MLP_AUTO (default) the weight-stationary kernel (weights resident in registers,
- * one workgroup per CU) when the network has the reference's 200-300-200 shape, else the
- * weight-streaming one; RT_DQN_MLP_STREAM always the weight-streaming kernel. */
+/* Kernel of the forward pass (same Q bit for bit; A/B measurement):
+ * RT_DQN_MLP_AUTO (default) and RT_DQN_MLP_STREAM: the weight-streaming kernel (64 rays per
+ * workgroup, weight fragments from L2); RT_DQN_MLP_STATIONARY: the weight-stationary one
+ * (weights resident in registers, one workgroup per CU) for the reference's 200-300-200
+ * shape, the streaming one otherwise. */
 #define RT_DQN_MLP_AUTO 0
 #define RT_DQN_MLP_STREAM 1
+#define RT_DQN_MLP_STATIONARY 2
 int rt_dqn_set_mlp(rt_dqn* dqn, int mode);
 /* DQNetwork::network_inference on n ray positions (host arrays): q = n x 144. */
 int rt_dqn_forward(rt_ctx* ctx, const rt_dqn* dqn, const float* loc /* n x 3 */, int n, float* q);
@@ -257,6 +259,32 @@ int rt_dqn_train_step_device(rt_ctx* ctx, rt_dqn_trainer* trainer, const float* 
 int rt_dqn_td_targets_device(rt_ctx* ctx, uint64_t seed, const float* d_next_q, const int32_t* d_terminal,
                              const float* d_reward, const float* d_discount, const uint32_t* d_pix, int sample,
                              int bounce, int n, float* d_target, void* stream);
+
+/* NeuralQPathtracer (GPU/deep_learning/neural_q_pathtracer.cu:226-600): renders while
+ * training `trainer`'s network, on the device.  Per sample: initialise_ray (:604-643); per
+ * bounce b until no path is bouncing or max_bounces: (b > 0) the network's Q at every ray's
+ * position and sample_batch_ray_directions_epsilon_greedy (nn_rendering_helpers.cu:330-389:
+ * importance_sample_direction with probability 1 - epsilon, else a uniform cell), trace_ray
+ * (:646-745: rewards 0 / light luminance x 200, discount = the surface's luminance,
+ * throughput on contributing paths), (b > 0) the learning rule per batch of batch_size rays
+ * (compute_td_targets on the new positions, trainer.update on the old ones with the sampled
+ * actions, neural_q_pathtracer.cu:420-513), sample_random_scene_pos_for_terminated_rays
+ * (:241-277, restarted rays learn but no longer contribute; the point is stored with y and
+ * z exchanged, as the reference stores it).  After a sample epsilon = max(epsilon -
+ * decay, min) (:543-546).  The frame is the throughput summed over the samples / spp.
+ * Reference settings: batch 4096, epsilon 0.05 / 0.05 / 0.01 (deep_learning_settings.h).
+ * stats (optional, spp x 3 floats): per sample the nn_training_stats.txt values (:553-583):
+ * average path length (sum of termination bounces / pixels), loss (summed over batches),
+ * zero-contribution paths ((r + g + b) / 3 < THROUGHPUT_THRESHOLD).  out_rgb: W x H x 3 or
+ * NULL.  Pixel ids key the RNG (Philox; seed = params->seed); successive frames continue
+ * the sample sequence. */
+typedef struct rt_neuralq rt_neuralq;
+int rt_neuralq_create(rt_ctx* ctx, const rt_scene* scene, rt_dqn_trainer* trainer, int batch_size,
+                      float epsilon_start, float epsilon_min, float epsilon_decay, rt_neuralq** out);
+int rt_neuralq_destroy(rt_neuralq* nq);
+int rt_neuralq_epsilon(const rt_neuralq* nq, float* epsilon);
+int rt_neuralq_render_frame(rt_ctx* ctx, rt_neuralq* nq, const rt_camera* cam, const rt_params* params,
+                            float* out_rgb, float* stats, uint64_t* out_ray_casts);
 
 /* ---- Expected-SARSA radiance volumes (BASELINE config 3) ------------------ */
 typedef struct rt_sarsa rt_sarsa;

@@ -50,8 +50,16 @@ constexpr int slots(int tiles) { return (tiles + kMlpWaves - 1) / kMlpWaves; }
 // MT = 8 (one 142 KB workgroup per CU) is 1.4x slower; a single flattened weight
 // stream over layers 1-3 with a 2-4 deep register ring was 2x slower (round-1 A/B,
 // DESIGN.md §4).
-constexpr int kStrideA = 320 + 8; // LDS row strides in bf16 elements (+16 B pad)
-constexpr int kStrideB = 224 + 8;
+// LDS activation rows (bf16) are XOR-swizzled at 16-B granularity, slot ^ ((row >> 2) & 7),
+// on strides of 336 / 272 elements: the B-operand ds_read_b128 of each 16-lane group then
+// hits 16 distinct 16-B slots (conflict-free; the padded 328 / 232 rows were 2-way) and
+// the 8-B epilogue stores are 2-way (bank rule of MI355X_MICROARCH.md §LDS, brute-forced
+// over strides and swizzles)
+constexpr int kStrideA = 336;
+constexpr int kStrideB = 272;
+__device__ __forceinline__ int swz(int row, int k, int stride) {
+    return row * stride + (((k >> 3) ^ ((row >> 2) & 7)) << 3) + (k & 7);
+}
 constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
 static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
@@ -109,7 +117,7 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
             bf16x4 h;
 #pragma unroll
             for (int r = 0; r < 4; ++r) h[r] = (__bf16)(d[r] > 0.0f ? d[r] : 0.0f);
-            *reinterpret_cast<bf16x4*>(out_lds + (m * 16 + r16) * out_stride + nt * 16 + kq * 4) = h;
+            *reinterpret_cast<bf16x4*>(out_lds + swz(m * 16 + r16, nt * 16 + kq * 4, out_stride)) = h;
         }
     }
 }
@@ -123,7 +131,7 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 // unconditional: a conditional MFMA makes the compiler shuttle every accumulator
 // between AGPRs and VGPRs each K step) and are not stored.
 // ---------------------------------------------------------------------------
-template <int NT, bool LAST, int MT>
+template <int NT, bool LAST, int MT, int KS = 0>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
                                           __bf16* out_lds, int out_stride) {
     const int lane = threadIdx.x & 63;
@@ -143,6 +151,43 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     for (int m = 0; m < MT; ++m)
 #pragma unroll
         for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (KS > 0) {
+        // K known at compile time (the reference's 200-300-200 shape): the weight
+        // fragments of step k+2 and the activations of step k+1 are in flight while the
+        // MFMAs of step k run (a 3-deep register ring, fully unrolled: no copies)
+        bf16x8 bw[3][NT], a[2][MT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bw[0][j] = *reinterpret_cast<const bf16x8*>(wrow[j]);
+        if (KS > 1) {
+#pragma unroll
+            for (int j = 0; j < NT; ++j) bw[1][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + 32 * 16);
+        }
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+            a[0][m] = *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, kg, in_stride));
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+            if (ks + 2 < KS) {
+#pragma unroll
+                for (int j = 0; j < NT; ++j)
+                    bw[(ks + 2) % 3][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + (ks + 2) * 32 * 16);
+            }
+            if (ks + 1 < KS) {
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    a[(ks + 1) & 1][m] =
+                        *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, (ks + 1) * 32 + kg, in_stride));
+            }
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % 3][j], a[ks & 1][m], acc[m][j], 0, 0, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);       // VMEM reads
+            __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);       // LDS reads
+            __builtin_amdgcn_sched_group_barrier(0x008, NT * MT, 0);  // MFMA
+        }
+    } else {
     // weight fragments ping-pong between b0 and b1 (no register copies, which would
     // make the loads of step k+1 wait inside step k): step k's MFMAs run while step
     // k+1's fragments are in flight; sched_group_barrier keeps the order
@@ -154,7 +199,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         bf16x8 a[MT];
 #pragma unroll
         for (int m = 0; m < MT; ++m)
-            a[m] = *reinterpret_cast<const bf16x8*>(in_lds + (m * 16 + r16) * in_stride + k0 + kg);
+            a[m] = *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, k0 + kg, in_stride));
 #pragma unroll
         for (int j = 0; j < NT; ++j)
 #pragma unroll
@@ -178,6 +223,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         __builtin_amdgcn_sched_group_barrier(0x008, NT * MT, 0);
     }
     if (k0 < K) step(k0, b0);  // odd number of K steps
+    }
     // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
     // (the weights are the MFMA's A operand, the activations its B operand, so a lane
     // holds 4 consecutive features of one ray: one 8-B (bf16) or 16-B (fp32) LDS store)
@@ -208,13 +254,13 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
                 bf16x4 h;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) h[r] = (__bf16)v[r];
-                *reinterpret_cast<bf16x4*>(out_lds + row * out_stride + col) = h;
+                *reinterpret_cast<bf16x4*>(out_lds + swz(row, col, out_stride)) = h;
             }
         }
     }
 }
 
-// One workgroup = MT*16 rays (LDS: MT=4 -> 71 KB, two workgroups per CU).
+// One workgroup = MT*16 rays (LDS: MT=4 -> 77 KB, two workgroups per CU).
 template <int MT>
 __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
@@ -246,11 +292,19 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
 #endif
     __syncthreads();
-    mlp_layer<slots(20), false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
-    __syncthreads();
-    mlp_layer<slots(14), false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB);  // N <= 224
-    __syncthreads();
-    mlp_layer<slots(9), true, MT>(net, 3, bufB, kStrideB, bufA, 0);           // N = 144
+    if (net.K[1] == 224 && net.K[2] == 320 && net.K[3] == 224) {  // the reference's 200-300-200 net
+        mlp_layer<slots(20), false, MT, 7>(net, 1, bufB, kStrideB, bufA, kStrideA);
+        __syncthreads();
+        mlp_layer<slots(14), false, MT, 10>(net, 2, bufA, kStrideA, bufB, kStrideB);
+        __syncthreads();
+        mlp_layer<slots(9), true, MT, 7>(net, 3, bufB, kStrideB, bufA, 0);
+    } else {
+        mlp_layer<slots(20), false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
+        __syncthreads();
+        mlp_layer<slots(14), false, MT>(net, 2, bufA, kStrideA, bufB, kStrideB);  // N <= 224
+        __syncthreads();
+        mlp_layer<slots(9), true, MT>(net, 3, bufB, kStrideB, bufA, 0);           // N = 144
+    }
     __syncthreads();
     // Q tile [kRows][144] from LDS (odd row stride: conflict-free column reads) in
     // 16-B stores: row-major rows are one contiguous run, action-major columns runs
@@ -398,6 +452,22 @@ __global__ __launch_bounds__(256) void k_dqn_frame_begin(const DqnLaunch a) {
     st3(a.rays.total, rid, make3(0.0f, 0.0f, 0.0f));
 }
 
+// Ray::sample_ray_through_pixel's direction for the jittered pixel position (x, y)
+__device__ __forceinline__ f3 dqn_camera_dir(const DqnLaunch& a, float x, float y) {
+    const f3 dir = normalize(make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height));
+    const float w = 1.0f;
+    f3 r;
+    r.x = (a.cos_y * dir.x + 0.0f * dir.y) + (-a.sin_y * dir.z + 0.0f * w);
+    r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
+    r.z = (a.sin_y * dir.x + 0.0f * dir.y) + (a.cos_y * dir.z + 0.0f * w);
+    const float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
+    f3 d;
+    d.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
+    d.y = (0.0f * r.x + a.cos_x * r.y) + (a.sin_x * r.z + 0.0f * rw);
+    d.z = (0.0f * r.x + -a.sin_x * r.y) + (a.cos_x * r.z + 0.0f * rw);
+    return d;
+}
+
 // initialise_ray + the first trace_ray (bounce 0: no Q evaluation)
 __global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a) {
     const int rid = blockIdx.x * 256 + threadIdx.x;
@@ -413,17 +483,7 @@ __global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a) {
             float r1, r2;
             draw2(a.rays.pix[pi], (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
             const float x = (float)px + r1, y = (float)py + r2;
-            f3 dir = normalize(make3(x - (float)a.width / 2.0f, y - (float)a.height / 2.0f, (float)a.height));
-            const float w = 1.0f;
-            f3 r;
-            r.x = (a.cos_y * dir.x + 0.0f * dir.y) + (-a.sin_y * dir.z + 0.0f * w);
-            r.y = (0.0f * dir.x + 1.0f * dir.y) + (0.0f * dir.z + 0.0f * w);
-            r.z = (a.sin_y * dir.x + 0.0f * dir.y) + (a.cos_y * dir.z + 0.0f * w);
-            const float rw = (0.0f * dir.x + 0.0f * dir.y) + (0.0f * dir.z + 1.0f * w);
-            f3 d;
-            d.x = (1.0f * r.x + 0.0f * r.y) + (0.0f * r.z + 0.0f * rw);
-            d.y = (0.0f * r.x + a.cos_x * r.y) + (a.sin_x * r.z + 0.0f * rw);
-            d.z = (0.0f * r.x + -a.sin_x * r.y) + (a.cos_x * r.z + 0.0f * rw);
+            const f3 d = dqn_camera_dir(a, x, y);
             f3 loc;
             int tri = 0;
             keep = dqn_trace(a, make3(a.cam_x, a.cam_y, a.cam_z), d, &loc, &tri, &tp);
@@ -531,14 +591,204 @@ __global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, fl
     action[i] = so.action;
 }
 
+// ---------------------------------------------------------------------------
+// Neural-Q training renderer (NeuralQPathtracer::render_frame,
+// GPU/deep_learning/neural_q_pathtracer.cu:226-600): every ray of the frame steps through
+// every bounce of a sample (terminated rays are restarted on the scene and keep feeding
+// the learning rule), the network being trained between bounces (rt_train.hip).
+// Philox events (pixel id, sample, event, counter): 0 camera jitter, 1 + b the Q-weighted
+// sampler of bounce b, kNqEvGreedy + b the epsilon draw / exploration cell and jitters,
+// kNqEvRestart + b and kNqEvRestartPos + b a restart's surface and position.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kNqEvGreedy = 0x1000u, kNqEvRestart = 0x2000u, kNqEvRestartPos = 0x3000u;
+constexpr float kThroughputThreshold = 0.0001f;  // THROUGHPUT_THRESHOLD (constants/monte_carlo_settings.h:11)
+
+// initialise_ray (neural_q_pathtracer.cu:604-643)
+__global__ __launch_bounds__(256) void k_nq_init(const DqnLaunch a, const NqRays r, int sample) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= r.n) return;
+    const int px = i % a.width, py = i / a.width;
+    float r1, r2;
+    draw2((uint32_t)i, (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+    const f3 d = dqn_camera_dir(a, (float)px + r1, (float)py + r2);
+    const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
+    st3(r.loc, i, cam);
+    st3(r.prev, i, cam);
+    st3(r.dir, i, d);
+    st3(r.tp, i, make3(1.0f, 1.0f, 1.0f));
+    r.tri[i] = -1;
+    r.state[i] = 0u;
+    r.reward[i] = 0.0f;
+    r.discount[i] = 1.0f;
+    r.bounces[i] = (uint32_t)a.max_bounces;
+    r.action[i] = 0;
+    r.pix[i] = (uint32_t)i;
+}
+
+// sample_batch_ray_directions_epsilon_greedy (nn_rendering_helpers.cu:330-389): with
+// probability 1 - eps importance_sample_direction on Q (sample_from_q; a ray whose Q admits
+// no cell keeps its direction, the reference's loop finding nothing), else a uniformly
+// chosen cell, (u - 0.0001) * 144, jittered (sample_ray_for_grid_index, :4-35:
+// throughput * cos / RHO).  q: [n][144], overwritten with Q * cos on the greedy rows.
+__global__ __launch_bounds__(256) void k_nq_sample(const DqnLaunch a, const NqRays r, float* q, float eps,
+                                                   int sample, int bounce) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= r.n) return;
+    const int tri = r.tri[i];
+    const float4 N4 = a.scene.shade[tri * kShadeF4 + 0];
+    const float4 T4 = a.scene.shade[tri * kShadeF4 + 1];
+    const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
+    const f3 N = make3(N4.x, N4.y, N4.z), T = make3(T4.x, T4.y, T4.z), B = make3(B4.x, B4.y, B4.z);
+    const f3 pos = ld3(r.loc, i);
+    f3 tp = ld3(r.tp, i);
+    const bool live = r.state[i] == 0u;
+    uint32_t o[4];
+    philox4x32_10(r.pix[i], (uint32_t)sample, kNqEvGreedy + (uint32_t)bounce, 0u, a.seed_lo, a.seed_hi, o);
+    const float rv = u01_oc(o[0]);
+    if (rv > eps) {
+        const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, 1, N, T, B, pos, r.pix[i], (uint32_t)sample,
+                                           1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, live);
+        if (so.action >= 0) {
+            st3(r.dir, i, so.dir);
+            r.action[i] = so.action;
+        } else {
+            r.action[i] = 0;
+        }
+    } else {
+        const float u = u01_oc(o[1]) - 0.0001f;
+        int idx = (int)(u * (float)kDqnActions);
+        idx = idx < 0 ? 0 : (idx > kDqnActions - 1 ? kDqnActions - 1 : idx);
+        const int gx = idx / kDqnGrid, gy = idx - gx * kDqnGrid;
+        const f3 d = grid_direction((float)gx + u01(o[2]), (float)gy + u01(o[3]), N, T, B, pos);
+        if (live) {
+            const float c = dot(N, d);
+            tp = make3((tp.x * c) / kRho, (tp.y * c) / kRho, (tp.z * c) / kRho);
+        }
+        st3(r.dir, i, d);
+        r.action[i] = idx;
+    }
+    st3(r.tp, i, tp);
+}
+
+// trace_ray (neural_q_pathtracer.cu:646-745): Ray(pos + dir * 1e-5, dir), GPU hit rule;
+// miss: reward 0, terminal; light: reward = its luminance x 200, terminal; surface: the
+// new state, discount = the material's luminance.  Throughputs and path lengths change
+// only for paths still contributing (state 0).  The position before the trace is the
+// learning rule's S_t.
+__global__ __launch_bounds__(256) void k_nq_trace(const DqnLaunch a, const NqRays r, int bounce) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    unsigned casts = 0;
+    if (i < r.n) {
+        const f3 pos = ld3(r.loc, i), dir = ld3(r.dir, i);
+        st3(r.prev, i, pos);
+        const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
+        const f3 d = normalize(dir);
+        const Hit h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
+        casts = 1;
+        const uint32_t st = r.state[i];
+        f3 tp = ld3(r.tp, i);
+        if (h.tri < 0 || h.tri >= a.scene.n_surf) {
+            const bool light = h.tri >= 0;
+            r.reward[i] = light ? r.tri_lum[h.tri] * 200.0f : 0.0f;
+            r.discount[i] = 0.0f;
+            if (st == 0u) {
+                if (light) {
+                    const float4 e = a.scene.shade[h.tri * kShadeF4 + 3];
+                    tp = make3(tp.x * e.x, tp.y * e.y, tp.z * e.z);
+                } else {
+                    tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+                }
+                r.bounces[i] = (uint32_t)bounce;
+            }
+            r.state[i] = 1u;
+            r.terminal[i] = 1;
+        } else {
+            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+            st3(r.loc, i, make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz));
+            r.tri[i] = h.tri;
+            if (st == 0u) {
+                const float4 c = a.scene.shade[h.tri * kShadeF4 + 3];  // diffuse_c / pi
+                tp = make3(tp.x * c.x, tp.y * c.y, tp.z * c.z);
+                r.flag[0] = 0;  // a path still bounces (a vector store; every writer stores 0)
+            }
+            r.reward[i] = 0.0f;
+            r.discount[i] = r.tri_lum[h.tri];
+            r.terminal[i] = 0;
+        }
+        st3(r.tp, i, tp);
+    }
+    const unsigned tot = wave_sum_u(casts);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&r.stats[2], (unsigned long long)tot);
+}
+
+// sample_random_scene_pos_for_terminated_rays (nn_rendering_helpers.cu:241-277): a random
+// surface, floor(surfaces_count * u), a point on it by rejection (Triangle::
+// sample_position_on_plane), stored with its y and z exchanged as the reference stores
+// it (ray_locations[i*3+2] = pos.y, [i*3+1] = pos.z); its normal; state 2.
+__global__ __launch_bounds__(256) void k_nq_restart(const DqnLaunch a, const NqRays r, int sample, int bounce) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= r.n || r.state[i] != 1u) return;
+    uint32_t o[4];
+    philox4x32_10(r.pix[i], (uint32_t)sample, kNqEvRestart + (uint32_t)bounce, 0u, a.seed_lo, a.seed_hi, o);
+    int s = (int)((float)a.scene.n_surf * u01_oc(o[0]));
+    s = s < a.scene.n_surf ? s : a.scene.n_surf - 1;
+    const float* v = r.surf_v + (size_t)s * 9;
+    float a1, a2;
+    uint32_t attempt = 0;
+    do {
+        philox4x32_10(r.pix[i], (uint32_t)sample, kNqEvRestartPos + (uint32_t)bounce, attempt++, a.seed_lo, a.seed_hi,
+                      o);
+        a1 = u01_oc(o[0]);
+        a2 = u01_oc(o[1]);
+    } while (a1 + a2 > 1.0f && attempt < 64u);
+    if (a1 + a2 > 1.0f) {  // (probability 2^-64: keep the point on the triangle)
+        a1 = 1.0f - a1;
+        a2 = 1.0f - a2;
+    }
+    float p[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) p[c] = (v[c] + a1 * (v[3 + c] - v[c])) + a2 * (v[6 + c] - v[c]);
+    st3(r.loc, i, make3(p[0], p[2], p[1]));
+    r.tri[i] = s;
+    r.state[i] = 2u;
+}
+
+// end of a sample: update_total_throughput (every ray's throughput, as the reference adds
+// it), sum_path_lengths and sum_zero_contribution_light_paths (nn_rendering_helpers.cu)
+__global__ __launch_bounds__(256) void k_nq_end_sample(const DqnLaunch a, const NqRays r) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    unsigned b = 0, z = 0;
+    if (i < r.n) {
+        const f3 tp = ld3(r.tp, i);
+        const f3 t = ld3(r.total, i);
+        st3(r.total, i, make3(t.x + tp.x, t.y + tp.y, t.z + tp.z));
+        b = r.bounces[i];
+        z = ((tp.x + tp.y + tp.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
+    }
+    const unsigned sb = wave_sum_u(b), sz = wave_sum_u(z);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&r.stats[0], (unsigned long long)sb);
+        atomicAdd(&r.stats[1], (unsigned long long)sz);
+    }
+}
+
+// update_device_buffer (nn_rendering_helpers.cu:159-172): the frame = total / SPP
+__global__ __launch_bounds__(256) void k_nq_image(const DqnLaunch a, const NqRays r, float* out, int spp) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= r.n) return;
+    const f3 t = ld3(r.total, i);
+    const float fs = (float)spp;
+    st3(out, i, make3(t.x / fs, t.y / fs, t.z / fs));
+}
+
 }  // namespace
 
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
                           int max_rows, float* q, int ldq, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
-    // the weight-stationary kernel (rt_dqn_ws.hip) for the reference's 200-300-200 network,
-    // this file's weight-streaming kernel for other widths (or when asked: rt_dqn_set_mlp)
-    if (net.mlp_mode != kMlpStream && dqn_mlp_ws_fits(net)) {
+    // this file's weight-streaming kernel; the weight-stationary one (rt_dqn_ws.hip) when
+    // asked (rt_dqn_set_mlp) and the network has the 200-300-200 shape
+    if (net.mlp_mode == kMlpStationary && dqn_mlp_ws_fits(net)) {
         int dev = 0, n_cu = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -592,6 +842,34 @@ hipError_t launch_dqn_sample_only(const DeviceScene& s, const float* q, const fl
     hipLaunchKernelGGL(k_dqn_sample_only, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, s,
                        const_cast<float*>(q), loc, tri, pix, n, sample, bounce, seed_lo, seed_hi, tp, dir_out,
                        action);
+    return hipGetLastError();
+}
+
+static unsigned nq_blocks(const NqRays& r) { return (unsigned)((r.n + 255) / 256); }
+
+hipError_t launch_nq_init(const DqnLaunch& a, const NqRays& r, int sample, hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_init, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, sample);
+    return hipGetLastError();
+}
+hipError_t launch_nq_sample(const DqnLaunch& a, const NqRays& r, float* q, float eps, int sample, int bounce,
+                            hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_sample, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, q, eps, sample, bounce);
+    return hipGetLastError();
+}
+hipError_t launch_nq_trace(const DqnLaunch& a, const NqRays& r, int bounce, hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_trace, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, bounce);
+    return hipGetLastError();
+}
+hipError_t launch_nq_restart(const DqnLaunch& a, const NqRays& r, int sample, int bounce, hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_restart, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, sample, bounce);
+    return hipGetLastError();
+}
+hipError_t launch_nq_end_sample(const DqnLaunch& a, const NqRays& r, hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_end_sample, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r);
+    return hipGetLastError();
+}
+hipError_t launch_nq_image(const DqnLaunch& a, const NqRays& r, float* out, int spp, hipStream_t stream) {
+    hipLaunchKernelGGL(k_nq_image, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, out, spp);
     return hipGetLastError();
 }
 

@@ -249,11 +249,12 @@ int rt_dqn_destroy(rt_dqn* dqn) {
     return RT_OK;
 }
 
-static_assert(RT_DQN_MLP_STREAM == rt::kMlpStream, "MLP mode constants");
+static_assert(RT_DQN_MLP_STATIONARY == rt::kMlpStationary, "MLP mode constants");
 
 int rt_dqn_set_mlp(rt_dqn* dqn, int mode) {
     if (!dqn) return err(RT_E_INVALID, "NULL argument");
-    if (mode != RT_DQN_MLP_AUTO && mode != RT_DQN_MLP_STREAM) return err(RT_E_INVALID, "bad MLP kernel mode");
+    if (mode != RT_DQN_MLP_AUTO && mode != RT_DQN_MLP_STREAM && mode != RT_DQN_MLP_STATIONARY)
+        return err(RT_E_INVALID, "bad MLP kernel mode");
     dqn->net.mlp_mode = mode;
     return RT_OK;
 }

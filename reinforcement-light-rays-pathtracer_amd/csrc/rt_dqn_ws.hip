@@ -56,6 +56,11 @@ __device__ __forceinline__ void mfma_w(f32x4& acc, const bf16x8& w, const bf16x8
     asm("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(acc) : "a"(w), "v"(x));
 }
 
+// Workgroup barrier for LDS traffic only: __syncthreads() also waits for every outstanding
+// global access (vmcnt(0)), which would put the Q stores and the next tile's position
+// loads on every barrier; a lone workgroup per CU has no other waves to cover that.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // element offset of (row, k) in a swizzled activation buffer
 __device__ __forceinline__ int swz(int row, int k, int stride) {
     return row * stride + ((((k >> 3) ^ ((row >> 2) & 7))) << 3) + (k & 7);
@@ -146,8 +151,8 @@ __device__ __forceinline__ void ws_layer(const bf16x8 (&w)[NT][KS], int wave, in
 }
 
 // layer 0 (folded, exact fp32 MFMA; see rt_dqn.hip mlp_layer0) into bufB
-__device__ __forceinline__ void ws_layer0(const DqnNet& net, const float* __restrict__ locs, __bf16* out, int wave,
-                                          int lane) {
+__device__ __forceinline__ void ws_layer0(const DqnNet& net, const float4* __restrict__ l0, const float* __restrict__ locs,
+                                          __bf16* out, int wave, int lane) {
     const int r16 = lane & 15, kq = lane >> 4;
     float b[kMT];
 #pragma unroll
@@ -157,7 +162,7 @@ __device__ __forceinline__ void ws_layer0(const DqnNet& net, const float* __rest
     for (int j = 0; j < 4; ++j) {  // 224 features = 14 tiles over 4 waves
         const int nt = wave + 4 * j;
         if (nt >= n_tiles) continue;  // wave-uniform
-        const float a = reinterpret_cast<const float*>(net.l0 + nt * 16 + r16)[kq];
+        const float a = reinterpret_cast<const float*>(l0 + nt * 16 + r16)[kq];
 #pragma unroll
         for (int m = 0; m < kMT; ++m) {
             const f32x4 d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b[m], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
@@ -169,40 +174,58 @@ __device__ __forceinline__ void ws_layer0(const DqnNet& net, const float* __rest
     }
 }
 
+// the rows' ray ids: list order, or the rows themselves
+__device__ __forceinline__ int row_id(const int32_t* __restrict__ list, int row, int n_rows) {
+    if (row >= n_rows) return -1;
+    return (list != nullptr) ? list[row] : row;
+}
+
 template <int NT1, int NT2, int NT3>
 __device__ void ws_wave(const DqnNet& net, const float* __restrict__ loc, const int32_t* __restrict__ list,
                         int n_rows, float* __restrict__ q, int ldq, __bf16* bufA, __bf16* bufB, float* locs,
-                        int wave, int lane) {
+                        const float4* l0s, const float* bias1, const float* bias2, const float* bias3, int wave,
+                        int lane) {
     bf16x8 w1[NT1][kKs1], w2[NT2][kKs2], w3[NT3][kKs3];
     load_weights<1, NT1, kKs1>(net.W[1], kK1, wave, lane, w1);
     load_weights<2, NT2, kKs2>(net.W[2], kK2, wave, lane, w2);
     load_weights<3, NT3, kKs3>(net.W[3], kK3, wave, lane, w3);
     const int n_tiles = (n_rows + kRows - 1) / kRows;
-    for (int t = blockIdx.x; t < n_tiles; t += gridDim.x) {  // block-uniform trip count
+    // ray positions one tile ahead (threads < kRows): the id load is issued at the top of
+    // a tile, the position loads after its layer 1, the LDS store at the next tile's top
+    const bool loader = threadIdx.x < kRows;
+    int t = blockIdx.x;
+    int nid = loader ? row_id(list, t * kRows + (int)threadIdx.x, n_rows) : -1;
+    float px = 0.0f, py = 0.0f, pz = 0.0f;
+    if (nid >= 0) {
+        px = loc[(size_t)nid * 3 + 0];
+        py = loc[(size_t)nid * 3 + 1];
+        pz = loc[(size_t)nid * 3 + 2];
+    }
+    for (; t < n_tiles; t += gridDim.x) {  // block-uniform trip count
         const int row0 = t * kRows;
         const int rows_valid = min(kRows, n_rows - row0);
-        if (threadIdx.x < kRows) {
+        if (loader) {
             const int row = threadIdx.x;
-            float x = 0.0f, y = 0.0f, z = 0.0f;
-            if (row < rows_valid) {
-                const int rid = (list != nullptr) ? list[row0 + row] : (row0 + row);
-                x = loc[(size_t)rid * 3 + 0];
-                y = loc[(size_t)rid * 3 + 1];
-                z = loc[(size_t)rid * 3 + 2];
-            }
-            locs[row * 3 + 0] = x;
-            locs[row * 3 + 1] = y;
-            locs[row * 3 + 2] = z;
+            locs[row * 3 + 0] = px;
+            locs[row * 3 + 1] = py;
+            locs[row * 3 + 2] = pz;
+            nid = row_id(list, (t + (int)gridDim.x) * kRows + row, n_rows);
         }
-        __syncthreads();
-        ws_layer0(net, locs, bufB, wave, lane);
-        __syncthreads();
-        ws_layer<1, NT1, kKs1, false, false>(w1, wave, lane, net.b[1], bufB, kStrB, bufA, kStrA);
-        __syncthreads();
-        ws_layer<2, NT2, kKs2, false, true>(w2, wave, lane, net.b[2], bufA, kStrA, bufB, kStrB);
-        __syncthreads();
-        ws_layer<3, NT3, kKs3, true, true>(w3, wave, lane, net.b[3], bufB, kStrB, bufA, 0);
-        __syncthreads();
+        lds_barrier();
+        ws_layer0(net, l0s, locs, bufB, wave, lane);
+        lds_barrier();
+        ws_layer<1, NT1, kKs1, false, false>(w1, wave, lane, bias1, bufB, kStrB, bufA, kStrA);
+        px = py = pz = 0.0f;
+        if (nid >= 0) {
+            px = loc[(size_t)nid * 3 + 0];
+            py = loc[(size_t)nid * 3 + 1];
+            pz = loc[(size_t)nid * 3 + 2];
+        }
+        lds_barrier();
+        ws_layer<2, NT2, kKs2, false, true>(w2, wave, lane, bias2, bufA, kStrA, bufB, kStrB);
+        lds_barrier();
+        ws_layer<3, NT3, kKs3, true, true>(w3, wave, lane, bias3, bufB, kStrB, bufA, 0);
+        lds_barrier();
         // the Q tile from LDS in 16-B stores (as k_dqn_mlp): rows, or action-major columns
         const float* stage = reinterpret_cast<const float*>(bufA);
         if (ldq == 0) {
@@ -220,7 +243,8 @@ __device__ void ws_wave(const DqnNet& net, const float* __restrict__ loc, const 
                     make_float4(sp[0], sp[kQStage], sp[2 * kQStage], sp[3 * kQStage]);
             }
         }
-        // the next tile's first writes (locs, bufB) do not touch what these stores read
+        // the next tile's first LDS writes (locs, then bufB after a barrier) do not touch
+        // the Q stage these stores read; bufA is next written after two barriers
     }
 }
 
@@ -231,14 +255,32 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_dqn_mlp_ws(const DqnNet net, 
     __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrA];
     __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrB];
     __shared__ float locs[kRows * 3];
+    // the layers' biases and the folded layer 0, read every tile: LDS copies
+    __shared__ __attribute__((aligned(16))) float4 l0s[kK1];
+    __shared__ __attribute__((aligned(16))) float bias1[kNt1 * 16];
+    __shared__ __attribute__((aligned(16))) float bias2[kNt2 * 16];
+    __shared__ __attribute__((aligned(16))) float bias3[kNt3 * 16];
     const int n_rows = (count != nullptr) ? min(*count, max_rows) : max_rows;
     if ((int)blockIdx.x * kRows >= n_rows) return;  // no tile for this workgroup: skip the weight loads
+    for (int i = threadIdx.x; i < kK1; i += kWsThreads) l0s[i] = net.l0[i];
+    for (int i = threadIdx.x; i < kNt1 * 16; i += kWsThreads) bias1[i] = net.b[1][i];
+    for (int i = threadIdx.x; i < kNt2 * 16; i += kWsThreads) bias2[i] = net.b[2][i];
+    for (int i = threadIdx.x; i < kNt3 * 16; i += kWsThreads) bias3[i] = net.b[3][i];
+    // (visible after the first tile's barrier)
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     switch (wave) {  // the per-wave tile counts are compile-time (register arrays)
-        case 0: ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, wave, lane); break;
-        case 1: ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, wave, lane); break;
-        case 2: ws_wave<5, 3, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, wave, lane); break;
-        default: ws_wave<5, 3, 3>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, wave, lane); break;
+        case 0:
+            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            break;
+        case 1:
+            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            break;
+        case 2:
+            ws_wave<5, 3, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            break;
+        default:
+            ws_wave<5, 3, 3>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            break;
     }
 }
 

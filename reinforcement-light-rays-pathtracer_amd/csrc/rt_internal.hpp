@@ -101,7 +101,7 @@ inline int filter_usable(const DeviceScene& s, float cx, float cy, float cz, flo
 constexpr int kDqnActions = 144;  // GRID_RESOLUTION^2 (GPU/constants/radiance_volumes_settings.h:9)
 constexpr int kDqnGrid = 12;
 
-constexpr int kMlpStream = 1;  // RT_DQN_MLP_STREAM
+constexpr int kMlpStationary = 2;  // RT_DQN_MLP_STATIONARY
 struct DqnNet {
     // layer 0 folded: [N[0]] x {-S0, -S1, -S2, c0}; h1 = ReLU(c0 - fma(S2, z, fma(S1, y, S0 x)))
     const float4* l0 = nullptr;
@@ -111,7 +111,7 @@ struct DqnNet {
     const float* b[4] = {nullptr, nullptr, nullptr, nullptr};      // fp32, padded (b[0] unused)
     int K[4] = {0, 0, 0, 0};      // padded input width of each layer (K[0] = n_in, unpadded)
     int N[4] = {0, 0, 0, 0};      // padded output width of each layer (multiple of 32; last = 144)
-    int mlp_mode = 0;             // RT_DQN_MLP_* (rtmi.h rt_dqn_set_mlp): kMlpStream = weight streaming
+    int mlp_mode = 0;             // RT_DQN_MLP_* (rtmi.h rt_dqn_set_mlp)
 };
 
 // Ray state of the DQN wavefront renderer (SoA over the rays of a frame part).
@@ -151,6 +151,37 @@ struct DqnLaunch {
     float* out;
     int use_filter;  // as RenderLaunch::use_filter
 };
+
+// Neural-Q training renderer (GPU/deep_learning/neural_q_pathtracer.cu:226-600): one ray
+// per pixel (id = y * width + x) through all bounces of a sample, in the reference's
+// per-ray arrays (SoA, device).
+struct NqRays {
+    int n = 0;                     // rays = pixels
+    float* loc = nullptr;          // [n][3] position (S_{t+1} after a trace)
+    float* prev = nullptr;         // [n][3] position before the trace (S_t of the learning rule)
+    float* dir = nullptr;          // [n][3] direction to trace next
+    float* tp = nullptr;           // [n][3] throughput
+    float* total = nullptr;        // [n][3] throughput summed over the frame's samples
+    int32_t* tri = nullptr;        // [n] surface of the position (its frame: shade N, T, B)
+    uint32_t* state = nullptr;     // [n] 0 active, 1 terminal, 2 restarted (learning only)
+    float* reward = nullptr;       // [n]
+    float* discount = nullptr;     // [n]
+    uint32_t* bounces = nullptr;   // [n] bounce of termination (MAX_RAY_BOUNCES if none)
+    int32_t* action = nullptr;     // [n] sampled cell (the learning rule's a_t)
+    int32_t* terminal = nullptr;   // [n] state == 1 (compute_td_targets' test)
+    uint32_t* pix = nullptr;       // [n] pixel ids (RNG keys; = ray ids)
+    int32_t* flag = nullptr;       // [1] 1 = every path has terminated (rays_finished)
+    const float* surf_v = nullptr;  // [n_surf][9] surface vertices (restarts)
+    const float* tri_lum = nullptr; // [n_tri] Material / AreaLight luminance 0.5 (max + min)
+    unsigned long long* stats = nullptr;  // [3] sum of bounces, zero-contribution paths, ray casts
+};
+hipError_t launch_nq_init(const DqnLaunch& a, const NqRays& r, int sample, hipStream_t stream);
+hipError_t launch_nq_sample(const DqnLaunch& a, const NqRays& r, float* q, float eps, int sample, int bounce,
+                            hipStream_t stream);
+hipError_t launch_nq_trace(const DqnLaunch& a, const NqRays& r, int bounce, hipStream_t stream);
+hipError_t launch_nq_restart(const DqnLaunch& a, const NqRays& r, int sample, int bounce, hipStream_t stream);
+hipError_t launch_nq_end_sample(const DqnLaunch& a, const NqRays& r, hipStream_t stream);
+hipError_t launch_nq_image(const DqnLaunch& a, const NqRays& r, float* out, int spp, hipStream_t stream);
 
 // q layout: ldq == 0 -> [row][144] (the C ABI's); ldq > 0 -> action-major q[a * ldq + row],
 // ldq a multiple of 64 covering every launched row (the renderer's, coalesced per action)

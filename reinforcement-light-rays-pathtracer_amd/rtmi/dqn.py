@@ -105,10 +105,10 @@ class Dqn:
     def handle(self):
         return self._h
 
-    MLP_AUTO, MLP_STREAM = 0, 1  # RT_DQN_MLP_*
+    MLP_AUTO, MLP_STREAM, MLP_STATIONARY = 0, 1, 2  # RT_DQN_MLP_*
 
     def set_mlp(self, mode: int) -> None:
-        """forward kernel: MLP_AUTO (weight-stationary for the 200-300-200 shape) or MLP_STREAM"""
+        """forward kernel: MLP_AUTO / MLP_STREAM (weight streaming) or MLP_STATIONARY"""
         check(lib().rt_dqn_set_mlp(self._h, mode))
 
     def forward(self, loc: np.ndarray) -> np.ndarray:
@@ -236,6 +236,57 @@ class DqnTrainer:
         bp = (ctypes.POINTER(ctypes.c_float) * 4)(*[_fp(x) for x in b])
         check(lib().rt_dqn_trainer_params(self._h, Wp, bp))
         return W, b
+
+
+class NeuralQ:
+    """NeuralQPathtracer (GPU/deep_learning/neural_q_pathtracer.cu:226-600) on the device:
+    epsilon-greedy sampling from the network being trained, trace_ray with rewards (light
+    luminance x 200), restarts of terminated rays, the learning rule per batch of rays, one
+    stats row per sample (rt_neuralq_render_frame).  The reference's run: archway, batch
+    4096, epsilon 0.05 (start = min, decay 0.01), 15 frames of SAMPLES_PER_PIXEL samples."""
+
+    def __init__(self, ctx: Context, scene: Scene, trainer: "DqnTrainer", batch_size: int = 4096,
+                 epsilon_start: float = 0.05, epsilon_min: float = 0.05, epsilon_decay: float = 0.01):
+        self.ctx, self.scene, self.trainer = ctx, scene, trainer
+        self._h = ctypes.c_void_p()
+        check(lib().rt_neuralq_create(ctx.handle, scene.handle, trainer._h, int(batch_size), float(epsilon_start),
+                                      float(epsilon_min), float(epsilon_decay), ctypes.byref(self._h)))
+
+    @property
+    def epsilon(self) -> float:
+        e = ctypes.c_float(0.0)
+        check(lib().rt_neuralq_epsilon(self._h, ctypes.byref(e)))
+        return float(e.value)
+
+    def render_frame(self, cam, params):
+        """(image H x W x 3, stats spp x 3 [average path length, loss, zero-contribution
+        paths] per sample, ray casts)."""
+        img = np.zeros((params.height, params.width, 3), np.float32)
+        stats = np.zeros((params.spp, 3), np.float32)
+        casts = ctypes.c_uint64(0)
+        check(lib().rt_neuralq_render_frame(self.ctx.handle, self._h, ctypes.byref(cam), ctypes.byref(params),
+                                            _fp(img), _fp(stats), ctypes.byref(casts)))
+        return img, stats, int(casts.value)
+
+    @staticmethod
+    def stats_lines(stats) -> str:
+        """nn_training_stats.txt lines (neural_q_pathtracer.cu:577-583): `avg_path_length
+        << " " << loss << " " << total_zclp` with ostream defaults (6 significant digits)."""
+        out = []
+        for avg, loss, z in np.asarray(stats, np.float32):
+            out.append(f"{float(avg):g} {float(loss):g} {int(z)}\n")
+        return "".join(out)
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_neuralq_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def td_targets_device(ctx: Context, seed: int, next_q_ptr: int, terminal_ptr: int, reward_ptr: int,

@@ -466,9 +466,9 @@ def test_dynet_write_read_round_trip(rtmi_mod, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["door_room", "archway"])
 def test_gpu_weight_stationary_forward_equals_streaming(rtmi_mod, gpu_ctx, kind):
-    """The weight-stationary forward (rt_dqn_ws.hip, the default for the 200-300-200 shape)
-    and the weight-streaming one (RT_DQN_MLP_STREAM) give the same Q bit for bit: same
-    fragments, same K order of the fp32 accumulation; ragged ray counts included."""
+    """The weight-stationary forward (rt_dqn_ws.hip, RT_DQN_MLP_STATIONARY) and the
+    weight-streaming one (the default) give the same Q bit for bit: same fragments, same K
+    order of the fp32 accumulation; ragged ray counts included."""
     g = rtmi_mod.obj_geometry(os.path.join(MODELS, kind + ".obj"), kind)
     W, b = trained(rtmi_mod) if kind == "door_room" else rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
     lo, hi = g.all_triangles().reshape(-1, 3).min(0), g.all_triangles().reshape(-1, 3).max(0)
@@ -476,7 +476,7 @@ def test_gpu_weight_stationary_forward_equals_streaming(rtmi_mod, gpu_ctx, kind)
     with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
         for n in (1, 31, 33, 1000, 70_001):
             loc = (lo + (hi - lo) * rng.random((n, 3))).astype(np.float32)
-            net.set_mlp(net.MLP_AUTO)
+            net.set_mlp(net.MLP_STATIONARY)
             qa = net.forward(loc)
             net.set_mlp(net.MLP_STREAM)
             qs = net.forward(loc)

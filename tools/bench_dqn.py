@@ -32,8 +32,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--max-bounces", type=int, default=80)
     ap.add_argument("--no-render", action="store_true", help="forward pass only (profiling)")
-    ap.add_argument("--mlp", default="auto", choices=["auto", "stream"],
-                    help="forward kernel: weight-stationary (auto) or weight-streaming")
+    ap.add_argument("--mlp", default="stream", choices=["stream", "stationary"],
+                    help="forward kernel: weight-streaming (default) or weight-stationary")
     args = ap.parse_args()
     g = rtmi.obj_geometry(os.path.join(ROOT, "assets", "models", args.scene + ".obj"), args.scene)
     if args.scene == "door_room":
@@ -46,7 +46,7 @@ def main():
     ctx = rtmi.Context(0)
     sc = rtmi.Scene(ctx, g)
     net = rtmi.dqn.Dqn(ctx, g.nn_vertices, W, b)
-    net.set_mlp(net.MLP_AUTO if args.mlp == "auto" else net.MLP_STREAM)
+    net.set_mlp(net.MLP_STATIONARY if args.mlp == "stationary" else net.MLP_STREAM)
     stream = torch.cuda.current_stream()
     res = {"scene": args.scene, "weights": weights, "n_in": int(g.nn_vertices.size), "mlp_kernel": args.mlp}
 

@@ -6,8 +6,9 @@
 One step = forward with activations kept, loss, backward, clipping and Adam over all
 parameters, on `batch` rays (the reference trains in batches of ray_batch_size).  Prints
 one JSON line per batch: ms per step (HIP events on the launch stream), rays/s, and the
-fp32 GEMM rate in algorithmic flops (forward 2*sum(in*out) per ray, backward dW the same,
-dX the same minus layer 0) against the 157.3 TF/s fp32 vector peak.
+step's rate in the reference's algorithmic flops (forward 2*sum(in*out) per ray, backward
+dW the same, dX the same minus layer 0) against the 157.3 TF/s fp32 peak; and the flops
+the MFMA GEMMs execute (layer 0 is folded: layers 1-3 forward, dW, dX).
 """
 import argparse
 import json
@@ -34,7 +35,11 @@ def main():
     W, b = rtmi.dqn.synthetic_weights(g.nn_vertices.size)
     dims = [W[0].shape[1]] + [w.shape[0] for w in W]
     mac = sum(dims[i] * dims[i + 1] for i in range(4))
+    # the reference's step (DyNet: explicit n_in-wide layer 0): forward, dW, dX (no dX of layer 0)
     flops_per_ray = 2 * mac * 3 - 2 * dims[0] * dims[1]
+    # what the GEMMs of this step execute: layer 0 is folded (no n_in-wide GEMM at all)
+    mac_gemm = sum(dims[i] * dims[i + 1] for i in range(1, 4))
+    gemm_flops_per_ray = 2 * mac_gemm * 3
     ctx = rtmi.Context(0)
     stream = torch.cuda.current_stream()
     rng = np.random.default_rng(0)
@@ -57,6 +62,8 @@ def main():
         print(json.dumps({"scene": args.scene, "dims": dims, "batch": n, "ms_per_step": round(ms, 4),
                           "rays_per_s": round(n / (ms * 1e-3), 1), "flops_per_ray": flops_per_ray,
                           "tflops": round(tf, 2), "frac_fp32_peak": round(tf / FP32_PEAK_TFLOPS, 4),
+                          "gemm_flops_per_ray": gemm_flops_per_ray,
+                          "gemm_tflops_executed": round(gemm_flops_per_ray * n / (ms * 1e-3) / 1e12, 2),
                           "loss_first": first[0], "loss_last": last[0]}), flush=True)
 
 
