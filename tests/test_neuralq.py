@@ -113,3 +113,33 @@ def test_door_room_obj_scene_runs(rtmi_mod, gpu_ctx):
         img, stats, casts = nq.render_frame(cam, p)
     assert np.isfinite(img).all() and img.mean() > 0
     assert np.isfinite(stats).all() and casts > 0
+
+
+def test_trained_network_beats_the_untrained_one(rtmi_mod, gpu_ctx):
+    """Two frames of Neural-Q training on the door room (from synthetic He-normal weights),
+    then the pretrained-network renderer (config 4's sampler) at equal spp: the trained
+    network's frame is closer to a 1024-spp uniform render than the untrained one's (MAPE),
+    and its paths are shorter.  Measured at 720^2 (tools/neuralq_train.py,
+    profiles/r2_neuralq_door_room_720.json): MAPE 0.63 vs 0.90, block-mean error vs the
+    reference's own 128-spp render 4.2 vs 45.4 of 255, 33.6 vs 50.6 casts per sample."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    S = 128
+    W0, b0 = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        with rtmi_mod.dqn.DqnTrainer(gpu_ctx, g.nn_vertices, W0, b0) as tr:
+            with rtmi_mod.dqn.NeuralQ(gpu_ctx, sc, tr, batch_size=4096) as nq:
+                p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=S, height=S, spp=2)
+                for _ in range(2):
+                    nq.render_frame(cam, p)
+            W1, b1 = tr.params()
+        pe = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=S, height=S, spp=16)
+        ref, _ = rtmi_mod.render(gpu_ctx, sc, cam, rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=S, height=S,
+                                                                         spp=1024, spp_split=16))
+        out = {}
+        for name, (W, b) in (("synthetic", (W0, b0)), ("trained", (W1, b1))):
+            with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+                out[name] = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, pe)
+    m = {k: float(np.mean(np.abs(v[0] - ref) / np.maximum(ref, 1e-3))) for k, v in out.items()}
+    assert m["trained"] < 0.85 * m["synthetic"], m
+    assert out["trained"][1] < out["synthetic"][1]
