@@ -6,6 +6,8 @@
 //
 //   ./build/reinforcement_demo sarsa <scene.obj> <kind> [frames] [spp] [out.bmp]
 //   ./build/reinforcement_demo dqn <scene.obj> <kind> <model> [frames] [spp] [out.bmp]
+//   ./build/reinforcement_demo neuralq <scene.obj> <kind> <model> [frames] [spp] [out.bmp]
+//     (trains from <model>; writes nn_training_stats.txt and trained.model)
 //   (kind: 1 door_room, 2 archway, 3 complex_light_room; scene "cornell" = the Cornell box)
 #include <stdio.h>
 #include <stdlib.h>
@@ -34,7 +36,8 @@ int main(int argc, char** argv) {
         fprintf(stderr, "usage: %s sarsa|dqn <scene.obj|cornell> <kind> [model] [frames] [spp] [out.bmp]\n", argv[0]);
         return 2;
     }
-    const bool dqn = strcmp(argv[1], "dqn") == 0;
+    const bool nq = strcmp(argv[1], "neuralq") == 0;
+    const bool dqn = nq || strcmp(argv[1], "dqn") == 0;
     const int kind = atoi(argv[3]);
     int a = 4;
     const char* model = dqn ? (argc > a ? argv[a++] : "") : "";
@@ -51,7 +54,14 @@ int main(int argc, char** argv) {
     Camera camera(camera_for(kind));
     try {
         DeviceScene ds(scene);
-        if (dqn) {
+        if (nq) {
+            NeuralQPathtracer pt(ds, model);
+            for (int f = 0; f < frames; ++f) {
+                const uint64_t casts = pt.render_frame(screen, camera, spp);
+                printf("frame %d: %llu ray casts, epsilon %.3f\n", f, (unsigned long long)casts, pt.epsilon());
+            }
+            pt.save_model("trained.model");
+        } else if (dqn) {
             PretrainedPathtracer pt(ds, model);
             for (int f = 0; f < frames; ++f) {
                 const uint64_t casts = pt.render_frame(screen, camera, spp);

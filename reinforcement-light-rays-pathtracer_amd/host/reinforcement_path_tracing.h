@@ -6,6 +6,8 @@
 //     reinforcement_path_tracing.cuh:1-30, host loop GPU/main.cu:260-350)
 //   PretrainedPathtracer::render_frame
 //     DQN Q-value sampling (GPU/deep_learning/pre_trained_pathtracer.cuh, main.cu:420-470)
+//   NeuralQPathtracer::render_frame
+//     rendering while training the network (GPU/deep_learning/neural_q_pathtracer.cuh)
 //
 // The reference's draw kernel learns while it renders and the distribution update
 // runs after it; here draw_reinforcement_path_tracing renders one frame and folds
@@ -147,19 +149,24 @@ inline void update_radiance_volume_distributions(RadianceMap&) {}
 
 // GPU/deep_learning/pre_trained_pathtracer.cuh: a trained DyNet Q-network loaded from the
 // reference's text model (Radiance_Map_Data/<scene>_12_12.model) and its frame renderer.
-class PretrainedPathtracer {
-   public:
-    PretrainedPathtracer(DeviceScene& ds, const std::string& model_path) : ds_(ds) {
+// a DQNetwork's parameters as dynet::TextFileLoader reads them (rt_dynet_read)
+struct DqnModel {
+    std::vector<int32_t> rows, cols;
+    std::vector<float> values;
+    const float* W[4];
+    const float* b[4];
+    int32_t hidden[3];
+    int n_in = 0, n_out = 0;
+    explicit DqnModel(const std::string& path) {
         int n_params = 0;
         int64_t n_values = 0;
-        detail::check(rt_dynet_read(model_path.c_str(), 0, nullptr, nullptr, nullptr, &n_params, &n_values));
+        detail::check(rt_dynet_read(path.c_str(), 0, nullptr, nullptr, nullptr, &n_params, &n_values));
         if (n_params != 8) throw std::runtime_error("expected 4 fully connected layers (8 parameters)");
-        std::vector<int32_t> rows(n_params), cols(n_params);
-        std::vector<float> values((size_t)n_values);
-        detail::check(rt_dynet_read(model_path.c_str(), n_params, rows.data(), cols.data(), values.data(), &n_params,
+        rows.resize(n_params);
+        cols.resize(n_params);
+        values.resize((size_t)n_values);
+        detail::check(rt_dynet_read(path.c_str(), n_params, rows.data(), cols.data(), values.data(), &n_params,
                                     &n_values));
-        const float* W[4];
-        const float* b[4];
         size_t off = 0;
         for (int l = 0; l < 4; ++l) {
             W[l] = values.data() + off;
@@ -167,9 +174,18 @@ class PretrainedPathtracer {
             b[l] = values.data() + off;
             off += (size_t)rows[2 * l + 1] * std::max(cols[2 * l + 1], 1);
         }
-        const int32_t hidden[3] = {rows[0], rows[2], rows[4]};
+        for (int l = 0; l < 3; ++l) hidden[l] = rows[2 * l];
+        n_in = cols[0];
+        n_out = rows[6];
+    }
+};
+
+class PretrainedPathtracer {
+   public:
+    PretrainedPathtracer(DeviceScene& ds, const std::string& model_path) : ds_(ds) {
+        const DqnModel m(model_path);
         const std::vector<float>& v = ds.vertices();
-        detail::check(rt_dqn_create(ds.ctx(), v.data(), (int)v.size(), hidden, rows[6], W, b, &net_));
+        detail::check(rt_dqn_create(ds.ctx(), v.data(), (int)v.size(), m.hidden, m.n_out, m.W, m.b, &net_));
     }
     ~PretrainedPathtracer() {
         if (net_) rt_dqn_destroy(net_);
@@ -192,6 +208,90 @@ class PretrainedPathtracer {
    private:
     DeviceScene& ds_;
     rt_dqn* net_ = nullptr;
+};
+
+// GPU/deep_learning/neural_q_pathtracer.cuh: renders while training the Q-network
+// (NeuralQPathtracer, main.cu:114-124: batch 4096), starting from a saved model (the
+// reference's LOAD_MODEL path, neural_q_pathtracer.cu:54-59); each sample's statistics
+// go to nn_training_stats.txt (:577-583) and save_model writes the trained network in
+// the reference's format (dynet::TextFileSaver, :193).
+class NeuralQPathtracer {
+   public:
+    NeuralQPathtracer(DeviceScene& ds, const std::string& model_path, unsigned batch_size = 4096,
+                      const std::string& stats_path = "nn_training_stats.txt")
+        : ds_(ds), stats_path_(stats_path) {
+        const DqnModel m(model_path);
+        const std::vector<float>& v = ds.vertices();
+        shapes_.assign(m.rows.begin(), m.rows.end());
+        n_in_ = m.n_in;
+        detail::check(rt_dqn_trainer_create(ds.ctx(), v.data(), (int)v.size(), m.hidden, m.n_out, m.W, m.b, 1e-3f,
+                                            &trainer_));
+        // EPSILON_START / EPSILON_MIN / EPSILON_DECAY (constants/deep_learning_settings.h:5-7)
+        detail::check(rt_neuralq_create(ds.ctx(), ds.scene(), trainer_, (int)batch_size, 0.05f, 0.05f, 0.01f, &nq_));
+    }
+    ~NeuralQPathtracer() {
+        if (nq_) rt_neuralq_destroy(nq_);
+        if (trainer_) rt_dqn_trainer_destroy(trainer_);
+    }
+    NeuralQPathtracer(const NeuralQPathtracer&) = delete;
+    NeuralQPathtracer& operator=(const NeuralQPathtracer&) = delete;
+
+    // render_frame (neural_q_pathtracer.cu:226-600): returns the frame's ray casts
+    uint64_t render_frame(SDLScreen& screen, const Camera& camera, int spp = 32) {
+        const rt_params p = gpu_engine_params(screen, spp);
+        const rt_camera cam = camera.to_rt();
+        std::vector<float> rgb((size_t)screen.width * screen.height * 3), stats((size_t)spp * 3);
+        uint64_t casts = 0;
+        detail::check(rt_neuralq_render_frame(ds_.ctx(), nq_, &cam, &p, rgb.data(), stats.data(), &casts));
+        screen.PutFrame(rgb.data());
+        std::ofstream f(stats_path_, std::ios::app);
+        for (int s = 0; s < spp; ++s)
+            f << stats[3 * s] << " " << stats[3 * s + 1] << " " << (long long)stats[3 * s + 2] << "\n";
+        if (!f) throw std::runtime_error("cannot append to " + stats_path_);
+        return casts;
+    }
+
+    float epsilon() const {
+        float e = 0.f;
+        detail::check(rt_neuralq_epsilon(nq_, &e));
+        return e;
+    }
+
+    // the trained network in the reference's DyNet text format
+    void save_model(const std::string& path) const {
+        std::vector<std::vector<float>> W(4), b(4);
+        float* Wp[4];
+        float* bp[4];
+        int32_t rows[8], cols[8];
+        int in = n_in_;
+        for (int l = 0; l < 4; ++l) {
+            const int out = shapes_[2 * l];
+            W[l].resize((size_t)out * in);
+            b[l].resize((size_t)out);
+            Wp[l] = W[l].data();
+            bp[l] = b[l].data();
+            rows[2 * l] = out;
+            cols[2 * l] = in;
+            rows[2 * l + 1] = out;
+            cols[2 * l + 1] = 0;  // a vector
+            in = out;
+        }
+        detail::check(rt_dqn_trainer_params(trainer_, Wp, bp));
+        std::vector<float> flat;
+        for (int l = 0; l < 4; ++l) {
+            flat.insert(flat.end(), W[l].begin(), W[l].end());
+            flat.insert(flat.end(), b[l].begin(), b[l].end());
+        }
+        detail::check(rt_dynet_write(path.c_str(), 8, rows, cols, flat.data()));
+    }
+
+   private:
+    DeviceScene& ds_;
+    std::string stats_path_;
+    std::vector<int32_t> shapes_;
+    int n_in_ = 0;
+    rt_dqn_trainer* trainer_ = nullptr;
+    rt_neuralq* nq_ = nullptr;
 };
 
 }  // namespace rtmi

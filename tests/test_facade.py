@@ -76,3 +76,30 @@ def test_reinforcement_demo_dqn_equals_c_abi(rtmi_mod, gpu_ctx, tmp_path):
     with rtmi_mod.Scene(gpu_ctx, geom) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, geom.nn_vertices, W, b) as net:
         img, _ = rtmi_mod.dqn.render(gpu_ctx, sc, net, rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p)
     assert np.array_equal(got, rtmi_mod.pack_argb(img))
+
+
+def test_reinforcement_demo_neuralq_equals_c_abi(rtmi_mod, gpu_ctx, tmp_path):
+    """NeuralQPathtracer from the reference's door_room model: the frames, the
+    nn_training_stats.txt lines and the saved trained model equal the C ABI's run."""
+    out = str(tmp_path / "nq.bmp")
+    obj = os.path.join(MODELS, "door_room.obj")
+    model = os.path.join(MODELS, "door_room_12_12.model")
+    log = run(["reinforcement_demo", "neuralq", obj, "1", model, "2", "1", out], tmp_path)
+    assert log.count("ray casts") == 2
+    got = read_bmp(out, 512, 512)
+    geom = rtmi_mod.obj_geometry(obj, "door_room")
+    W, b = rtmi_mod.dqn.split_layers(rtmi_mod.dqn.read_dynet(model))
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=512, height=512, spp=1)
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc, rtmi_mod.dqn.DqnTrainer(gpu_ctx, geom.nn_vertices, W, b) as tr, \
+            rtmi_mod.dqn.NeuralQ(gpu_ctx, sc, tr) as nq:
+        stats = []
+        for _ in range(2):
+            img, st, _ = nq.render_frame(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p)
+            stats.append(st)
+        W2, b2 = tr.params()
+    assert np.array_equal(got, rtmi_mod.pack_argb(img))
+    want = rtmi_mod.dqn.NeuralQ.stats_lines(np.concatenate(stats))
+    assert open(tmp_path / "nn_training_stats.txt").read() == want
+    saved = rtmi_mod.dqn.read_dynet(str(tmp_path / "trained.model"))
+    for x, y in zip(saved, rtmi_mod.dqn.join_layers(W2, b2)):
+        assert x.shape == y.shape and np.array_equal(x, y)
