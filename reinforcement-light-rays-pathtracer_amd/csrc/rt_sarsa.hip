@@ -444,9 +444,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     if (valid && chunk == 0) {
         const float fs = (float)a.spp;
         float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
-        dst[0] = tot.x / fs;
-        dst[1] = tot.y / fs;
-        dst[2] = tot.z / fs;
+        store_rgb(dst, tot.x / fs, tot.y / fs, tot.z / fs);
     }
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);

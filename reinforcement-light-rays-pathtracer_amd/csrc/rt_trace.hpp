@@ -11,6 +11,17 @@
 
 namespace rt {
 
+// One pixel's RGB as a single 12-B store (global_store_dwordx3): three dword stores of a
+// lone lane are three partial-line writes in the memory system's count
+typedef float rgb3 __attribute__((ext_vector_type(3), aligned(4)));
+__device__ __forceinline__ void store_rgb(float* dst, float r, float g, float b) {
+    rgb3 v;
+    v.x = r;
+    v.y = g;
+    v.z = b;
+    *reinterpret_cast<rgb3*>(dst) = v;
+}
+
 constexpr float kRho = 1.0f / (2.0f * kPi);  // RHO: GPU/constants/image_settings.h:14
 
 // Triangle records are read-only for a launch: loads through the constant address
