@@ -348,25 +348,11 @@ __global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
     }
 }
 
-#ifndef RT_PS_MIN_WAVES
-#define RT_PS_MIN_WAVES 7  // 72 VGPRs: 7 waves per SIMD (4.84 vs 4.91 ms at 75 VGPRs, profiles/r2c_ab.log)
-#endif
+// the work of k_render_ps for one wave with at least one pixel; returns the lane's casts
 template <int SAMPLER, int RULE>
-__global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
+__device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDesc& blk, int q, int chunk, int lane,
+                                            int lx, int ly, int px, int py, bool valid) {
     extern __shared__ float s_ps[];
-    const int lg = a.split_log2;
-    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
-    const int part = blockIdx.x & (a.split - 1);
-    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
-    const int chunk = threadIdx.x & (a.split - 1);
-    const int lane = threadIdx.x & 63;
-    const int lx = q & 15;
-    const int ly = q >> 4;
-    const int px = blk.px0 + lx;
-    const int py = blk.py0 + ly;
-    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
-    const uint64_t vmask = __ballot(valid);
-    if (vmask == 0ull) return;  // no barrier in this kernel: a wave may leave early
     const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
     const float4* __restrict__ shade = a.scene.shade;
     const int n_surf = a.scene.n_surf;
@@ -553,9 +539,41 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
         float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
         store_rgb(dst, tot.x / fs, tot.y / fs, tot.z / fs);
     }
+    return n_casts;
+}
+
+#ifndef RT_PS_MIN_WAVES
+#define RT_PS_MIN_WAVES 7  // 72 VGPRs: 7 waves per SIMD (4.84 vs 4.91 ms at 75 VGPRs, profiles/r2c_ab.log)
+#endif
+template <int SAMPLER, int RULE>
+__global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
+    const int lg = a.split_log2;
+    const BlockDesc blk = a.blocks[blockIdx.x >> lg];
+    // XCD-aware parts: workgroups go to the 8 XCDs round-robin by blockIdx, so the
+    // workgroups of one XCD take consecutive parts (whole pixel rows of the block) and a
+    // row's output lines are written through one XCD's L2 instead of eight
+    int part = blockIdx.x & (a.split - 1);
+    if (a.split >= 8) part = ((part & 7) << (lg - 3)) | (part >> 3);
+    const int q = (part << (8 - lg)) + ((int)threadIdx.x >> lg);
+    const int chunk = threadIdx.x & (a.split - 1);
+    const int lane = threadIdx.x & 63;
+    const int lx = q & 15;
+    const int ly = q >> 4;
+    const int px = blk.px0 + lx;
+    const int py = blk.py0 + ly;
+    const bool valid = (px < a.clip_x1) && (py < a.clip_y1);
+    const uint64_t vmask = __ballot(valid);
+    // ray casts: one atomic per workgroup (a wave's count through LDS, one barrier at the
+    // end; every wave reaches it, a wave without pixels contributes 0): one atomic per
+    // wave put 16 MB per launch of atomic write traffic on a 3 MB frame
+    __shared__ unsigned wg_casts[4];
+    const unsigned n_casts = (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE>(a, blk, q, chunk, lane, lx, ly, px, py, valid);
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
-        if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
+        if (lane == 0) wg_casts[threadIdx.x >> 6] = total;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicAdd(a.casts, (unsigned long long)((wg_casts[0] + wg_casts[1]) + (wg_casts[2] + wg_casts[3])));
     }
 }
 
