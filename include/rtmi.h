@@ -145,6 +145,20 @@ int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig /* n x 3 
 int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
                         const float* d_dir, int n, float t_scale, int hit_rule, float* d_t,
                         int32_t* d_hit, void* stream);
+/* Diagnostic: rt_intersect by a chosen hit-test method.  Every method returns the same
+ * bits (the exact test decides; the filters only skip triangles it must reject):
+ *   RT_ISECT_SCAN    the single-phase exact scan of every triangle
+ *   RT_ISECT_FILTER  the fp32 two-phase filter (rays within the scene's filter bounds,
+ *                    else RT_E_UNSUPPORTED)
+ *   RT_ISECT_MFMA    the matrix-core filter of k_render_ps's bounce casts (a ray whose
+ *                    origin is outside the scene's box + 1 keeps every triangle)
+ * out_cand (optional, MFMA only): per ray, the triangles that reached the exact test. */
+#define RT_ISECT_SCAN 0
+#define RT_ISECT_FILTER 1
+#define RT_ISECT_MFMA 2
+int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
+                        float t_scale, int hit_rule, int method, float* out_t, int32_t* out_hit,
+                        int32_t* out_cand);
 
 /* draw_default_path_tracing (CPU/path_tracing/default_path_tracing.cpp:5-18;
  * GPU kernel GPU/path_tracing/default_path_tracing.cu:7-34): render the rectangle

@@ -4,6 +4,7 @@
 
 #include <math.h>
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include <cmath>
 #include <stdio.h>
@@ -288,6 +289,120 @@ bool build_filter(const float4& P0, const float4& P1, const float4& P2, double o
     return true;
 }
 
+// ---- matrix-core filter image (rt_internal.hpp, kMfRound; rt_trace.hpp, closest_hit_mf) ----
+
+uint16_t bf16_rne(float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    u += 0x7fffu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+double bf16_value(uint16_t h) {
+    const uint32_t u = (uint32_t)h << 16;
+    float f;
+    memcpy(&f, &u, 4);
+    return (double)f;
+}
+
+// x = hi + lo + r with |r| <= 2^-16 (1 + 2^-7) |x|
+void bf16_split(double x, uint16_t* hi, uint16_t* lo) {
+    *hi = bf16_rne((float)x);
+    *lo = bf16_rne((float)(x - bf16_value(*hi)));
+}
+
+// The four rows of one triangle over the features (d, o', R, 1) and its margins.
+// Error of the matrix-core evaluation of a row against its real value: the split
+// drops at most 3.1 * 2^-16 of sum |f_i b_i| (hi*lo, lo*hi kept; lo*lo and the split
+// remainders dropped), the fp32 accumulation of the 30 products adds <= 2^-18 of it
+// (measured 5.3 * 2^-24, profiles/probe/r2_mfma_split_probe.log), the rounding of
+// R and o' a few u: under 3.5 * 2^-16 S.  The exact float test is within 16u S = 2^-20 S
+// (build_filter).  The margins are build_filter's at c = 2^-12 >= 4.5x their sum, with
+// |d_i| <= dinf = kMfDirBound, B = mf_bound + max |v0_i| and the t test folded into
+// T' = T - ets A (|o'_i| <= mf_bound + dinf ets_max, ets_max = eps kFiltMaxTScale):
+//   S_A = dinf M,  S_U = 2 dinf B |e2|_1,  S_V = 2 dinf B |e1|_1,  S_T' <= (B + dinf ets_max) M
+//   eA = c S_A + F,  EW = 2 (c S_U + c S_V + eA) + F,  ET = c S_T' + 2 ets_max eA + F
+bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double mf_bound, double rows[4][10],
+                   float4* marg) {
+    const double v0[3] = {P0.x, P0.y, P0.z};
+    const double a[3] = {P1.x, P1.y, P1.z};  // e1
+    const double b[3] = {P2.x, P2.y, P2.z};  // e2
+    double N[3], G1[3], G2[3], M = 0.0, vmax = 0.0, n1 = 0.0, n2 = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        const int j = (i + 1) % 3, k = (i + 2) % 3;
+        N[i] = a[j] * b[k] - a[k] * b[j];
+        M += fabs(a[j] * b[k]) + fabs(a[k] * b[j]);
+        G1[i] = v0[j] * a[k] - v0[k] * a[j];
+        G2[i] = v0[j] * b[k] - v0[k] * b[j];
+        vmax = fmax(vmax, fabs(v0[i]));
+        n1 += fabs(a[i]);
+        n2 += fabs(b[i]);
+    }
+    const double w0 = v0[0] * N[0] + v0[1] * N[1] + v0[2] * N[2];
+    for (int r = 0; r < 4; ++r)
+        for (int k = 0; k < 10; ++k) rows[r][k] = 0.0;
+    for (int i = 0; i < 3; ++i) {
+        rows[0][i] = N[i];          // A  = d.N
+        rows[1][3 + i] = N[i];      // T' = o'.N + w0
+        rows[2][i] = -G2[i];        // U  = -G2.d + e2.R
+        rows[2][6 + i] = b[i];
+        rows[3][i] = G1[i];         // V  = G1.d - e1.R
+        rows[3][6 + i] = -a[i];
+    }
+    rows[1][9] = w0;
+    const double B = mf_bound + vmax;
+    const double c = ldexp(1.0, -12), F = ldexp(1.0, -90), dinf = (double)rt::kMfDirBound;
+    const double ets_max = 1e-5 * (double)rt::kFiltMaxTScale;
+    const double eA = c * dinf * M + F;
+    const double EW = 2.0 * (c * 2.0 * dinf * B * n2 + c * 2.0 * dinf * B * n1 + eA) + F;
+    const double ET = c * (B + dinf * ets_max) * M + 2.0 * ets_max * eA + F;
+    if (!(M < ldexp(1.0, 36)) || !(B < ldexp(1.0, 20)) || !std::isfinite(EW) || !std::isfinite(ET)) return false;
+    *marg = make_float4(round_up(eA), round_up(EW), round_up(ET), 0.0f);
+    return true;
+}
+
+// Device image of the matrix-core filter: frag (8 * rounds groups x 64 lanes x 8 bf16)
+// and marg (8 * rounds groups x 4 slots); layout in rt_internal.hpp.
+bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, std::vector<uint16_t>* frag,
+                    std::vector<float4>* marg) {
+    const int rounds = (n + rt::kMfRound - 1) / rt::kMfRound;
+    const size_t groups = (size_t)rounds * rt::kMfGroupsPerRound;
+    frag->assign(groups * 64 * 8, 0);
+    marg->assign(groups * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+    for (int r = 0; r < rounds; ++r) {
+        const int base = r * rt::kMfRound;
+        const int cnt = std::min(rt::kMfRound, n - base);
+        const int G = (cnt + 3) / 4;
+        for (int g = 0; g < G; ++g) {
+            const size_t gi = (size_t)r * rt::kMfGroupsPerRound + g;
+            for (int s = 0; s < 4; ++s) {
+                const int tl = s * G + (G - 1 - g);
+                if (tl >= cnt) continue;  // pad slot: zero rows and margins (masked off)
+                const int t = base + tl;
+                double rows[4][10];
+                if (!build_mf_rows(isect[(size_t)t * 3], isect[(size_t)t * 3 + 1], isect[(size_t)t * 3 + 2],
+                                   mf_bound, rows, &(*marg)[gi * 4 + s]))
+                    return false;
+                for (int i = 0; i < 4; ++i) {
+                    uint16_t bh[10], bl[10];
+                    for (int k = 0; k < 10; ++k) bf16_split(rows[i][k], &bh[k], &bl[k]);
+                    // the K order of the ray operand (rt_internal.hpp)
+                    const uint16_t kv[32] = {bh[0], bh[1], bh[2], bh[3], bh[4], bh[5], bh[6], bh[7],
+                                             bh[8], bh[9], bh[0], bh[1], bh[2], bh[3], bh[4], bh[5],
+                                             bh[6], bh[7], bh[8], bh[9], bl[0], bl[1], bl[2], bl[3],
+                                             bl[4], bl[5], bl[6], bl[7], bl[8], bl[9], 0, 0};
+                    const int row = 4 * s + i;
+                    for (int p = 0; p < 4; ++p) {
+                        const int lane = 16 * p + row;
+                        for (int j = 0; j < 8; ++j) (*frag)[(gi * 64 + lane) * 8 + j] = kv[8 * p + j];
+                    }
+                }
+            }
+        }
+    }
+    return true;
+}
+
 }  // namespace
 
 namespace rt {
@@ -425,13 +540,24 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     for (int i = 0; i < n && filt_ok; ++i)
         filt_ok = build_filter(isect[(size_t)i * 3 + 0], isect[(size_t)i * 3 + 1], isect[(size_t)i * 3 + 2],
                                obound, &filt[(size_t)i * rt::kFiltF4]);
+    // matrix-core filter of rays from surface points: origins within the scene's box + 1
+    double vmax_scene = 0.0;
+    for (float x : sc->tri) vmax_scene = fmax(vmax_scene, fabs((double)x));
+    // the kernel compares with this float; the margins are built for it
+    const double mf_bound = (double)round_up(vmax_scene * (1.0 + ldexp(1.0, -10)) + ldexp(1.0, -10));
+    std::vector<uint16_t> mf_frag;
+    std::vector<float4> mf_marg;
+    const bool mf_ok = filt_ok && build_mf_image(isect, n, mf_bound, &mf_frag, &mf_marg);
     sc->dev.n_surf = n_surf;
     sc->dev.n_tri = n;
     sc->dev.origin_bound = (float)obound;
+    sc->dev.mf_bound = (float)mf_bound;
     auto cleanup = [&]() {
         if (sc->dev.isect) (void)hipFree(sc->dev.isect);
         if (sc->dev.shade) (void)hipFree(sc->dev.shade);
         if (sc->dev.filt) (void)hipFree(sc->dev.filt);
+        if (sc->dev.mf_frag) (void)hipFree(sc->dev.mf_frag);
+        if (sc->dev.mf_marg) (void)hipFree(sc->dev.mf_marg);
         if (sc->dev.code_cpu) (void)hipFree(sc->dev.code_cpu);
         if (sc->dev.code_gpu) (void)hipFree(sc->dev.code_gpu);
         delete sc;
@@ -449,6 +575,14 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
         if (e == hipSuccess)
             e = hipMemcpy(sc->dev.filt, filt.data(), sizeof(float4) * filt.size(), hipMemcpyHostToDevice);
     }
+    if (e == hipSuccess && mf_ok) {
+        e = hipMalloc(&sc->dev.mf_frag, sizeof(uint16_t) * mf_frag.size());
+        if (e == hipSuccess) e = hipMalloc(&sc->dev.mf_marg, sizeof(float4) * mf_marg.size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->dev.mf_frag, mf_frag.data(), sizeof(uint16_t) * mf_frag.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->dev.mf_marg, mf_marg.data(), sizeof(float4) * mf_marg.size(), hipMemcpyHostToDevice);
+    }
     if (e != hipSuccess) {
         cleanup();
         return fail(RT_E_HIP, "scene upload failed: %s", hipGetErrorString(e));
@@ -465,6 +599,8 @@ int rt_scene_destroy(rt_scene* scene) {
     (void)hipFree(scene->dev.code_cpu);
     (void)hipFree(scene->dev.code_gpu);
     if (scene->dev.filt) (void)hipFree(scene->dev.filt);
+    if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
+    if (scene->dev.mf_marg) (void)hipFree(scene->dev.mf_marg);
     delete scene;
     return RT_OK;
 }
@@ -523,6 +659,59 @@ int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig, const fl
     (void)hipFree(d_t);
     (void)hipFree(d_h);
     if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect: %s", hipGetErrorString(e));
+    return RT_OK;
+}
+
+int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
+                        float t_scale, int hit_rule, int method, float* out_t, int32_t* out_hit,
+                        int32_t* out_cand) {
+    if (!ctx || !scene) return fail(RT_E_INVALID, "ctx/scene is NULL");
+    if (n < 0) return fail(RT_E_INVALID, "n < 0");
+    if (n == 0) return RT_OK;
+    if (!orig || !dir || !out_t || !out_hit) return fail(RT_E_INVALID, "NULL buffer");
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+    if (method != RT_ISECT_SCAN && method != RT_ISECT_FILTER && method != RT_ISECT_MFMA)
+        return fail(RT_E_INVALID, "bad method %d", method);
+    if (out_cand && method != RT_ISECT_MFMA) return fail(RT_E_INVALID, "out_cand needs RT_ISECT_MFMA");
+    if (method == RT_ISECT_MFMA && (!scene->dev.mf_frag || !(t_scale > 0.0f && t_scale <= rt::kFiltMaxTScale)))
+        return fail(RT_E_UNSUPPORTED, "no matrix-core filter image for this scene / t_scale");
+    if (method == RT_ISECT_FILTER) {
+        float omax = 0.0f, dmax = 0.0f;
+        for (size_t k = 0; k < 3 * (size_t)n; ++k) {
+            omax = fmaxf(omax, fabsf(orig[k]));
+            dmax = fmaxf(dmax, fabsf(dir[k]));
+        }
+        if (!(dmax <= 2.0f) || !rt::filter_usable(scene->dev, omax, 0.0f, 0.0f, t_scale))
+            return fail(RT_E_UNSUPPORTED, "rays outside the filter's bounds");
+    }
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
+    int32_t *d_h = nullptr, *d_c = nullptr;
+    const size_t b3 = sizeof(float) * 3 * (size_t)n;
+    hipError_t e = hipMalloc(&d_o, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_d, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_t, sizeof(float) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess && out_cand) e = hipMalloc(&d_c, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(d_o, orig, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_d, dir, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        if (method == RT_ISECT_MFMA)
+            e = rt::launch_intersect_mf(scene->dev, d_o, d_d, n, t_scale, hit_rule, d_t, d_h, d_c, 0);
+        else
+            e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, method == RT_ISECT_FILTER ? 1 : 0,
+                                     d_t, d_h, 0);
+    }
+    if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && out_cand) e = hipMemcpy(out_cand, d_c, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_o);
+    (void)hipFree(d_d);
+    (void)hipFree(d_t);
+    (void)hipFree(d_h);
+    if (d_c) (void)hipFree(d_c);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect_method: %s", hipGetErrorString(e));
     return RT_OK;
 }
 
@@ -600,7 +789,19 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     a.out_pitch = tile_size;
     a.out = d_out;
     a.casts = reinterpret_cast<unsigned long long*>(d_casts);
+    // RT_PS_PROF (with an RT_PROF=1 kernel build): k_render_ps's per-phase cycle sums to stderr
+    static const bool prof = getenv("RT_PS_PROF") != nullptr;
+    if (prof) RT_HIP(hipMalloc(&a.prof, 8 * sizeof(unsigned long long)));
+    if (prof) RT_HIP(hipMemsetAsync(a.prof, 0, 8 * sizeof(unsigned long long), (hipStream_t)stream));
     RT_HIP(rt::launch_render(a, (hipStream_t)stream));
+    if (prof) {
+        unsigned long long v[8];
+        RT_HIP(hipStreamSynchronize((hipStream_t)stream));
+        RT_HIP(hipMemcpy(v, a.prof, sizeof(v), hipMemcpyDeviceToHost));
+        RT_HIP(hipFree(a.prof));
+        fprintf(stderr, "{\"ps_prof\": {\"primary\": %llu, \"shade\": %llu, \"masks\": %llu, \"exact\": %llu, "
+                        "\"bounce_total\": %llu, \"trips\": %llu}}\n", v[0], v[1], v[2], v[3], v[4], v[5]);
+    }
     return RT_OK;
 }
 

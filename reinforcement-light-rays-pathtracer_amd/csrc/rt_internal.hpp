@@ -41,10 +41,33 @@ constexpr int kShadeF4 = 5;
 constexpr int kFiltF4 = 5;
 constexpr float kFiltMaxTScale = 16384.0f;
 
+// Matrix-core form of the same filter for rays from surface points (rt_trace.hpp,
+// closest_hit_mf; built by rt_capi.cpp, build_mf_image).  Per ray the ten features
+// f = (d, o', R = d x o, 1), o' = -o - ets d (RULE 0) or -o (RULE 1); per triangle four
+// rows over f: A = d.N, T' = w0 + o'.N, U = e2.R - G2.d, V = -e1.R + G1.d (double,
+// split into bf16 hi + lo).  One v_mfma_f32_16x16x32_bf16 evaluates
+// sum fh bh + fl bh + fh bl for 4 triangles x 16 rays, K = 32:
+//   k  0.. 7: fh0..fh7 | bh0..bh7      k 16..23: fl6..fl9, fh0..fh3 | bh6..bh9, bl0..bl3
+//   k  8..15: fh8, fh9, fl0..fl5 | bh8, bh9, bh0..bh5    k 24..31: fh4..fh9, 0, 0 | bl4..bl9, 0, 0
+// Triangles go in rounds of 32 (round r: triangles 32 r .., G = ceil(count / 4) groups);
+// group g of a round holds triangle s G + (G - 1 - g) in slot s = 0..3 (rows 4 s + i,
+// i = A, T', U, V).  Device image per group (index 8 r + g):
+//   frag: 64 lanes x 8 bf16 (lane l: row l & 15, k = 8 (l >> 4) ..), the A operand
+//   marg: 4 slots x {eA, EW, ET, 0}: the margins of the filter at c = 2^-12
+// The margins hold for |d_i| <= kMfDirBound (unit directions), |o_i| <= mf_bound (the
+// scene's box, widened by 2^-10 relative + 2^-10: surface points and the bounce loop's
+// 1e-5 offset) and t_scale <= kFiltMaxTScale; a lane outside keeps every triangle.
+constexpr int kMfRound = 32;
+constexpr int kMfGroupsPerRound = 8;
+constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
+
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
     float4* shade = nullptr;   // n_tri * kShadeF4
     float4* filt = nullptr;    // n_tri * kFiltF4 (nullptr: no filter records for this scene)
+    uint4* mf_frag = nullptr;  // matrix-core filter image (above; nullptr: none)
+    float4* mf_marg = nullptr;
+    float mf_bound = 0.0f;     // |o_i| bound of the matrix-core margins
     float origin_bound = 0.0f; // |o_i| bound the filter records were built for
     int32_t* code_cpu = nullptr;  // n_tri packed hit codes under hit rule CPU
     int32_t* code_gpu = nullptr;  // ... under hit rule GPU
@@ -78,6 +101,8 @@ struct RenderLaunch {
     // k_cull_ps (diagnostic): kRenderCullWords 64-bit candidate masks per wave
     // (n_blocks * split * 4 waves); unused by the renders
     unsigned long long* cull;
+    // RT_PROF builds only: per-phase s_memtime cycle sums of k_render_ps (8 counters)
+    unsigned long long* prof;
 };
 constexpr int kRenderCullWords = 4;  // candidate masks per wave: scenes of <= 256 triangles
 
@@ -270,6 +295,9 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, int use_filter, float* out_t,
                             int32_t* out_hit, hipStream_t stream);
+// the matrix-core filter (closest_hit_mf) on caller rays; cand: optional candidates per ray
+hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
+                               int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream);
 
 // exhaustive rcp_rn == 1.0f/x check over all 2^32 floats (4096 x 256 threads x 4096)
 hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream);

@@ -50,6 +50,28 @@ __global__ __launch_bounds__(256) void k_intersect(const DeviceScene s, int use_
     out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
 }
 
+// The matrix-core filter on caller rays (rt_intersect_method): every lane of a wave
+// takes part, lanes past n cast a dummy ray with no candidates.  cand (optional): the
+// candidates of each ray that reached the exact test.
+template <int RULE>
+__global__ __launch_bounds__(256) void k_intersect_mf(const DeviceScene s, const int32_t* __restrict__ code,
+                                                      const float* __restrict__ orig,
+                                                      const float* __restrict__ dir, int n, float t_scale,
+                                                      float* __restrict__ out_t, int32_t* __restrict__ out_hit,
+                                                      int32_t* __restrict__ cand) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool in = r < n;
+    const f3 o = in ? make3(orig[3 * r + 0], orig[3 * r + 1], orig[3 * r + 2]) : make3(0.0f, 0.0f, 0.0f);
+    const f3 d = in ? make3(dir[3 * r + 0], dir[3 * r + 1], dir[3 * r + 2]) : make3(0.0f, 0.0f, 1.0f);
+    __shared__ float wls[4][kMfWaveFloats];
+    int nc = 0;
+    const Hit h = closest_hit_mf<RULE, true>(s, o, d, t_scale, in, wls[threadIdx.x >> 6], &nc);
+    if (!in) return;
+    out_t[r] = (h.tri >= 0) ? h.t : __builtin_inff();
+    out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
+    if (cand != nullptr) cand[r] = nc;
+}
+
 
 
 
@@ -349,12 +371,13 @@ __global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
 }
 
 // the work of k_render_ps for one wave with at least one pixel; returns the lane's casts
-template <int SAMPLER, int RULE>
-__device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDesc& blk, int q, int chunk, int lane,
-                                            int lx, int ly, int px, int py, bool valid) {
+template <int SAMPLER, int RULE, int MF>
+__device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceScene& ms, float* wl,
+                                            const BlockDesc& blk, int q, int chunk, int lane, int lx, int ly, int px,
+                                            int py, bool valid) {
     extern __shared__ float s_ps[];
     const uint32_t pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
-    const float4* __restrict__ shade = a.scene.shade;
+    const float4* __restrict__ shade = ms.shade;  // (RT_PS_SCENE_LDS: the workgroup's LDS copy)
     const int n_surf = a.scene.n_surf;
     const int pc = a.per_chunk;
     float* const slots = s_ps + (size_t)(threadIdx.x >> 6) * pc * kPsFields * 64 + lane;
@@ -366,6 +389,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDe
 
     // ---- phase P: primary rays of the lane's samples ----
     unsigned n_casts = 0;
+#if RT_PROF
+    uint64_t pt[6] = {0, 0, 0, 0, 0, 0};  // P, shade, filter masks, exact, post, loops
+    uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
     const float nts = a.t_scale;
     cfloat4* __restrict__ isect = as_const(a.scene.isect);
     for (int k = 0; k < pc; ++k) {
@@ -410,6 +437,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDe
     }
 
     // ---- phase S: bounces ----
+#if RT_PROF
+    const uint64_t t_s = __builtin_amdgcn_s_memtime();
+    pt[0] += t_s - t0;
+#endif
     f3 acc = make3(0.0f, 0.0f, 0.0f);
     int k = 0;          // next slot
     int cur = 0;        // sample of the live path
@@ -444,42 +475,71 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDe
         return false;
     };
     bool live = valid && fetch();
+    // the bounce casts on the matrix cores when the scene has the image (wave-uniform)
+    const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
     for (;;) {
         if (__ballot(live) == 0ull) break;
+        if (!use_mf && !live) continue;
+#if RT_PROF
+        const uint64_t ta = __builtin_amdgcn_s_memtime();
+        pt[5] += 1;
+#endif
+        int s_tri = 0;
+        float s_cos = 0.0f;
+        if (live) {
+            // shade the live path's surface hit h (depth < max_bounces by construction)
+            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+            const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+            const float4 N = shade[h.tri * kShadeF4 + 0];
+            const float4 T = shade[h.tri * kShadeF4 + 1];
+            const float4 B = shade[h.tri * kShadeF4 + 2];
+            float r1, r2;
+            draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+            float cos_theta, sin_theta;
+            if (SAMPLER == 0) {
+                cos_theta = r1;
+                sin_theta = sqrtf(1.0f - r1 * r1);
+            } else {
+                cos_theta = sqrtf(r1);
+                sin_theta = sqrtf(1.0f - r1);
+            }
+            float sphi, cphi;
+            sincos_turn(r2, &sphi, &cphi);
+            const float sx = sin_theta * cphi, sz = sin_theta * sphi;
+            const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
+                                (sx * B.y + cos_theta * N.y) + sz * T.y,
+                                (sx * B.z + cos_theta * N.z) + sz * T.z);
+            s_tri = h.tri;
+            s_cos = cos_theta;
+            if (depth == 0) {
+                f_tri0 = s_tri;
+                f_cos0 = s_cos;
+            }
+            o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
+            d = normalize(sd);
+            ++depth;
+        }
+        // every lane of the wave takes part in the matrix-core filter; a lane without a
+        // live path casts its stale (finite) ray with no candidates
+#if RT_PROF
+        const uint64_t tb = __builtin_amdgcn_s_memtime();
+        uint64_t tm = tb;
+#endif
+        if (use_mf)
+#if RT_PROF
+            h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl, nullptr, &tm);
+#else
+            h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl);
+#endif
+        else
+            h = closest_hit_sel<RULE>(a.scene, 1, o, d, a.t_scale);
+#if RT_PROF
+        const uint64_t tc = __builtin_amdgcn_s_memtime();
+        pt[1] += tb - ta;
+        pt[2] += tm - tb;
+        pt[3] += tc - tm;
+#endif
         if (!live) continue;
-        // shade the live path's surface hit h (depth < max_bounces by construction)
-        const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
-        const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
-        const float4 N = shade[h.tri * kShadeF4 + 0];
-        const float4 T = shade[h.tri * kShadeF4 + 1];
-        const float4 B = shade[h.tri * kShadeF4 + 2];
-        float r1, r2;
-        draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
-        float cos_theta, sin_theta;
-        if (SAMPLER == 0) {
-            cos_theta = r1;
-            sin_theta = sqrtf(1.0f - r1 * r1);
-        } else {
-            cos_theta = sqrtf(r1);
-            sin_theta = sqrtf(1.0f - r1);
-        }
-        float sphi, cphi;
-        sincos_turn(r2, &sphi, &cphi);
-        const float sx = sin_theta * cphi, sz = sin_theta * sphi;
-        const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
-                            (sx * B.y + cos_theta * N.y) + sz * T.y,
-                            (sx * B.z + cos_theta * N.z) + sz * T.z);
-        const int s_tri = h.tri;
-        const float s_cos = cos_theta;
-        if (depth == 0) {
-            f_tri0 = s_tri;
-            f_cos0 = s_cos;
-        }
-        o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
-        d = normalize(sd);
-        ++depth;
-
-        h = closest_hit_sel<RULE>(a.scene, 1, o, d, a.t_scale);
         ++n_casts;
 
         bool terminal = true;
@@ -523,6 +583,18 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDe
         }
     }
 
+#if RT_PROF
+    pt[4] = __builtin_amdgcn_s_memtime() - t_s;  // the whole bounce phase
+    if (a.prof != nullptr && lane == 0) {
+        for (int i = 0; i < 6; ++i) atomicAdd(a.prof + i, (unsigned long long)pt[i]);
+    }
+#endif
+#if RT_PROF
+    pt[4] = __builtin_amdgcn_s_memtime() - t_s;  // the whole bounce phase
+    if (a.prof != nullptr && lane == 0) {
+        for (int i = 0; i < 6; ++i) atomicAdd(a.prof + i, (unsigned long long)pt[i]);
+    }
+#endif
     // fold the chunk sums of a pixel in chunk order: ((P0 + P1) + P2) + ...
     const int base = lane & ~(a.split - 1);
     f3 tot = acc;
@@ -543,9 +615,9 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const BlockDe
 }
 
 #ifndef RT_PS_MIN_WAVES
-#define RT_PS_MIN_WAVES 7  // 72 VGPRs: 7 waves per SIMD (4.84 vs 4.91 ms at 75 VGPRs, profiles/r2c_ab.log)
+#define RT_PS_MIN_WAVES 4  // the matrix-core filter's operands: ~99 VGPRs
 #endif
-template <int SAMPLER, int RULE>
+template <int SAMPLER, int RULE, int MF>
 __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -567,7 +639,42 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
     // end; every wave reaches it, a wave without pixels contributes 0): one atomic per
     // wave put 16 MB per launch of atomic write traffic on a 3 MB frame
     __shared__ unsigned wg_casts[4];
-    const unsigned n_casts = (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE>(a, blk, q, chunk, lane, lx, ly, px, py, valid);
+    // LDS after the sample slots (launch_render_t sizes it): the waves' exact-phase
+    // regions, then (RT_MF_LDS) the matrix-core filter's image
+    DeviceScene ms = a.scene;
+    float* wl = nullptr;
+    if (MF > 0) {
+        extern __shared__ float s_ps[];
+        float* const mf_base = s_ps + (size_t)4 * a.per_chunk * kPsFields * 64;
+        wl = mf_base + (size_t)(threadIdx.x >> 6) * kMfWaveFloats;
+        float* next = mf_base + 4 * kMfWaveFloats;
+#if RT_PS_SCENE_LDS
+        // hit-test and shading records of the scene (divergent per-lane reads: LDS latency
+        // instead of L1/L2)
+        {
+            const int n = a.scene.n_tri;
+            float4* li = reinterpret_cast<float4*>(next);
+            float4* ls = li + (size_t)n * kIsectF4;
+            for (int i = threadIdx.x; i < n * kIsectF4; i += 256) li[i] = a.scene.isect[i];
+            for (int i = threadIdx.x; i < n * kShadeF4; i += 256) ls[i] = a.scene.shade[i];
+            ms.isect = li;
+            ms.shade = ls;
+            next = reinterpret_cast<float*>(ls + (size_t)n * kShadeF4);
+        }
+#endif
+#if RT_MF_LDS
+        const int ng = mf_groups(a.scene.n_tri);
+        uint4* lf = reinterpret_cast<uint4*>(next);
+        float4* lm = reinterpret_cast<float4*>(lf + (size_t)ng * 64);
+        for (int i = threadIdx.x; i < ng * 64; i += 256) lf[i] = a.scene.mf_frag[i];
+        for (int i = threadIdx.x; i < ng * 4; i += 256) lm[i] = a.scene.mf_marg[i];
+        ms.mf_frag = lf;
+        ms.mf_marg = lm;
+#endif
+        if (RT_PS_SCENE_LDS || RT_MF_LDS) __syncthreads();
+    }
+    const unsigned n_casts =
+        (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE, MF>(a, ms, wl, blk, q, chunk, lane, lx, ly, px, py, valid);
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
         if (lane == 0) wg_casts[threadIdx.x >> 6] = total;
@@ -620,6 +727,22 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
     return hipGetLastError();
 }
 
+hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
+                               int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if (s.mf_frag == nullptr || s.mf_marg == nullptr || !(t_scale > 0.0f && t_scale <= kFiltMaxTScale))
+        return hipErrorInvalidValue;
+    const dim3 block(256);
+    const dim3 grid((unsigned)((n + 255) / 256));
+    if (hit_rule == 0)
+        hipLaunchKernelGGL(k_intersect_mf<0>, grid, block, 0, stream, s, s.code_cpu, orig, dir, n, t_scale, out_t,
+                           out_hit, cand);
+    else
+        hipLaunchKernelGGL(k_intersect_mf<1>, grid, block, 0, stream, s, s.code_gpu, orig, dir, n, t_scale, out_t,
+                           out_hit, cand);
+    return hipGetLastError();
+}
+
 #ifndef RT_STEAL_MAX_LDS
 #define RT_STEAL_MAX_LDS (64 * 1024)  // sample stealing when its LDS fits (0: never)
 #endif
@@ -639,8 +762,19 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= 64 * kRenderCullWords) {
         const size_t ps_lds = (size_t)4 * a.per_chunk * kPsFields * 64 * sizeof(float);
         if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
-            hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE>), dim3((unsigned)(a.n_blocks * a.split)), dim3(256),
-                               ps_lds, stream, a);
+            size_t mf_lds = 0;
+            if (RT_MF && a.scene.mf_frag != nullptr) {
+                mf_lds = (size_t)4 * kMfWaveFloats * sizeof(float);
+                if (RT_PS_SCENE_LDS) mf_lds += (size_t)a.scene.n_tri * (kIsectF4 + kShadeF4) * sizeof(float4);
+                if (RT_MF_LDS) mf_lds += (size_t)mf_groups(a.scene.n_tri) * (64 * sizeof(uint4) + 4 * sizeof(float4));
+            }
+            const dim3 grid((unsigned)(a.n_blocks * a.split));
+            if (mf_lds > 0 && a.scene.n_tri <= 64)
+                hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 1>), grid, dim3(256), ps_lds + mf_lds, stream, a);
+            else if (mf_lds > 0)
+                hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 4>), grid, dim3(256), ps_lds + mf_lds, stream, a);
+            else
+                hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 0>), grid, dim3(256), ps_lds, stream, a);
             return;
         }
     }

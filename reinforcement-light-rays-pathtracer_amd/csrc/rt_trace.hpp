@@ -380,8 +380,319 @@ __device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ f
     return h;
 }
 
+// ---- The filter on the matrix cores (rays from surface points) ----
+// closest_hit_filtered spends 31 VALU instructions per (ray, triangle) pair, 18 of them
+// the four dot products A, T, U, V.  closest_hit_mf evaluates those on
+// v_mfma_f32_16x16x32_bf16 (features and rows split into bf16 hi + lo, three products
+// per term: rt_internal.hpp, kMfRound) and keeps 11 VALU instructions per pair for
+// the sign fold and the three tests, at margins 16x wider (c = 2^-12, build_mf_rows in
+// rt_capi.cpp) than the fp32 filter's.  Wave-level: every lane of the wave calls it
+// (`active` false: a lane whose result is not used; it gets no candidates).
+typedef __bf16 mf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 mf_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float mf_f32x4 __attribute__((ext_vector_type(4)));
+typedef float mf_f32x2 __attribute__((ext_vector_type(2)));
+
+// x, y -> bf16x2 hi (RNE) and bf16x2 lo = RNE(x - hi) (x - hi is exact)
+__device__ __forceinline__ void mf_split2(float x, float y, uint32_t* hi, uint32_t* lo) {
+    const mf_f32x2 v = {x, y};
+    const uint32_t hb = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, mf_bf16x2));
+    const mf_f32x2 r = {x - __uint_as_float(hb << 16), y - __uint_as_float(hb & 0xffff0000u)};
+    *hi = hb;
+    *lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, mf_bf16x2));
+}
+
+// 4x4 transpose of the 16-lane rows: in, x_p at row r = M[r][p]; out, x_c at row r = M[c][r]
+__device__ __forceinline__ void mf_transpose(uint32_t& x0, uint32_t& x1, uint32_t& x2, uint32_t& x3) {
+    auto a = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);  // rows 2,3 of x0 <-> rows 0,1 of x2
+    auto b = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
+    auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);  // odd rows of x0 <-> even rows of x1
+    auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+    x0 = c[0];
+    x1 = c[1];
+    x2 = d[0];
+    x3 = d[1];
+}
+
+__device__ __forceinline__ mf_bf16x8 mf_frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {a, b, c, d};
+    return __builtin_bit_cast(mf_bf16x8, v);
+}
+
+// keep bit (bit 31) of one pair from the row values A, T', U, V and the margins
+__device__ __forceinline__ uint32_t mf_keep(mf_f32x4 q, float4 m) {
+    const uint32_t sg = __float_as_uint(q[0]) & 0x80000000u;
+    const float su = __uint_as_float(__float_as_uint(q[2]) ^ sg);
+    const float sv = __uint_as_float(__float_as_uint(q[3]) ^ sg);
+    const float st = __uint_as_float(__float_as_uint(q[1]) ^ sg);
+    const float aa = fabsf(q[0]);
+    const float w = (aa - su) - sv;
+    const float mn = fminf(fminf(su, sv), w);
+    return keep_bit(m.x - aa, mn + m.y, st + m.z);
+}
+
+// groups of the image that hold triangles (all rounds but the last are full)
+__host__ __device__ inline int mf_groups(int n_tri) {
+    if (n_tri <= 0) return 0;
+    const int rounds = (n_tri + kMfRound - 1) / kMfRound;
+    const int last = n_tri - (rounds - 1) * kMfRound;
+    return (rounds - 1) * kMfGroupsPerRound + (last + 3) / 4;
+}
+
+// The exact test of triangle i without the t window: t if the triangle passes
+// (detA != 0, t >= 0, u, v >= 0, u + v <= 1, t > eps for RULE 0), else +inf; the
+// operations of exact_one (same operands, same order, so the same bits).  Accepting t
+// when t < best + eps (RULE 0) / t < best (RULE 1), in index order, is exact_one's
+// result (+inf, like a NaN, never passes either window).
+template <int RULE>
+__device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i, f3 o, float nDx, float nDy,
+                                          float nDz) {
+    const float4 A = tri[i * kIsectF4 + 0];
+    const float4 E1 = tri[i * kIsectF4 + 1];
+    const float4 E2 = tri[i * kIsectF4 + 2];
+    const float bx = o.x - A.x, by = o.y - A.y, bz = o.z - A.z;
+    const float s1 = nDy * E2.z - E2.y * nDz;
+    const float s2 = nDy * E1.z - E1.y * nDz;
+    const float detA = (nDx * A.w - E1.x * s1) + E2.x * s2;
+    const float s3 = by * E2.z - E2.y * bz;
+    const float s4 = by * E1.z - E1.y * bz;
+    const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
+    const float s5 = nDy * bz - by * nDz;
+    const float s6 = E1.y * bz - by * E1.z;
+    const float det_u = (nDx * s3 - bx * s1) + E2.x * s5;
+    const float det_v = (nDx * s6 - E1.x * s5) + bx * s2;
+    float t, u, v;
+    if (RULE == 0) {
+        const float inv = RT_RCP(detA);
+        t = det_t * inv;
+        u = det_u * inv;
+        v = det_v * inv;
+    } else {
+        t = det_t / detA;
+        u = det_u / detA;
+        v = det_v / detA;
+    }
+    const bool ok = (detA != 0.0f) && (t >= 0.0f) && (u >= 0.0f) && (v >= 0.0f) && ((u + v) <= 1.0f) &&
+                    (RULE != 0 || t > kEps);
+    return ok ? t : __builtin_inff();
+}
+
+#ifndef RT_PROF
+#define RT_PROF 0  // 1: k_render_ps sums per-phase s_memtime cycles into RenderLaunch::prof
+#endif
+#ifndef RT_MF_COOP
+#define RT_MF_COOP 1  // 0: each lane runs its own candidates' exact tests (A/B builds)
+#endif
+
+// LDS of one wave for the shared exact phase: rays [6][64] (o, -D), pairs [cap] u16
+// (lane << 6 | triangle of the block), t [cap]
+#ifndef RT_MF_PAIR_CAP
+#define RT_MF_PAIR_CAP 256
+#endif
+constexpr int kMfPairCap = RT_MF_PAIR_CAP;
+constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2 + kMfPairCap;
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// The exact phase of one 64-triangle block (triangles tri0 + bit of F) shared by the
+// wave: the lanes' candidate pairs are listed in LDS in (lane, index) order and tested
+// 64 at a time by all lanes, then each lane folds its own results in index order.  The
+// trip count is (candidates of the wave) / 64 instead of the largest per-lane count.
+template <int RULE>
+__device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, int tri0, uint64_t F, f3 o,
+                                              float nDx, float nDy, float nDz, float* wl, int lane, Hit& h) {
+    const int cnt = __builtin_popcountll(F);
+    int incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (total == 0) return;
+    const int excl = incl - cnt;
+    float* ray = wl;
+    uint16_t* pr = reinterpret_cast<uint16_t*>(wl + 6 * 64);
+    float* tv = wl + 6 * 64 + kMfPairCap / 2;
+    ray[0 * 64 + lane] = o.x;
+    ray[1 * 64 + lane] = o.y;
+    ray[2 * 64 + lane] = o.z;
+    ray[3 * 64 + lane] = nDx;
+    ray[4 * 64 + lane] = nDy;
+    ray[5 * 64 + lane] = nDz;
+    for (int cb = 0; cb < total; cb += kMfPairCap) {
+        {
+            uint64_t G = F;
+            int p = excl - cb;
+            while (G != 0ull) {
+                const int b = __builtin_ctzll(G);
+                G &= G - 1ull;
+                if (p >= 0 && p < kMfPairCap) pr[p] = (uint16_t)((lane << 6) | b);
+                ++p;
+            }
+        }
+        wave_lds_sync();
+        const int nb = min(kMfPairCap, total - cb);
+        for (int k = lane; k < nb; k += 64) {
+            const uint32_t q = pr[k];
+            const int rl = (int)(q >> 6);
+            const f3 ro = make3(ray[0 * 64 + rl], ray[1 * 64 + rl], ray[2 * 64 + rl]);
+            tv[k] = exact_tv<RULE>(isect, tri0 + (int)(q & 63u), ro, ray[3 * 64 + rl], ray[4 * 64 + rl],
+                                   ray[5 * 64 + rl]);
+        }
+        wave_lds_sync();
+        {
+            uint64_t G = F;
+            int p = excl - cb;
+            while (G != 0ull) {
+                const int b = __builtin_ctzll(G);
+                G &= G - 1ull;
+                if (p >= 0 && p < kMfPairCap) {
+                    const float t = tv[p];
+                    if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
+                        h.t = t;
+                        h.tri = tri0 + b;
+                    }
+                }
+                ++p;
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// s.mf_frag / s.mf_marg may point to a workgroup's LDS copy of the image (k_render_ps);
+// wl: the wave's LDS for the shared exact phase (kMfWaveFloats floats)
+// NB: 64-triangle blocks per super-block (1: scenes of <= 64 triangles, fewer registers)
+template <int RULE, bool COUNT = false, int NB = 4>
+__device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, float t_scale, bool active,
+                                              float* wl, int* n_cand = nullptr, uint64_t* t_mask_end = nullptr) {
+    const float nDx = -(d.x * t_scale);
+    const float nDy = -(d.y * t_scale);
+    const float nDz = -(d.z * t_scale);
+    const bool finite = __builtin_isfinite(o.x) & __builtin_isfinite(o.y) & __builtin_isfinite(o.z) &
+                        __builtin_isfinite(d.x) & __builtin_isfinite(d.y) & __builtin_isfinite(d.z);
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    const bool keep_all = !(finite && om <= s.mf_bound && dm <= kMfDirBound);
+    const int lane = threadIdx.x & 63;
+    const int slot = lane >> 4;
+    const uint4* __restrict__ frag = s.mf_frag;
+    const float4* __restrict__ marg = s.mf_marg;
+    const mf_f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+
+    Hit h;
+    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+    h.tri = -1;
+    const int n_tri = s.n_tri;
+    // super-blocks of 256 triangles: the masks of all 8 rounds first (the ray operands
+    // die there), then the exact phase of each 64-triangle block
+    for (int sb = 0; sb < n_tri; sb += 2 * NB * kMfRound) {
+        uint64_t F0 = 0ull, F1 = 0ull, F2 = 0ull, F3 = 0ull;
+        {
+            const float Rx = fmaf(d.y, o.z, -(d.z * o.y));
+            const float Ry = fmaf(d.z, o.x, -(d.x * o.z));
+            const float Rz = fmaf(d.x, o.y, -(d.y * o.x));
+            const float ets = (RULE == 0) ? kEps * t_scale : 0.0f;
+            const float px = fmaf(-ets, d.x, -o.x), py = fmaf(-ets, d.y, -o.y), pz = fmaf(-ets, d.z, -o.z);
+            // features f = (d, o', R, 1) as bf16 pairs: h_k = (fh_2k, fh_2k+1), l_k likewise
+            uint32_t h0, h1, h2, h3, h4, l0, l1, l2, l3, l4;
+            mf_split2(d.x, d.y, &h0, &l0);
+            mf_split2(d.z, px, &h1, &l1);
+            mf_split2(py, pz, &h2, &l2);
+            mf_split2(Rx, Ry, &h3, &l3);
+            mf_split2(Rz, 1.0f, &h4, &l4);
+            // the four K parts of the lane's ray, then across the rows: B operand of ray block c
+            uint32_t b00 = h0, b01 = h1, b02 = h2, b03 = h3;  // k  0.. 7
+            uint32_t b10 = h4, b11 = l0, b12 = l1, b13 = l2;  // k  8..15
+            uint32_t b20 = l3, b21 = l4, b22 = h0, b23 = h1;  // k 16..23
+            uint32_t b30 = h2, b31 = h3, b32 = h4, b33 = 0u;  // k 24..31
+            mf_transpose(b00, b10, b20, b30);
+            mf_transpose(b01, b11, b21, b31);
+            mf_transpose(b02, b12, b22, b32);
+            mf_transpose(b03, b13, b23, b33);
+            const mf_bf16x8 B0 = mf_frag(b00, b01, b02, b03), B1 = mf_frag(b10, b11, b12, b13);
+            const mf_bf16x8 B2 = mf_frag(b20, b21, b22, b23), B3 = mf_frag(b30, b31, b32, b33);
+            const int n_rounds = min(2 * NB, (n_tri - sb + kMfRound - 1) / kMfRound);
+#pragma clang loop unroll(disable)
+            for (int rr = 0; rr < n_rounds; ++rr) {
+                const int r = sb / kMfRound + rr;
+                const int cnt = min(kMfRound, n_tri - r * kMfRound);
+                const int G = (cnt + 3) >> 2;
+                uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
+                const int gi0 = r * kMfGroupsPerRound;
+                uint4 afn = frag[gi0 * 64 + lane];
+                float4 mgn = marg[gi0 * 4 + slot];
+                for (int g = 0; g < G; ++g) {
+                    const uint4 af = afn;
+                    const float4 mg = mgn;
+                    if (g + 1 < G) {  // the next group's operand and margins ahead of this group's work
+                        afn = frag[(gi0 + g + 1) * 64 + lane];
+                        mgn = marg[(gi0 + g + 1) * 4 + slot];
+                    }
+                    const mf_bf16x8 A = mf_frag(af.x, af.y, af.z, af.w);
+                    const mf_f32x4 q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B0, zero, 0, 0, 0);
+                    const mf_f32x4 q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B1, zero, 0, 0, 0);
+                    const mf_f32x4 q2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B2, zero, 0, 0, 0);
+                    const mf_f32x4 q3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B3, zero, 0, 0, 0);
+                    m0 = __builtin_amdgcn_alignbit(m0, mf_keep(q0, mg), 31);
+                    m1 = __builtin_amdgcn_alignbit(m1, mf_keep(q1, mg), 31);
+                    m2 = __builtin_amdgcn_alignbit(m2, mf_keep(q2, mg), 31);
+                    m3 = __builtin_amdgcn_alignbit(m3, mf_keep(q3, mg), 31);
+                }
+                // lane (slot s, ray q) holds m_c for ray 16 c + q; after the transpose lane
+                // (c, q) holds the masks of slots 0..3 of its own ray: bit j of slot s's mask
+                // is triangle s G + j of the round
+                mf_transpose(m0, m1, m2, m3);
+                uint32_t Fr = m0 | (m1 << G) | (m2 << (2 * G)) | (m3 << (3 * G));
+                const uint32_t all = (cnt >= 32) ? 0xffffffffu : ((1u << cnt) - 1u);
+                Fr = keep_all ? all : (Fr & all);
+                const uint64_t Fs = (uint64_t)Fr << (32 * (rr & 1));  // wave-uniform word select
+                const int w = rr >> 1;
+                F0 |= (w == 0) ? Fs : 0ull;
+                if (NB > 1) {
+                    F1 |= (w == 1) ? Fs : 0ull;
+                    F2 |= (w == 2) ? Fs : 0ull;
+                    F3 |= (w == 3) ? Fs : 0ull;
+                }
+            }
+        }
+#if RT_PROF
+        if (t_mask_end) *t_mask_end = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+        for (int w = 0; w < NB; ++w) {
+            const int tri0 = sb + 64 * w;
+            if (tri0 >= n_tri) break;
+            const uint64_t Fw = active ? (w == 0 ? F0 : w == 1 ? F1 : w == 2 ? F2 : F3) : 0ull;
+            if (COUNT) *n_cand += __builtin_popcountll(Fw);
+#if RT_MF_COOP
+            mf_exact_wave<RULE>(s.isect, tri0, Fw, o, nDx, nDy, nDz, wl, lane, h);
+#else
+            uint64_t G = Fw;
+            while (G != 0ull) {
+                const int b = __builtin_ctzll(G);
+                G &= G - 1ull;
+                exact_one<RULE>(s.isect, tri0 + b, o, nDx, nDy, nDz, h);
+            }
+#endif
+        }
+    }
+    return h;
+}
+
 #ifndef RT_FILTER
 #define RT_FILTER 1  // 0: always the single-phase scan (A/B builds)
+#endif
+#ifndef RT_MF
+#define RT_MF 1  // 0: the bounce casts of k_render_ps on the fp32 filter (A/B builds)
+#endif
+#ifndef RT_PS_SCENE_LDS
+#define RT_PS_SCENE_LDS 1  // k_render_ps<MF>: the scene's isect/shade records in LDS (0: global)
+#endif
+#ifndef RT_MF_LDS
+#define RT_MF_LDS 0  // 1: k_render_ps reads the image from a workgroup copy in LDS (0: global)
 #endif
 
 template <int RULE>

@@ -35,7 +35,7 @@ EXPORTS = (
     "rt_params_default", "rt_ctx_create", "rt_ctx_destroy", "rt_last_error",
     "rt_cornell_counts", "rt_cornell_geometry", "rt_obj_geometry",
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
-    "rt_intersect", "rt_intersect_device", "rt_render", "rt_render_tiles_device",
+    "rt_intersect", "rt_intersect_device", "rt_intersect_method", "rt_render", "rt_render_tiles_device",
     "rt_pack_argb", "rt_save_bmp", "rt_save_png", "rt_selftest", "rt_filter_build", "rt_rect_candidates", "rt_cull_masks_device",
     "rt_dynet_read", "rt_dynet_write", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_set_mlp", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
@@ -97,6 +97,7 @@ def _declare(lib):
         "rt_scene_normals": (i, [_P, _FP]),
         "rt_intersect": (i, [_P, _P, _FP, _FP, i, f, i, _FP, _IP]),
         "rt_intersect_device": (i, [_P, _P, _P, _P, i, f, i, _P, _P, _P]),
+        "rt_intersect_method": (i, [_P, _P, _FP, _FP, i, f, i, i, _FP, _IP, _IP]),
         "rt_render": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
                           _FP, _U64P]),
         "rt_render_tiles_device": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams),

@@ -196,6 +196,23 @@ def intersect(ctx: Context, scene: Scene, orig: np.ndarray, direction: np.ndarra
     return t, h
 
 
+ISECT_SCAN, ISECT_FILTER, ISECT_MFMA = 0, 1, 2
+
+
+def intersect_method(ctx: Context, scene: Scene, orig: np.ndarray, direction: np.ndarray, t_scale: float,
+                     hit_rule: int, method: int, count: bool = False):
+    """rt_intersect_method: (t, hit) or, with count (ISECT_MFMA), (t, hit, candidates per ray)."""
+    o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+    n = o.shape[0]
+    t = np.zeros(n, np.float32)
+    h = np.zeros(n, np.int32)
+    c = np.zeros(n, np.int32) if count else None
+    check(lib().rt_intersect_method(ctx.handle, scene.handle, _fp(o), _fp(d), n, float(t_scale), hit_rule,
+                                    method, _fp(t), _ip(h), _ip(c) if count else None))
+    return (t, h, c) if count else (t, h)
+
+
 def intersect_device(ctx: Context, scene: Scene, orig_ptr: int, dir_ptr: int, n: int,
                      t_scale: float, hit_rule: int, t_ptr: int, hit_ptr: int, stream: int = 0):
     check(lib().rt_intersect_device(ctx.handle, scene.handle, ctypes.c_void_p(orig_ptr),

@@ -1,12 +1,12 @@
 #!/bin/bash
-# GPU session: parity tests of the default build, then in-process A/B of variants
-# on both presets.  Usage: bash tools/gpu_ab.sh variant1 variant2 ...
-mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-tail -3 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
-if [ $rc -gt 1 ]; then exit $rc; fi
-V=""; for v in "$@"; do V="$V build/variants/$v"; done
-timeout -k 10 300 python tools/ab_render.py $V --rounds 5 > gpurun_out/ab.log 2>&1 || exit $?
-tail -1 gpurun_out/ab.log
-timeout -k 10 300 python tools/ab_render.py $V --rounds 3 --preset 1 > gpurun_out/ab_gpu.log 2>&1 || exit $?
-tail -1 gpurun_out/ab_gpu.log
+# in-process A/B of librtmi variants (tools/ab_render.py), Cornell CPU preset bench config
+#   bash tools/gpu_ab.sh <tag> variant1 variant2 ...
+set -o pipefail
+tag=$1; shift
+cd "$(dirname "$0")/.." && mkdir -p gpurun_out
+args=""
+for v in "$@"; do args="$args build/variants/$v"; done
+timeout -k 10 300 python3 tools/ab_render.py $args --split 64 --rounds 7 > gpurun_out/${tag}_ab.json 2>gpurun_out/${tag}_ab.err || { tail -5 gpurun_out/${tag}_ab.err; exit 1; }
+python3 -c "
+import json;d=json.load(open('gpurun_out/${tag}_ab.json'))
+for k,v in d['results'].items(): print(k.split('/')[-1], v['ms_median'], v['gcasts_s'], v['same_image'])"
