@@ -130,6 +130,14 @@ def roofline(geom, casts_per_launch: float, kernel_ms: float, default_workload: 
         })
         if line["pmc_clock_ghz"]:
             line["frac_at_pmc_clock"] = round(valu / (1024 * line["pmc_clock_ghz"] * 1e9 * t / 2.0), 4)
+        # the bounce casts' filter on the matrix cores (v_mfma_f32_16x16x32_bf16): instructions
+        # and the matrix pipe's busy cycles (summed over the 1024 SIMDs) per launch
+        mf = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_INSTS_MFMA", 0.0) for k in ks)
+        mfb = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for k in ks)
+        if mf:
+            line["mfma_insts_per_launch"] = mf
+            line["mfma_insts_per_cast"] = round(mf / casts_per_launch, 3)
+            line["mfma_busy_frac"] = round(mfb / (1024 * 2.4e9 * t), 4)
     useful = casts_per_launch * 71.0 * n_tri / t / 1e12
     line["brute_force_tflops"] = round(useful, 2)
     line["brute_force_frac_of_fp32"] = round(useful / VALU_PEAK_TFLOPS, 4)
@@ -334,7 +342,7 @@ def main():
             },
             "ray_casts_per_step": total_casts // args.steps,
             "roofline": roofline(geom, rank_casts / args.steps, kernel_ms, default, {
-                "uniform": "k_render_ps<0,0>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal>",
+                "uniform": "k_render_ps<0,0,MF>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal>",
                 "sarsa": "k_sarsa_render + k_sarsa_apply", "dqn": "k_dqn_mlp + k_dqn_bounce (wavefront)"}[sampler]),
         }
         if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
