@@ -156,9 +156,34 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
 #define RT_ISECT_SCAN 0
 #define RT_ISECT_FILTER 1
 #define RT_ISECT_MFMA 2
+#define RT_ISECT_BVH 3 /* the exact BVH path (built on demand; every triangle's grazing test) */
 int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
                         float t_scale, int hit_rule, int method, float* out_t, int32_t* out_hit,
                         int32_t* out_cand);
+
+/* ---- acceleration structure for large scenes ----
+ * The reference scans every triangle per ray (CPU/rays/ray.cpp:14-28, GPU/rays/ray.cu:
+ * 16-141) and has no acceleration structure; Models/bunny.obj (4,968 triangles) and
+ * Medieval_House.obj (2,663) make that scan the whole cost.  The BVH path returns the
+ * scan's hit bit for bit (both hit rules): padded boxes that prove the exact test fails,
+ * per-origin lists of the triangles a ray could graze (rt_bvh.cpp).  RT_ACCEL_AUTO (the
+ * default) builds and uses it for scenes above RT_BVH_AUTO_MIN triangles; RT_ACCEL_SCAN
+ * never uses it; RT_ACCEL_BVH builds it for any scene (A/B).  Renders and rt_intersect
+ * follow the mode. */
+#define RT_ACCEL_AUTO 0
+#define RT_ACCEL_SCAN 1
+#define RT_ACCEL_BVH 2
+#define RT_BVH_AUTO_MIN 256
+int rt_scene_set_accel(rt_scene* scene, int mode);
+/* nodes, tree depth, grazing-list entries over all regions (out pointers may be NULL) */
+int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* glist_entries);
+/* rt_intersect through the BVH path with each ray's origin region: region[i] = the
+ * surface triangle (rt_scene index) a bounce ray leaves, its grazing list applies while
+ * the origin is within that triangle's region box; < 0 = unknown (every triangle's test).
+ * region may be NULL (all unknown).  Host arrays. */
+int rt_intersect_regions(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir,
+                         const int32_t* region, int n, float t_scale, int hit_rule, float* out_t,
+                         int32_t* out_hit);
 
 /* draw_default_path_tracing (CPU/path_tracing/default_path_tracing.cpp:5-18;
  * GPU kernel GPU/path_tracing/default_path_tracing.cu:7-34): render the rectangle

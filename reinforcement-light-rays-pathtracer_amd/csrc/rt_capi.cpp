@@ -68,7 +68,109 @@ struct rt_scene {
     std::vector<float> tri;      // host copy, n_tri x 9 (surfaces then lights)
     std::vector<float> albedo;   // n_surf x 3
     std::vector<float> emission; // n_light x 3
+    // exact BVH path (rt_bvh.cpp): built for scenes above RT_BVH_AUTO_MIN triangles or on
+    // request (rt_scene_set_accel); camera grazing lists cached per camera position (kept
+    // until the scene is destroyed: a launch in flight may still read an older one)
+    int accel = RT_ACCEL_AUTO;
+    bool has_bvh = false;
+    rt::BvhHost bvh;
+    float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, region
+    int32_t* d_gstart = nullptr;
+    int4* d_glist = nullptr;
+    struct CamList {
+        float x, y, z;
+        int4* ptr;
+        int n;
+        float lam;
+    };
+    mutable std::vector<CamList> cams;
 };
+
+namespace {
+// the BVH's device arrays, or nothing
+int scene_build_bvh(rt_scene* sc) {
+    if (sc->has_bvh) return RT_OK;
+    std::vector<float4> isect((size_t)sc->dev.n_tri * rt::kIsectF4);
+    if (hipMemcpy(isect.data(), sc->dev.isect, sizeof(float4) * isect.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return RT_E_HIP;
+    if (!rt::bvh_build(isect.data(), sc->dev.n_tri, &sc->bvh)) return RT_E_UNSUPPORTED;
+    const rt::BvhHost& b = sc->bvh;
+    const std::vector<float4>* arr[4] = {&b.nodes, &b.tris, &b.graze, &b.region};
+    hipError_t e = hipSuccess;
+    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
+        e = hipMalloc(&sc->d_bvh[k], sizeof(float4) * arr[k]->size());
+        if (e == hipSuccess)
+            e = hipMemcpy(sc->d_bvh[k], arr[k]->data(), sizeof(float4) * arr[k]->size(), hipMemcpyHostToDevice);
+    }
+    if (e == hipSuccess) e = hipMalloc(&sc->d_gstart, sizeof(int32_t) * b.gstart.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(sc->d_gstart, b.gstart.data(), sizeof(int32_t) * b.gstart.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&sc->d_glist, sizeof(int4) * std::max<size_t>(1, b.glist.size()));
+    if (e == hipSuccess && !b.glist.empty())
+        e = hipMemcpy(sc->d_glist, b.glist.data(), sizeof(int4) * b.glist.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return RT_E_HIP;
+    sc->has_bvh = true;
+    return RT_OK;
+}
+
+void scene_free_bvh(rt_scene* sc) {
+    for (auto& p : sc->d_bvh) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
+    if (sc->d_gstart) (void)hipFree(sc->d_gstart);
+    if (sc->d_glist) (void)hipFree(sc->d_glist);
+    sc->d_gstart = nullptr;
+    sc->d_glist = nullptr;
+    for (auto& c : sc->cams)
+        if (c.ptr) (void)hipFree(c.ptr);
+    sc->cams.clear();
+    sc->has_bvh = false;
+}
+
+bool scene_uses_bvh(const rt_scene* sc) {
+    if (!sc->has_bvh) return false;
+    if (sc->accel == RT_ACCEL_BVH) return true;
+    return sc->accel == RT_ACCEL_AUTO && sc->dev.n_tri > RT_BVH_AUTO_MIN;
+}
+
+// the device view of the scene for a launch from a camera at cam (BVH fields set when
+// the BVH path is on; the camera's grazing list built and cached on first use)
+rt::DeviceScene launch_scene(const rt_scene* sc, const float* cam) {
+    rt::DeviceScene d = sc->dev;
+    if (!scene_uses_bvh(sc)) return d;
+    d.bvh_nodes = sc->d_bvh[0];
+    d.bvh_tris = sc->d_bvh[1];
+    d.bvh_graze = sc->d_bvh[2];
+    d.bvh_region = sc->d_bvh[3];
+    d.bvh_gstart = sc->d_gstart;
+    d.bvh_glist = sc->d_glist;
+    d.bvh_sig_a = sc->bvh.sig_a;
+    d.bvh_sig_b = sc->bvh.sig_b;
+    d.bvh_lam_max = sc->bvh.lam_max;
+    if (cam == nullptr) return d;
+    for (const auto& c : sc->cams)
+        if (c.x == cam[0] && c.y == cam[1] && c.z == cam[2]) {
+            d.bvh_cam_glist = c.ptr;
+            d.bvh_cam_n = c.n;
+            d.bvh_cam_lam = c.lam;
+            return d;
+        }
+    std::vector<int4> list;
+    const float lam = rt::bvh_camera_list(sc->bvh, sc->dev.n_tri, cam[0], cam[1], cam[2], &list);
+    rt_scene::CamList c{cam[0], cam[1], cam[2], nullptr, (int)list.size(), lam};
+    if (hipMalloc(&c.ptr, sizeof(int4) * std::max<size_t>(1, list.size())) != hipSuccess) return d;
+    if (!list.empty() && hipMemcpy(c.ptr, list.data(), sizeof(int4) * list.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(c.ptr);
+        return d;  // no camera list: camera rays take the full grazing scan (lam 0)
+    }
+    sc->cams.push_back(c);
+    d.bvh_cam_glist = c.ptr;
+    d.bvh_cam_n = c.n;
+    d.bvh_cam_lam = c.lam;
+    return d;
+}
+}  // namespace
 
 namespace rt {
 void release_dqn_workspace(const rt_ctx* ctx);
@@ -186,7 +288,7 @@ int check_params(const rt_params* p) {
 rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p) {
     rt::RenderLaunch a;
     memset(&a, 0, sizeof(a));
-    a.scene = scene->dev;
+    a.scene = launch_scene(scene, cam ? cam->pos : nullptr);
     a.width = p->width;
     a.height = p->height;
     a.spp = p->spp;
@@ -587,6 +689,8 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
         cleanup();
         return fail(RT_E_HIP, "scene upload failed: %s", hipGetErrorString(e));
     }
+    // large scenes: the exact BVH path (a scene it cannot be built for keeps the scan)
+    if (n > RT_BVH_AUTO_MIN && scene_build_bvh(sc) != RT_OK) scene_free_bvh(sc);
     *out = sc;
     return RT_OK;
 }
@@ -601,7 +705,70 @@ int rt_scene_destroy(rt_scene* scene) {
     if (scene->dev.filt) (void)hipFree(scene->dev.filt);
     if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
     if (scene->dev.mf_marg) (void)hipFree(scene->dev.mf_marg);
+    scene_free_bvh(scene);
     delete scene;
+    return RT_OK;
+}
+
+int rt_scene_set_accel(rt_scene* scene, int mode) {
+    if (!scene) return fail(RT_E_INVALID, "scene is NULL");
+    if (mode != RT_ACCEL_AUTO && mode != RT_ACCEL_SCAN && mode != RT_ACCEL_BVH)
+        return fail(RT_E_INVALID, "bad accel mode %d", mode);
+    int rc = set_device(scene->ctx);
+    if (rc != RT_OK) return rc;
+    if (mode == RT_ACCEL_BVH || (mode == RT_ACCEL_AUTO && scene->dev.n_tri > RT_BVH_AUTO_MIN)) {
+        rc = scene_build_bvh(scene);
+        if (rc != RT_OK) return fail(rc, "BVH build failed (scene outside the filter's ranges?)");
+    }
+    scene->accel = mode;
+    return RT_OK;
+}
+
+int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* glist_entries) {
+    if (!scene) return fail(RT_E_INVALID, "scene is NULL");
+    if (n_nodes) *n_nodes = scene->has_bvh ? scene->bvh.n_nodes : 0;
+    if (depth) *depth = scene->has_bvh ? scene->bvh.depth : 0;
+    if (glist_entries) *glist_entries = scene->has_bvh ? (int64_t)scene->bvh.glist.size() : 0;
+    return RT_OK;
+}
+
+int rt_intersect_regions(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir,
+                         const int32_t* region, int n, float t_scale, int hit_rule, float* out_t,
+                         int32_t* out_hit) {
+    if (!ctx || !scene) return fail(RT_E_INVALID, "ctx/scene is NULL");
+    if (n < 0) return fail(RT_E_INVALID, "n < 0");
+    if (n == 0) return RT_OK;
+    if (!orig || !dir || !out_t || !out_hit) return fail(RT_E_INVALID, "NULL buffer");
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+    int rc = set_device(ctx);
+    if (rc != RT_OK) return rc;
+    rc = scene_build_bvh(const_cast<rt_scene*>(scene));
+    if (rc != RT_OK) return fail(rc, "BVH build failed");
+    // the BVH fields whatever the scene's mode
+    const int saved = scene->accel;
+    const_cast<rt_scene*>(scene)->accel = RT_ACCEL_BVH;
+    const rt::DeviceScene ds = launch_scene(scene, nullptr);
+    const_cast<rt_scene*>(scene)->accel = saved;
+    float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
+    int32_t *d_h = nullptr, *d_r = nullptr;
+    const size_t b3 = sizeof(float) * 3 * (size_t)n;
+    hipError_t e = hipMalloc(&d_o, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_d, b3);
+    if (e == hipSuccess) e = hipMalloc(&d_t, sizeof(float) * (size_t)n);
+    if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess && region) e = hipMalloc(&d_r, sizeof(int32_t) * (size_t)n);
+    if (e == hipSuccess) e = hipMemcpy(d_o, orig, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(d_d, dir, b3, hipMemcpyHostToDevice);
+    if (e == hipSuccess && region) e = hipMemcpy(d_r, region, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = rt::launch_intersect_bvh(ds, d_o, d_d, d_r, n, t_scale, hit_rule, d_t, d_h, 0);
+    if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+    (void)hipFree(d_o);
+    (void)hipFree(d_d);
+    (void)hipFree(d_t);
+    (void)hipFree(d_h);
+    if (d_r) (void)hipFree(d_r);
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect_regions: %s", hipGetErrorString(e));
     return RT_OK;
 }
 
@@ -619,6 +786,11 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
     if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
+    if (scene_uses_bvh(scene)) {  // the BVH path checks each ray's range itself
+        RT_HIP(rt::launch_intersect_bvh(launch_scene(scene, nullptr), d_orig, d_dir, nullptr, n, t_scale, hit_rule,
+                                        d_t, d_hit, (hipStream_t)stream));
+        return RT_OK;
+    }
     // device rays of unknown range: the single-phase scan (no filter bounds to rely on)
     RT_HIP(rt::launch_intersect(scene->dev, d_orig, d_dir, n, t_scale, hit_rule, 0, d_t, d_hit,
                                 (hipStream_t)stream));
@@ -650,8 +822,13 @@ int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig, const fl
         dmax = fmaxf(dmax, fabsf(dir[k]));
     }
     const int use_filter = (dmax <= 2.0f) ? rt::filter_usable(scene->dev, omax, 0.0f, 0.0f, t_scale) : 0;
-    if (e == hipSuccess)
-        e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, use_filter, d_t, d_h, 0);
+    if (e == hipSuccess) {
+        if (scene_uses_bvh(scene))
+            e = rt::launch_intersect_bvh(launch_scene(scene, nullptr), d_o, d_d, nullptr, n, t_scale, hit_rule, d_t,
+                                         d_h, 0);
+        else
+            e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, use_filter, d_t, d_h, 0);
+    }
     if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
     (void)hipFree(d_o);
@@ -670,6 +847,10 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
     if (n == 0) return RT_OK;
     if (!orig || !dir || !out_t || !out_hit) return fail(RT_E_INVALID, "NULL buffer");
     if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+    if (method == RT_ISECT_BVH) {
+        if (out_cand) return fail(RT_E_INVALID, "out_cand needs RT_ISECT_MFMA");
+        return rt_intersect_regions(ctx, scene, orig, dir, nullptr, n, t_scale, hit_rule, out_t, out_hit);
+    }
     if (method != RT_ISECT_SCAN && method != RT_ISECT_FILTER && method != RT_ISECT_MFMA)
         return fail(RT_E_INVALID, "bad method %d", method);
     if (out_cand && method != RT_ISECT_MFMA) return fail(RT_E_INVALID, "out_cand needs RT_ISECT_MFMA");

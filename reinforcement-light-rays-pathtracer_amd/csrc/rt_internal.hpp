@@ -61,6 +61,32 @@ constexpr int kMfRound = 32;
 constexpr int kMfGroupsPerRound = 8;
 constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
 
+// Exact BVH path for large scenes (rt_bvh.cpp, rt_trace.hpp closest_hit_bvh).
+//   nodes: 2 float4 per node {lo.xyz, link}, {hi.xyz, count} (int bits in w): count > 0 a
+//          leaf of tris [link, link + count), else children link, link + 1
+//   tris:  the kIsectF4 records in leaf order, [1].w = the original index (int bits)
+//   graze: per triangle {N (float), threshold of |d.N| for any origin within obound}
+//   region: per triangle the box (2 float4) a bounce origin from it lies in, lo.w = the
+//           window up to which its list is complete;
+//   gstart/glist: per region, the triangles that can be grazed from it {index, threshold,
+//           lambda_crit, 0}, by lambda_crit (the window from which each can matter)
+constexpr int kBvhK = 4;          // regular pairs: |A| >= K EW (barycentrics >= -1/K)
+constexpr int kBvhListMax = 512;  // grazing-list entries per origin region
+constexpr int kBvhMaxDepth = 24;  // traversal stack entries per lane (tree depth < 24)
+constexpr int kBvhCand = 4;       // rule-0 candidates kept per ray (overflow: exact scan)
+struct BvhHost {
+    std::vector<float4> nodes, tris, graze, region;
+    std::vector<int32_t> gstart;
+    std::vector<int4> glist;
+    std::vector<double> ti_cache;  // per triangle: N, w0, |N|, M, n1 + n2, vmax (camera lists)
+    int n_nodes = 0, depth = 0;
+    float sig_a = 0.f, sig_b = 0.f, lam_max = 0.f;
+    double B_s = 0.0, obound = 0.0;
+};
+bool bvh_build(const float4* isect, int n, BvhHost* out);
+// returns lambda_max of the list (the camera's window bound)
+float bvh_camera_list(const BvhHost& h, int n, float cx, float cy, float cz, std::vector<int4>* out);
+
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
     float4* shade = nullptr;   // n_tri * kShadeF4
@@ -71,6 +97,17 @@ struct DeviceScene {
     float origin_bound = 0.0f; // |o_i| bound the filter records were built for
     int32_t* code_cpu = nullptr;  // n_tri packed hit codes under hit rule CPU
     int32_t* code_gpu = nullptr;  // ... under hit rule GPU
+    // BVH path (nullptr: none); cam_glist is set per launch (bvh_camera_list)
+    const float4* bvh_nodes = nullptr;
+    const float4* bvh_tris = nullptr;
+    const float4* bvh_graze = nullptr;
+    const float4* bvh_region = nullptr;
+    const int32_t* bvh_gstart = nullptr;
+    const int4* bvh_glist = nullptr;
+    const int4* bvh_cam_glist = nullptr;
+    int bvh_cam_n = 0;
+    float bvh_cam_lam = 0.0f;  // lambda_max of the camera list
+    float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f, bvh_lam_max = 0.0f;
     int n_surf = 0;
     int n_tri = 0;
 };
@@ -295,6 +332,10 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, int use_filter, float* out_t,
                             int32_t* out_hit, hipStream_t stream);
+// the exact BVH path on caller rays; region: optional origin triangle per ray (< 0: unknown)
+hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, const int32_t* region,
+                                int n, float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
+                                hipStream_t stream);
 // the matrix-core filter (closest_hit_mf) on caller rays; cand: optional candidates per ray
 hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
                                int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream);

@@ -72,6 +72,26 @@ __global__ __launch_bounds__(256) void k_intersect_mf(const DeviceScene s, const
     if (cand != nullptr) cand[r] = nc;
 }
 
+// The exact BVH path on caller rays (large scenes): region[r] >= 0 the surface triangle
+// the ray leaves (its grazing list), otherwise (or region == nullptr) every triangle's
+// grazing test.
+template <int RULE>
+__global__ __launch_bounds__(256) void k_intersect_bvh(const DeviceScene s, const int32_t* __restrict__ code,
+                                                       const float* __restrict__ orig, const float* __restrict__ dir,
+                                                       const int32_t* __restrict__ region, int n, float t_scale,
+                                                       float* __restrict__ out_t, int32_t* __restrict__ out_hit) {
+    __shared__ int stk[kBvhMaxDepth * 256];
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const f3 o = make3(orig[3 * r + 0], orig[3 * r + 1], orig[3 * r + 2]);
+    const f3 d = make3(dir[3 * r + 0], dir[3 * r + 1], dir[3 * r + 2]);
+    int reg = (region != nullptr) ? region[r] : -2;
+    if (reg < 0 || reg >= s.n_tri) reg = -2;
+    const Hit h = closest_hit_bvh<RULE>(s, o, d, t_scale, reg, stk + threadIdx.x);
+    out_t[r] = (h.tri >= 0) ? h.t : __builtin_inff();
+    out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
+}
+
 
 
 
@@ -85,12 +105,17 @@ __global__ __launch_bounds__(256) void k_intersect_mf(const DeviceScene s, const
 // for the longest chunk: ~90% lane use at 4 samples per lane).  Each sample's value
 // goes to LDS; at the end lane c sums samples [c m, (c + 1) m) in order, exactly the
 // chunk sum of the fixed assignment, so the image is bit-identical.
-template <int PRESET, int SAMPLER, int RULE, bool STEAL>
+//
+// BVH: large scenes cast through closest_hit_bvh (the exact BVH path: same hits as the
+// scan), with the lane's origin region: the camera, or the surface a bounce leaves.
+template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1
 #endif
 __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch a) {
     extern __shared__ float s_val[];  // STEAL: [pixel of the workgroup][spp][3]
+    __shared__ int s_stk[BVH ? kBvhMaxDepth * 256 : 1];
+    int reg = -1;  // BVH: origin region of the current ray (-1: the camera)
     // workgroup -> (16x16 block, part); lane -> (pixel of the block, sample chunk)
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -133,7 +158,8 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
 
-        const Hit h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
+        const Hit h = BVH ? closest_hit_bvh<RULE>(a.scene, o, d, a.t_scale, reg, s_stk + threadIdx.x)
+                          : closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
         ++n_casts;
 
         bool terminal = false;
@@ -215,6 +241,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
             }
             o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
             d = normalize(sd);
+            reg = h.tri;
             ++depth;
             if (PRESET == 1 && depth == a.max_bounces) terminal = true;  // loop exhausted -> 0
         }
@@ -237,6 +264,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
                 ++s;
             }
             depth = 0;
+            reg = -1;
             tp = make3(1.0f, 1.0f, 1.0f);
             o = make3(a.cam_x, a.cam_y, a.cam_z);
             if (s < s_end) {
@@ -298,6 +326,15 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
 // LDS: per wave and sample slot k, five 64-lane rows (lane-contiguous: conflict-free):
 //   continuing: d.x, d.y, d.z, t, triangle;  ended: L.x, L.y, L.z, -, -1.
 constexpr int kPsFields = 5;
+
+#ifndef RT_PS_STEAL
+#define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
+#endif
+// floats of LDS per wave: the sample slots, then (RT_PS_STEAL) the wave's queue of
+// continuing samples, one u16 (k << 6 | lane) per slot
+__host__ __device__ constexpr int ps_wave_floats(int pc) {
+    return pc * kPsFields * 64 + (RT_PS_STEAL ? pc * 32 : 0);
+}
 
 // the bits of 64-triangle group g that are triangles of an n-triangle scene
 __device__ __forceinline__ uint64_t tri_mask(int n, int g) {
@@ -380,7 +417,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     const float4* __restrict__ shade = ms.shade;  // (RT_PS_SCENE_LDS: the workgroup's LDS copy)
     const int n_surf = a.scene.n_surf;
     const int pc = a.per_chunk;
-    float* const slots = s_ps + (size_t)(threadIdx.x >> 6) * pc * kPsFields * 64 + lane;
+    float* const wslots = s_ps + (size_t)(threadIdx.x >> 6) * ps_wave_floats(pc);
+    float* const slots = wslots + lane;
     const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
 
     // ---- candidate triangles of the wave's pixel rectangle (rect_cull, rt_cull.hpp) ----
@@ -451,6 +489,47 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     h.tri = 0;
     int f_tri0 = 0;
     float f_cos0 = 0.0f;
+#if RT_PS_STEAL
+    // The wave's continuing samples form one queue (slot-major: k, then lane), so a lane
+    // whose path ends takes the next queued sample of any lane of the wave instead of
+    // only its own: the wave runs ceil(casts / 64) trips instead of its busiest lane's.
+    // A finished sample's value goes back into its slot; every lane then sums its own
+    // slots in sample order (the fixed-chunk sum: the image is unchanged).
+    uint16_t* const queue = reinterpret_cast<uint16_t*>(wslots + pc * kPsFields * 64);
+    int q_total = 0;
+    for (int kk = 0; kk < pc; ++kk) {
+        const bool cont = valid && __float_as_int(slots[kk * kPsFields * 64 + 4 * 64]) >= 0;
+        const uint64_t m = __ballot(cont);
+        if (cont) queue[q_total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)((kk << 6) | lane);
+        q_total += __builtin_popcountll(m);
+    }
+    int q_next = 0;       // wave-uniform: next queue entry
+    float* own = slots;   // slot of the live path's sample (any lane's)
+    uint32_t lpix = pix;  // its pixel (RNG key)
+    bool live = false;
+    auto claim = [&]() {  // wave-level: lanes without a path take the next queued samples
+        const uint64_t need = __ballot(!live);
+        if (need == 0ull || q_next >= q_total) return;
+        const int j = q_next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+        if (!live && j < q_total) {
+            const uint32_t e = queue[j];
+            const int ol = (int)(e & 63u), kk = (int)(e >> 6);
+            own = wslots + kk * kPsFields * 64 + ol;
+            d = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
+            h.t = own[3 * 64];
+            h.tri = __float_as_int(own[4 * 64]);
+            o = cam;
+            depth = 0;
+            const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the lane's pixel
+            lpix = (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
+            cur = (ol & (a.split - 1)) * pc + kk;
+            live = true;
+        }
+        q_next = min(q_total, q_next + __builtin_popcountll(need));
+    };
+#endif
     // next continuing sample of the lane (adding the values of the ended ones in order)
     auto fetch = [&]() -> bool {
         while (k < pc) {
@@ -474,10 +553,17 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         }
         return false;
     };
+#if RT_PS_STEAL
+    (void)fetch;
+#else
     bool live = valid && fetch();
+#endif
     // the bounce casts on the matrix cores when the scene has the image (wave-uniform)
     const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
     for (;;) {
+#if RT_PS_STEAL
+        claim();
+#endif
         if (__ballot(live) == 0ull) break;
         if (!use_mf && !live) continue;
 #if RT_PROF
@@ -494,7 +580,11 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             const float4 T = shade[h.tri * kShadeF4 + 1];
             const float4 B = shade[h.tri * kShadeF4 + 2];
             float r1, r2;
+#if RT_PS_STEAL
+            draw2(lpix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+#else
             draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+#endif
             float cos_theta, sin_theta;
             if (SAMPLER == 0) {
                 cos_theta = r1;
@@ -576,19 +666,29 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             terminal = false;  // shade h on the next trip
         }
         if (terminal) {
+#if RT_PS_STEAL
+            own[0 * 64] = L.x;
+            own[1 * 64] = L.y;
+            own[2 * 64] = L.z;
+            live = false;
+#else
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
             live = fetch();
+#endif
         }
     }
-
-#if RT_PROF
-    pt[4] = __builtin_amdgcn_s_memtime() - t_s;  // the whole bounce phase
-    if (a.prof != nullptr && lane == 0) {
-        for (int i = 0; i < 6; ++i) atomicAdd(a.prof + i, (unsigned long long)pt[i]);
+#if RT_PS_STEAL
+    // the lane's own samples in order: ended ones hold their value in fields 0..2
+    for (int kk = 0; kk < pc; ++kk) {
+        const float* sl = slots + kk * kPsFields * 64;
+        acc.x = acc.x + sl[0 * 64];
+        acc.y = acc.y + sl[1 * 64];
+        acc.z = acc.z + sl[2 * 64];
     }
 #endif
+
 #if RT_PROF
     pt[4] = __builtin_amdgcn_s_memtime() - t_s;  // the whole bounce phase
     if (a.prof != nullptr && lane == 0) {
@@ -645,7 +745,7 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
     float* wl = nullptr;
     if (MF > 0) {
         extern __shared__ float s_ps[];
-        float* const mf_base = s_ps + (size_t)4 * a.per_chunk * kPsFields * 64;
+        float* const mf_base = s_ps + (size_t)4 * ps_wave_floats(a.per_chunk);
         wl = mf_base + (size_t)(threadIdx.x >> 6) * kMfWaveFloats;
         float* next = mf_base + 4 * kMfWaveFloats;
 #if RT_PS_SCENE_LDS
@@ -727,6 +827,21 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
     return hipGetLastError();
 }
 
+hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, const int32_t* region,
+                                int n, float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
+                                hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if (s.bvh_nodes == nullptr) return hipErrorInvalidValue;
+    const dim3 block(256), grid((unsigned)((n + 255) / 256));
+    if (hit_rule == 0)
+        hipLaunchKernelGGL(k_intersect_bvh<0>, grid, block, 0, stream, s, s.code_cpu, orig, dir, region, n, t_scale,
+                           out_t, out_hit);
+    else
+        hipLaunchKernelGGL(k_intersect_bvh<1>, grid, block, 0, stream, s, s.code_gpu, orig, dir, region, n, t_scale,
+                           out_t, out_hit);
+    return hipGetLastError();
+}
+
 hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
                                int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
@@ -759,8 +874,9 @@ hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const fl
 
 template <int PRESET, int SAMPLER, int RULE>
 static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
-    if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= 64 * kRenderCullWords) {
-        const size_t ps_lds = (size_t)4 * a.per_chunk * kPsFields * 64 * sizeof(float);
+    if (PRESET == 0 && RT_PS && a.use_filter && a.scene.n_tri <= 64 * kRenderCullWords &&
+        a.scene.bvh_nodes == nullptr) {
+        const size_t ps_lds = (size_t)4 * ps_wave_floats(a.per_chunk) * sizeof(float);
         if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
             size_t mf_lds = 0;
             if (RT_MF && a.scene.mf_frag != nullptr) {
@@ -779,12 +895,18 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
         }
     }
     const size_t lds = (size_t)(256 / a.split) * (size_t)a.spp * 3 * sizeof(float);
-    if (PRESET == 1 && lds <= (size_t)RT_STEAL_MAX_LDS)
-        hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true>), dim3((unsigned)(a.n_blocks * a.split)),
-                           dim3(256), lds, stream, a);
-    else
-        hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false>), dim3((unsigned)(a.n_blocks * a.split)),
-                           dim3(256), 0, stream, a);
+    const dim3 grid((unsigned)(a.n_blocks * a.split));
+    const bool steal = PRESET == 1 && lds <= (size_t)RT_STEAL_MAX_LDS;
+    if (a.scene.bvh_nodes != nullptr) {
+        if (steal)
+            hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, true>), grid, dim3(256), lds, stream, a);
+        else
+            hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, true>), grid, dim3(256), 0, stream, a);
+    } else if (steal) {
+        hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false>), grid, dim3(256), lds, stream, a);
+    } else {
+        hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false>), grid, dim3(256), 0, stream, a);
+    }
 }
 
 hipError_t launch_cull(const RenderLaunch& a, hipStream_t stream) {

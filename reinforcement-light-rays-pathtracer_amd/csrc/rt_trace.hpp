@@ -481,6 +481,9 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #ifndef RT_PROF
 #define RT_PROF 0  // 1: k_render_ps sums per-phase s_memtime cycles into RenderLaunch::prof
 #endif
+#ifndef RT_MF_PINGPONG
+#define RT_MF_PINGPONG 1  // 0: one operand set prefetched a group ahead (copied each group)
+#endif
 #ifndef RT_MF_COOP
 #define RT_MF_COOP 1  // 0: each lane runs its own candidates' exact tests (A/B builds)
 #endif
@@ -622,15 +625,8 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
                 const int G = (cnt + 3) >> 2;
                 uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
                 const int gi0 = r * kMfGroupsPerRound;
-                uint4 afn = frag[gi0 * 64 + lane];
-                float4 mgn = marg[gi0 * 4 + slot];
-                for (int g = 0; g < G; ++g) {
-                    const uint4 af = afn;
-                    const float4 mg = mgn;
-                    if (g + 1 < G) {  // the next group's operand and margins ahead of this group's work
-                        afn = frag[(gi0 + g + 1) * 64 + lane];
-                        mgn = marg[(gi0 + g + 1) * 4 + slot];
-                    }
+                // one 4-triangle group: 4 MFMAs (ray blocks 0..3), keep bits shifted in
+                auto group = [&](const uint4 af, const float4 mg) {
                     const mf_bf16x8 A = mf_frag(af.x, af.y, af.z, af.w);
                     const mf_f32x4 q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B0, zero, 0, 0, 0);
                     const mf_f32x4 q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B1, zero, 0, 0, 0);
@@ -640,7 +636,39 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
                     m1 = __builtin_amdgcn_alignbit(m1, mf_keep(q1, mg), 31);
                     m2 = __builtin_amdgcn_alignbit(m2, mf_keep(q2, mg), 31);
                     m3 = __builtin_amdgcn_alignbit(m3, mf_keep(q3, mg), 31);
+                };
+#if RT_MF_PINGPONG
+                // two operand sets in flight, no register copies: group g + 1's loads are
+                // issued before group g's MFMAs (32-bit offsets from the round's base)
+                const uint4* __restrict__ fr = frag + (size_t)gi0 * 64 + lane;
+                const float4* __restrict__ mr = marg + (size_t)gi0 * 4 + slot;
+                // (loads unconditional, clamped to the last group: a redundant reload of it)
+                uint4 fa = fr[0];
+                float4 ma = mr[0];
+                for (int g = 0; g < G; g += 2) {
+                    const int g1 = min(g + 1, G - 1);
+                    const uint4 fb = fr[g1 * 64];
+                    const float4 mb = mr[g1 * 4];
+                    group(fa, ma);
+                    if (g + 1 >= G) break;
+                    const int g2 = min(g + 2, G - 1);
+                    fa = fr[g2 * 64];
+                    ma = mr[g2 * 4];
+                    group(fb, mb);
                 }
+#else
+                uint4 afn = frag[gi0 * 64 + lane];
+                float4 mgn = marg[gi0 * 4 + slot];
+                for (int g = 0; g < G; ++g) {
+                    const uint4 af = afn;
+                    const float4 mg = mgn;
+                    if (g + 1 < G) {  // the next group's operand and margins ahead of this group's work
+                        afn = frag[(gi0 + g + 1) * 64 + lane];
+                        mgn = marg[(gi0 + g + 1) * 4 + slot];
+                    }
+                    group(af, mg);
+                }
+#endif
                 // lane (slot s, ray q) holds m_c for ray 16 c + q; after the transpose lane
                 // (c, q) holds the masks of slots 0..3 of its own ray: bit j of slot s's mask
                 // is triangle s G + j of the round
@@ -702,6 +730,223 @@ __device__ __forceinline__ Hit closest_hit_sel(const DeviceScene& s, int use_fil
     if (use_filter) return closest_hit_filtered<RULE>(s.filt, s.isect, s.n_tri, o, d, t_scale);
 #endif
     return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
+}
+
+// ---- Exact BVH path (large scenes; rt_bvh.cpp has the proof obligations) ----
+// Rule-1 result: the smallest t below 999999, ties to the smallest index (the scan's
+// strict t < best in index order).  Rule 0 (t < best + eps, ties to the later index)
+// depends on the order, but only through the triangles with t below tmin + 2 eps: the
+// first triangle with t = tmin resets the scan's best to tmin, and after it a triangle
+// is accepted only below best + eps.  Those few are kept (index, t), sorted by index
+// and folded as the scan folds them; if the fold's best could reach the cut, or more
+// than kBvhCand arrive, the ray takes the exact scan.
+struct BvhCand {
+    float tmin, cut;               // rule 0: smallest t, fl(fl(tmin + eps) + eps)
+    float ct[kBvhCand];
+    int ci[kBvhCand];
+    int nc;
+    bool overflow;
+    float bt;                      // rule 1: best t, index
+    int bi;
+};
+
+template <int RULE>
+__device__ __forceinline__ void bvh_insert(BvhCand& c, float t, int idx) {
+    if (RULE == 1) {
+        if (t < c.bt || (t == c.bt && idx < c.bi)) {
+            c.bt = t;
+            c.bi = idx;
+        }
+        return;
+    }
+    if (!(t < c.cut)) return;
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k)
+        if (k < c.nc && c.ci[k] == idx) return;  // listed already (BVH leaf and grazing list)
+    if (c.nc == kBvhCand) {
+        c.overflow = true;
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k)
+        if (k == c.nc) {
+            c.ct[k] = t;
+            c.ci[k] = idx;
+        }
+    ++c.nc;
+    if (t < c.tmin) {
+        c.tmin = t;
+        c.cut = (t + kEps) + kEps;
+    }
+}
+
+// the window of the traversal in ray-parameter units (lambda = t * t_scale): a regular
+// pair passing the exact test with t below the cut has lambda <= (cut ts + a) / (1 - b)
+template <int RULE>
+__device__ __forceinline__ float bvh_lam_hi(const BvhCand& c, const DeviceScene& s, float t_scale) {
+    const float cut = (RULE == 0) ? c.cut : c.bt;
+    return ((cut * t_scale + s.bvh_sig_a) / (1.0f - s.bvh_sig_b)) * 1.0000002f;
+}
+
+// region: >= 0 the surface triangle a bounce ray leaves, -1 the launch's camera,
+// -2 unknown (every triangle's grazing test).  stk: the lane's LDS stack, stride 256.
+template <int RULE>
+__device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, int region, int* stk) {
+    const float nDx = -(d.x * t_scale), nDy = -(d.y * t_scale), nDz = -(d.z * t_scale);
+    const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
+    // outside the bounds the records were built for (non-finite included): the scan
+    if (!(om <= s.origin_bound && dm <= kMfDirBound && t_scale <= kFiltMaxTScale))
+        return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
+    BvhCand c;
+    c.tmin = FLT_MAX;
+    c.cut = FLT_MAX;
+    c.nc = 0;
+    c.overflow = false;
+    c.bt = 999999.0f;
+    c.bi = -1;
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k) {
+        c.ct[k] = 0.0f;
+        c.ci[k] = 0;
+    }
+    // slab test: directions clamped away from 0 by 2^-100 (the node padding covers it)
+    auto safe = [](float x) { return (fabsf(x) < 7.8886091e-31f) ? copysignf(7.8886091e-31f, x) : x; };
+    const float ix = 1.0f / safe(d.x), iy = 1.0f / safe(d.y), iz = 1.0f / safe(d.z);
+    const float lam_lo = -2.0f * s.bvh_sig_a - 1e-6f;
+    const float4* __restrict__ nodes = s.bvh_nodes;
+    const float4* __restrict__ tris = s.bvh_tris;
+    auto slab = [&](int n, float lam_hi, float* entry) -> bool {
+        const float4 lo = nodes[2 * n], hi = nodes[2 * n + 1];
+        const float x0 = (lo.x - o.x) * ix, x1 = (hi.x - o.x) * ix;
+        const float y0 = (lo.y - o.y) * iy, y1 = (hi.y - o.y) * iy;
+        const float z0 = (lo.z - o.z) * iz, z1 = (hi.z - o.z) * iz;
+        const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), lam_lo));
+        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), lam_hi));
+        *entry = tn;
+        return tn <= tf;
+    };
+    int sp = 0;
+    int node = 0;
+    for (;;) {
+        const float4 hi = nodes[2 * node + 1];
+        const int cnt = __float_as_int(hi.w);
+        const int link = __float_as_int(nodes[2 * node].w);
+        if (cnt > 0) {
+            for (int j = link; j < link + cnt; ++j) {
+                const float t = exact_tv<RULE>(tris, j, o, nDx, nDy, nDz);
+                if (t <= FLT_MAX) bvh_insert<RULE>(c, t, __float_as_int(tris[j * kIsectF4 + 1].w));
+            }
+        } else {
+            const float lh = bvh_lam_hi<RULE>(c, s, t_scale);
+            float e0, e1;
+            const bool h0 = slab(link, lh, &e0);
+            const bool h1 = slab(link + 1, lh, &e1);
+            if (h0 && h1) {
+                const bool first0 = e0 <= e1;
+                stk[(sp++) * 256] = first0 ? link + 1 : link;
+                node = first0 ? link : link + 1;
+                continue;
+            }
+            if (h0 || h1) {
+                node = h0 ? link : link + 1;
+                continue;
+            }
+        }
+        if (sp == 0) break;
+        node = stk[(--sp) * 256];
+    }
+    // grazing pairs: the region's list, or every triangle
+    const float4* __restrict__ gz = s.bvh_graze;
+    bool full = region < -1;
+    if (region >= 0) {
+        const float4 L = s.bvh_region[2 * region], H = s.bvh_region[2 * region + 1];
+        full = !(o.x >= L.x && o.x <= H.x && o.y >= L.y && o.y <= H.y && o.z >= L.z && o.z <= H.z);
+    }
+    if (!full) {
+        // the list is complete up to window lam_k (entries by lambda_crit): a ray with a
+        // wider window scans every triangle; otherwise the entries up to its window
+        const float cut = (RULE == 0) ? c.cut : c.bt;
+        const float lam_cut = cut * t_scale * 1.0000002f;
+        const float lam_k = (region >= 0) ? s.bvh_region[2 * region].w : s.bvh_cam_lam;
+        full = !(lam_cut <= lam_k);
+        if (!full) {
+            const int4* gl = (region >= 0) ? s.bvh_glist + s.bvh_gstart[region] : s.bvh_cam_glist;
+            const int gn = (region >= 0) ? s.bvh_gstart[region + 1] - s.bvh_gstart[region] : s.bvh_cam_n;
+            for (int k = 0; k < gn; ++k) {
+                const int4 e = gl[k];
+                if (__int_as_float(e.z) > lam_cut) break;
+                const float4 g = gz[e.x];
+                const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
+                if (fabsf(a) <= __int_as_float(e.y)) {
+                    const float t = exact_tv<RULE>(s.isect, e.x, o, nDx, nDy, nDz);
+                    if (t <= FLT_MAX) bvh_insert<RULE>(c, t, e.x);
+                }
+            }
+        }
+    }
+    if (full) {
+        for (int i = 0; i < s.n_tri; ++i) {
+            const float4 g = gz[i];
+            const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
+            if (fabsf(a) <= g.w) {
+                const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
+                if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
+            }
+        }
+    }
+    Hit h;
+    if (RULE == 1) {
+        h.t = c.bt;
+        h.tri = c.bi;
+        return h;
+    }
+    if (c.overflow) return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
+    // the listed triangles below the final cut, in index order (insertion sort)
+    float ft[kBvhCand];
+    int fi[kBvhCand];
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k) {
+        ft[k] = 0.0f;
+        fi[k] = 0x7fffffff;
+    }
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k) {
+        if (k < c.nc && c.ct[k] < c.cut) {
+            float t = c.ct[k];
+            int i = c.ci[k];
+#pragma unroll
+            for (int j = 0; j < kBvhCand; ++j) {  // keep fi ascending: swap the larger one on
+                if (j <= m && i < fi[j]) {
+                    const float tt = ft[j];
+                    const int ii = fi[j];
+                    ft[j] = t;
+                    fi[j] = i;
+                    t = tt;
+                    i = ii;
+                }
+            }
+            ++m;
+        }
+    }
+    h.t = FLT_MAX;
+    h.tri = -1;
+    bool seen = false;
+    float bmax = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kBvhCand; ++k) {
+        if (k < m) {
+            if (ft[k] < h.t + kEps) {
+                h.t = ft[k];
+                h.tri = fi[k];
+            }
+            if (ft[k] == c.tmin) seen = true;
+            if (seen) bmax = fmaxf(bmax, h.t);
+        }
+    }
+    if (m > 0 && !(bmax + kEps <= c.cut)) return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
+    return h;
 }
 
 // two uniforms of event `ev` of sample `smp` of pixel `pix`

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""The exact BVH path vs the filter scan on the large scenes:
+bunny (4,968 triangles) in the Cornell box, GPU preset (80 bounces) and CPU preset, and
+Medieval_House.obj intersect batches.  Same images / hits bit for bit (checked here).
+
+    python tools/bench_bvh.py [--size 256] [--spp 16] [--rounds 3]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import rtmi  # noqa: E402
+from test_bvh import bunny_cornell, house, surface_rays  # noqa: E402
+
+
+def timed_render(ctx, sc, cam, p, tiles, out, casts, stream, rounds):
+    best = None
+    for _ in range(rounds):
+        casts.zero_()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rtmi.render_tiles_device(ctx, sc, cam, p, tiles, 32, out.data_ptr(), casts.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    return best, int(casts.item()), out.clone()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--spp", type=int, default=16)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    res = {}
+    with rtmi.Context(0) as ctx:
+        stream = torch.cuda.current_stream()
+        for preset in (1, 0):
+            g = bunny_cornell(rtmi, preset)
+            p = rtmi.default_params(preset, width=args.size, height=args.size, spp=args.spp, spp_split=8)
+            cam = rtmi.camera(rtmi.CAMERAS["cornell"])
+            tiles = rtmi.tiles.rank_tiles(args.size, args.size, 32, 0, 1)
+            out = torch.zeros((len(tiles), 32, 32, 3), device="cuda")
+            casts = torch.zeros(1, dtype=torch.int64, device="cuda")
+            with rtmi.Scene(ctx, g) as sc:
+                r = {"triangles": g.n_tri, **sc.accel_info()}
+                for mode, name in ((rtmi.ACCEL_BVH, "bvh"), (rtmi.ACCEL_SCAN, "scan")):
+                    sc.set_accel(mode)
+                    timed_render(ctx, sc, cam, p, tiles, out, casts, stream, 1)  # warm-up
+                    dt, n, img = timed_render(ctx, sc, cam, p, tiles, out, casts, stream, args.rounds)
+                    r[name] = {"ms": round(dt * 1e3, 2), "casts": n, "gcasts_s": round(n / dt / 1e9, 3)}
+                    r[name + "_img"] = img
+                r["same_image"] = bool(torch.equal(r.pop("bvh_img").view(torch.int32), r.pop("scan_img").view(torch.int32)))
+                r["speedup"] = round(r["scan"]["ms"] / r["bvh"]["ms"], 2)
+            res[f"bunny_cornell_preset{preset}_{args.size}x{args.size}_{args.spp}spp"] = r
+            print(json.dumps({k: v for k, v in r.items()}), flush=True)
+        g = house(rtmi)
+        with rtmi.Scene(ctx, g) as sc:
+            r = {"triangles": g.n_tri, **sc.accel_info()}
+            o, d, reg = surface_rays(g.all_triangles(), 1 << 20, 3, True)
+            for name, fn in (("bvh_regions", lambda: rtmi.intersect_regions(ctx, sc, o, d, reg, 720.0, 1)),
+                             ("bvh_unknown", lambda: rtmi.intersect_regions(ctx, sc, o, d, None, 720.0, 1)),
+                             ("scan", lambda: rtmi.intersect_method(ctx, sc, o, d, 720.0, 1, rtmi.ISECT_SCAN))):
+                fn()
+                t0 = time.perf_counter()
+                h = fn()
+                r[name] = {"ms_incl_copies": round((time.perf_counter() - t0) * 1e3, 2)}
+                r[name + "_h"] = h
+            r["same_hits"] = bool(np.array_equal(r.pop("bvh_regions_h")[1], r["scan_h"][1])
+                                  and np.array_equal(r.pop("bvh_unknown_h")[1], r.pop("scan_h")[1]))
+            res["house_intersect_1M"] = r
+            print(json.dumps(r), flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
