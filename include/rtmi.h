@@ -34,6 +34,7 @@ extern "C" {
 #define RT_E_NOMEM (-3)       /* allocation failed */
 #define RT_E_IO (-4)          /* file could not be opened / parsed */
 #define RT_E_UNSUPPORTED (-5) /* valid request this build does not implement */
+#define RT_E_INTERNAL (-6)    /* a self-check of the library failed */
 
 #define RT_HIT_NONE (-1)
 #define RT_HIT_TYPE_LIGHT 1u   /* enum IntersectionType AREA_LIGHT(_PLANE) */
@@ -184,6 +185,12 @@ int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t
 int rt_intersect_regions(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir,
                          const int32_t* region, int n, float t_scale, int hit_rule, float* out_t,
                          int32_t* out_hit);
+/* Host only (no GPU): build the BVH of n triangles (n x 9 vertices, the rt_scene_create
+ * order) and check its invariants (every triangle in one leaf, boxes nested and holding
+ * their triangles, grazing lists sorted and listing their own triangle).  stats
+ * (optional, 4 entries): nodes, depth, grazing-list entries, leaves.  RT_E_INTERNAL with
+ * rt_last_error() naming the first violation. */
+int rt_bvh_check(const float* tri_v, int n, int64_t* stats);
 
 /* draw_default_path_tracing (CPU/path_tracing/default_path_tracing.cpp:5-18;
  * GPU kernel GPU/path_tracing/default_path_tracing.cu:7-34): render the rectangle

@@ -27,7 +27,9 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "rt_internal.hpp"
@@ -290,14 +292,17 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         h.tris[(size_t)k * 3 + 2] = isect[(size_t)i * 3 + 2];
         memcpy(&h.tris[(size_t)k * 3 + 1].w, &i, 4);  // original index (the record's w is 0)
     }
-    // grazing data: the normal as a float and the threshold for any origin within obound
+    // grazing data: the normal as a float, the threshold for surface origins (within B_s)
+    // and, apart, the one for any origin within obound (the full scan)
     h.graze.resize((size_t)n);
+    h.graze_full.resize((size_t)n);
     for (int i = 0; i < n; ++i) {
         const TriInfo& t = ti[(size_t)i];
         float4 g;
         g.x = (float)t.N[0]; g.y = (float)t.N[1]; g.z = (float)t.N[2];
-        g.w = graze_threshold(t, bounds_for(t, obound));
+        g.w = graze_threshold(t, bounds_for(t, B_s));
         h.graze[(size_t)i] = g;
+        h.graze_full[(size_t)i] = graze_threshold(t, bounds_for(t, obound));
     }
     // origin regions: each triangle's box grown by the padding, the offset of the
     // bounce origin (1e-5 x |sd| <= 1.02e-5) and the error of the hit position
@@ -311,13 +316,11 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
     h.gstart.assign((size_t)n + 1, 0);
     h.glist.clear();
     std::vector<double> p_s((size_t)n), q_s((size_t)n);
-    std::vector<float> thr_s((size_t)n);
     for (int i = 0; i < n; ++i) {
         const TriInfo& t = ti[(size_t)i];
         const Bounds bs = bounds_for(t, B_s);
         p_s[(size_t)i] = bs.ET / t.nlen * (1.0 + 1e-6) + ldexp(1.0, -40);
         q_s[(size_t)i] = (kK * bs.EW + bs.eA) / t.nlen * (1.0 + 1e-6);
-        thr_s[(size_t)i] = graze_threshold(t, bs);
     }
     std::vector<std::pair<double, int>> cand;
     for (int k = 0; k < n; ++k) {
@@ -327,9 +330,9 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         const Bounds bk = bounds_for(t, obound);
         const double den = kK * bk.EW - bk.eA;
         const double g = 1.02e-5 + bk.ET / den + (bk.eA / den + 4.0 * kU) * lam_max + mu;
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = t.lo[a] - g;
-            hi[a] = t.hi[a] + g;
+        for (int a = 0; a < 3; ++a) {  // within the box the B_s thresholds hold for
+            lo[a] = std::max(t.lo[a] - g, -B_s);
+            hi[a] = std::min(t.hi[a] + g, B_s);
         }
         cand.clear();
         for (int i = 0; i < n; ++i) {
@@ -349,12 +352,10 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         h.region[(size_t)k * 2] = L;
         h.region[(size_t)k * 2 + 1] = H;
         for (const auto& c : cand) {
-            int4 e;
+            int2 e;
             e.x = c.second;
-            memcpy(&e.y, &thr_s[(size_t)c.second], 4);
             const float lcf = down(c.first);
-            memcpy(&e.z, &lcf, 4);
-            e.w = 0;
+            memcpy(&e.y, &lcf, 4);
             h.glist.push_back(e);
         }
         h.gstart[(size_t)k + 1] = (int32_t)h.glist.size();
@@ -420,6 +421,75 @@ float bvh_camera_list(const BvhHost& h, int n, float cx, float cy, float cz, std
         out->push_back(e);
     }
     return down(lam);
+}
+
+// Invariants of a host build (rt_bvh_check, CPU tests): every triangle in exactly one
+// leaf; each node's box holds its children's / its triangles' (vertices + padding);
+// each region's box holds its triangle, its list is sorted by lambda_crit and lists the
+// triangle itself at 0.  Returns an empty string or the first violation.
+std::string bvh_check(const float4* isect, int n, const BvhHost& h) {
+    char buf[160];
+    std::vector<int> seen((size_t)n, 0);
+    auto node_lo = [&](int k, int a) { return (&h.nodes[(size_t)k * 2].x)[a]; };
+    auto node_hi = [&](int k, int a) { return (&h.nodes[(size_t)k * 2 + 1].x)[a]; };
+    for (int k = 0; k < h.n_nodes; ++k) {
+        int link, cnt;
+        memcpy(&link, &h.nodes[(size_t)k * 2].w, 4);
+        memcpy(&cnt, &h.nodes[(size_t)k * 2 + 1].w, 4);
+        if (cnt > 0) {
+            for (int j = link; j < link + cnt; ++j) {
+                int i;
+                memcpy(&i, &h.tris[(size_t)j * 3 + 1].w, 4);
+                if (i < 0 || i >= n) return "leaf index out of range";
+                ++seen[(size_t)i];
+                const float4 P0 = isect[(size_t)i * 3], P1 = isect[(size_t)i * 3 + 1], P2 = isect[(size_t)i * 3 + 2];
+                const double v[3][3] = {{P0.x, P0.y, P0.z},
+                                        {P0.x + (double)P1.x, P0.y + (double)P1.y, P0.z + (double)P1.z},
+                                        {P0.x + (double)P2.x, P0.y + (double)P2.y, P0.z + (double)P2.z}};
+                for (int a = 0; a < 3; ++a)
+                    for (int q = 0; q < 3; ++q)
+                        if (!(node_lo(k, a) < v[q][a] && v[q][a] < node_hi(k, a))) {
+                            snprintf(buf, sizeof buf, "triangle %d outside leaf %d", i, k);
+                            return buf;
+                        }
+            }
+        } else {
+            if (link <= k || link + 1 >= h.n_nodes) return "bad child link";
+            for (int c = link; c <= link + 1; ++c)
+                for (int a = 0; a < 3; ++a)
+                    if (node_lo(c, a) < node_lo(k, a) || node_hi(c, a) > node_hi(k, a)) {
+                        snprintf(buf, sizeof buf, "node %d outside its parent %d", c, k);
+                        return buf;
+                    }
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (seen[(size_t)i] != 1) {
+            snprintf(buf, sizeof buf, "triangle %d in %d leaves", i, seen[(size_t)i]);
+            return buf;
+        }
+    for (int k = 0; k < n; ++k) {
+        const float4 L = h.region[(size_t)k * 2], H = h.region[(size_t)k * 2 + 1];
+        const float4 P0 = isect[(size_t)k * 3];
+        if (!(L.x <= P0.x && P0.x <= H.x && L.y <= P0.y && P0.y <= H.y && L.z <= P0.z && P0.z <= H.z)) {
+            snprintf(buf, sizeof buf, "region %d misses its triangle", k);
+            return buf;
+        }
+        float prev = -1.0f;
+        bool self = false;
+        for (int j = h.gstart[(size_t)k]; j < h.gstart[(size_t)k + 1]; ++j) {
+            float lc;
+            memcpy(&lc, &h.glist[(size_t)j].y, 4);
+            if (lc < prev) return "grazing list not sorted";
+            prev = lc;
+            if (h.glist[(size_t)j].x == k && lc == 0.0f) self = true;
+        }
+        if (!self) {
+            snprintf(buf, sizeof buf, "region %d does not list its own triangle", k);
+            return buf;
+        }
+    }
+    return std::string();
 }
 
 }  // namespace rt

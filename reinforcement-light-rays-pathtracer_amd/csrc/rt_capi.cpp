@@ -75,8 +75,9 @@ struct rt_scene {
     bool has_bvh = false;
     rt::BvhHost bvh;
     float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, region
+    float* d_graze_full = nullptr;
     int32_t* d_gstart = nullptr;
-    int4* d_glist = nullptr;
+    int2* d_glist = nullptr;
     struct CamList {
         float x, y, z;
         int4* ptr;
@@ -102,12 +103,16 @@ int scene_build_bvh(rt_scene* sc) {
         if (e == hipSuccess)
             e = hipMemcpy(sc->d_bvh[k], arr[k]->data(), sizeof(float4) * arr[k]->size(), hipMemcpyHostToDevice);
     }
+    if (e == hipSuccess) e = hipMalloc(&sc->d_graze_full, sizeof(float) * b.graze_full.size());
+    if (e == hipSuccess)
+        e = hipMemcpy(sc->d_graze_full, b.graze_full.data(), sizeof(float) * b.graze_full.size(),
+                      hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&sc->d_gstart, sizeof(int32_t) * b.gstart.size());
     if (e == hipSuccess)
         e = hipMemcpy(sc->d_gstart, b.gstart.data(), sizeof(int32_t) * b.gstart.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&sc->d_glist, sizeof(int4) * std::max<size_t>(1, b.glist.size()));
+    if (e == hipSuccess) e = hipMalloc(&sc->d_glist, sizeof(int2) * std::max<size_t>(1, b.glist.size()));
     if (e == hipSuccess && !b.glist.empty())
-        e = hipMemcpy(sc->d_glist, b.glist.data(), sizeof(int4) * b.glist.size(), hipMemcpyHostToDevice);
+        e = hipMemcpy(sc->d_glist, b.glist.data(), sizeof(int2) * b.glist.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) return RT_E_HIP;
     sc->has_bvh = true;
     return RT_OK;
@@ -119,6 +124,8 @@ void scene_free_bvh(rt_scene* sc) {
         p = nullptr;
     }
     if (sc->d_gstart) (void)hipFree(sc->d_gstart);
+    if (sc->d_graze_full) (void)hipFree(sc->d_graze_full);
+    sc->d_graze_full = nullptr;
     if (sc->d_glist) (void)hipFree(sc->d_glist);
     sc->d_gstart = nullptr;
     sc->d_glist = nullptr;
@@ -142,6 +149,7 @@ rt::DeviceScene launch_scene(const rt_scene* sc, const float* cam) {
     d.bvh_nodes = sc->d_bvh[0];
     d.bvh_tris = sc->d_bvh[1];
     d.bvh_graze = sc->d_bvh[2];
+    d.bvh_graze_full = sc->d_graze_full;
     d.bvh_region = sc->d_bvh[3];
     d.bvh_gstart = sc->d_gstart;
     d.bvh_glist = sc->d_glist;
@@ -721,6 +729,29 @@ int rt_scene_set_accel(rt_scene* scene, int mode) {
         if (rc != RT_OK) return fail(rc, "BVH build failed (scene outside the filter's ranges?)");
     }
     scene->accel = mode;
+    return RT_OK;
+}
+
+int rt_bvh_check(const float* tri_v, int n, int64_t* stats) {
+    if (!tri_v || n <= 0) return fail(RT_E_INVALID, "no triangles");
+    std::vector<float4> isect((size_t)n * rt::kIsectF4);
+    for (int i = 0; i < n; ++i) isect_record(tri_v + (size_t)i * 9, &isect[(size_t)i * 3]);
+    rt::BvhHost h;
+    if (!rt::bvh_build(isect.data(), n, &h)) return fail(RT_E_UNSUPPORTED, "BVH build failed");
+    const std::string err = rt::bvh_check(isect.data(), n, h);
+    if (stats) {
+        int64_t leaves = 0;
+        for (int k = 0; k < h.n_nodes; ++k) {
+            int cnt;
+            memcpy(&cnt, &h.nodes[(size_t)k * 2 + 1].w, 4);
+            leaves += cnt > 0;
+        }
+        stats[0] = h.n_nodes;
+        stats[1] = h.depth;
+        stats[2] = (int64_t)h.glist.size();
+        stats[3] = leaves;
+    }
+    if (!err.empty()) return fail(RT_E_INTERNAL, "BVH invariant: %s", err.c_str());
     return RT_OK;
 }
 

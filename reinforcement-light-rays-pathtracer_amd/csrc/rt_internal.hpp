@@ -1,6 +1,7 @@
 // rt_internal.hpp — types shared by the C-ABI layer and the gfx950 kernels.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include <hip/hip_runtime.h>
@@ -65,25 +66,29 @@ constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
 //   nodes: 2 float4 per node {lo.xyz, link}, {hi.xyz, count} (int bits in w): count > 0 a
 //          leaf of tris [link, link + count), else children link, link + 1
 //   tris:  the kIsectF4 records in leaf order, [1].w = the original index (int bits)
-//   graze: per triangle {N (float), threshold of |d.N| for any origin within obound}
+//   graze: per triangle {N (float), threshold of |d.N| for origins within the scene box};
+//          graze_full: the threshold for any origin within obound (the full scan)
 //   region: per triangle the box (2 float4) a bounce origin from it lies in, lo.w = the
 //           window up to which its list is complete;
-//   gstart/glist: per region, the triangles that can be grazed from it {index, threshold,
-//           lambda_crit, 0}, by lambda_crit (the window from which each can matter)
+//   gstart/glist: per region, the triangles that can be grazed from it {index,
+//           lambda_crit}, by lambda_crit (the window from which each can matter); the
+//           camera list (per launch) {index, threshold, lambda_crit, 0}
 constexpr int kBvhK = 4;          // regular pairs: |A| >= K EW (barycentrics >= -1/K)
-constexpr int kBvhListMax = 512;  // grazing-list entries per origin region
+constexpr int kBvhListMax = 4096;  // grazing-list entries per origin region
 constexpr int kBvhMaxDepth = 24;  // traversal stack entries per lane (tree depth < 24)
 constexpr int kBvhCand = 4;       // rule-0 candidates kept per ray (overflow: exact scan)
 struct BvhHost {
     std::vector<float4> nodes, tris, graze, region;
+    std::vector<float> graze_full;
     std::vector<int32_t> gstart;
-    std::vector<int4> glist;
+    std::vector<int2> glist;
     std::vector<double> ti_cache;  // per triangle: N, w0, |N|, M, n1 + n2, vmax (camera lists)
     int n_nodes = 0, depth = 0;
     float sig_a = 0.f, sig_b = 0.f, lam_max = 0.f;
     double B_s = 0.0, obound = 0.0;
 };
 bool bvh_build(const float4* isect, int n, BvhHost* out);
+std::string bvh_check(const float4* isect, int n, const BvhHost& h);
 // returns lambda_max of the list (the camera's window bound)
 float bvh_camera_list(const BvhHost& h, int n, float cx, float cy, float cz, std::vector<int4>* out);
 
@@ -101,9 +106,10 @@ struct DeviceScene {
     const float4* bvh_nodes = nullptr;
     const float4* bvh_tris = nullptr;
     const float4* bvh_graze = nullptr;
+    const float* bvh_graze_full = nullptr;
     const float4* bvh_region = nullptr;
     const int32_t* bvh_gstart = nullptr;
-    const int4* bvh_glist = nullptr;
+    const int2* bvh_glist = nullptr;
     const int4* bvh_cam_glist = nullptr;
     int bvh_cam_n = 0;
     float bvh_cam_lam = 0.0f;  // lambda_max of the camera list

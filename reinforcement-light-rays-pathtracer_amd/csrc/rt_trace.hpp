@@ -870,10 +870,22 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         const float lam_cut = cut * t_scale * 1.0000002f;
         const float lam_k = (region >= 0) ? s.bvh_region[2 * region].w : s.bvh_cam_lam;
         full = !(lam_cut <= lam_k);
-        if (!full) {
-            const int4* gl = (region >= 0) ? s.bvh_glist + s.bvh_gstart[region] : s.bvh_cam_glist;
-            const int gn = (region >= 0) ? s.bvh_gstart[region + 1] - s.bvh_gstart[region] : s.bvh_cam_n;
+        if (!full && region >= 0) {
+            const int2* gl = s.bvh_glist + s.bvh_gstart[region];
+            const int gn = s.bvh_gstart[region + 1] - s.bvh_gstart[region];
             for (int k = 0; k < gn; ++k) {
+                const int2 e = gl[k];
+                if (__int_as_float(e.y) > lam_cut) break;
+                const float4 g = gz[e.x];
+                const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
+                if (fabsf(a) <= g.w) {
+                    const float t = exact_tv<RULE>(s.isect, e.x, o, nDx, nDy, nDz);
+                    if (t <= FLT_MAX) bvh_insert<RULE>(c, t, e.x);
+                }
+            }
+        } else if (!full) {
+            const int4* gl = s.bvh_cam_glist;
+            for (int k = 0; k < s.bvh_cam_n; ++k) {
                 const int4 e = gl[k];
                 if (__int_as_float(e.z) > lam_cut) break;
                 const float4 g = gz[e.x];
@@ -889,7 +901,7 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         for (int i = 0; i < s.n_tri; ++i) {
             const float4 g = gz[i];
             const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-            if (fabsf(a) <= g.w) {
+            if (fabsf(a) <= s.bvh_graze_full[i]) {
                 const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
                 if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
             }
