@@ -358,8 +358,13 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
             memcpy(&e.y, &lcf, 4);
             h.glist.push_back(e);
         }
+        // each list starts 16-B aligned and is readable 4 entries past its end (the
+        // kernel's 4-wide steps): pad with entries that end any walk
+        const int2 stop = {0, 0x7f800000};  // lambda_crit = +inf
+        while (h.glist.size() % 2 != 0) h.glist.push_back(stop);
         h.gstart[(size_t)k + 1] = (int32_t)h.glist.size();
     }
+    for (int k = 0; k < 4; ++k) h.glist.push_back({0, 0x7f800000});
     h.n_nodes = (int)nn;
     h.depth = bld.depth;
     h.sig_a = up(sa * (1.0 + 1e-6));

@@ -796,7 +796,7 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
     const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     // outside the bounds the records were built for (non-finite included): the scan
-    if (!(om <= s.origin_bound && dm <= kMfDirBound && t_scale <= kFiltMaxTScale))
+    if (!(om <= s.origin_bound && dm <= kMfDirBound && t_scale > 0.0f && t_scale <= kFiltMaxTScale))
         return closest_hit<RULE>(s.isect, s.n_tri, o, d, t_scale);
     BvhCand c;
     c.tmin = FLT_MAX;
@@ -871,17 +871,32 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         const float lam_k = (region >= 0) ? s.bvh_region[2 * region].w : s.bvh_cam_lam;
         full = !(lam_cut <= lam_k);
         if (!full && region >= 0) {
+            // four entries per step, all loads in flight before the tests (the list is
+            // sorted: an entry past the window ends it; past-the-end reads stay inside
+            // the padded array)
             const int2* gl = s.bvh_glist + s.bvh_gstart[region];
             const int gn = s.bvh_gstart[region + 1] - s.bvh_gstart[region];
-            for (int k = 0; k < gn; ++k) {
-                const int2 e = gl[k];
-                if (__int_as_float(e.y) > lam_cut) break;
-                const float4 g = gz[e.x];
-                const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-                if (fabsf(a) <= g.w) {
-                    const float t = exact_tv<RULE>(s.isect, e.x, o, nDx, nDy, nDz);
-                    if (t <= FLT_MAX) bvh_insert<RULE>(c, t, e.x);
+            for (int k = 0; k < gn; k += 4) {
+                const int4 e01 = *reinterpret_cast<const int4*>(gl + k);
+                const int4 e23 = *reinterpret_cast<const int4*>(gl + k + 2);
+                const int idx[4] = {e01.x, e01.z, e23.x, e23.z};
+                const float lc[4] = {__int_as_float(e01.y), __int_as_float(e01.w), __int_as_float(e23.y),
+                                     __int_as_float(e23.w)};
+                float4 g[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) g[j] = gz[(k + j < gn) ? idx[j] : 0];
+                bool stop = false;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const bool in = (k + j < gn) && !(lc[j] > lam_cut);
+                    stop = stop || !in;
+                    const float a = fmaf(d.z, g[j].z, fmaf(d.y, g[j].y, d.x * g[j].x));
+                    if (!stop && fabsf(a) <= g[j].w) {
+                        const float t = exact_tv<RULE>(s.isect, idx[j], o, nDx, nDy, nDz);
+                        if (t <= FLT_MAX) bvh_insert<RULE>(c, t, idx[j]);
+                    }
                 }
+                if (stop) break;
             }
         } else if (!full) {
             const int4* gl = s.bvh_cam_glist;
