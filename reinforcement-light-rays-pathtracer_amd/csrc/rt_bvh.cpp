@@ -365,6 +365,96 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         h.gstart[(size_t)k + 1] = (int32_t)h.glist.size();
     }
     for (int k = 0; k < 4; ++k) h.glist.push_back({0, 0x7f800000});
+    // Normal-space index of the full grazing test (rays with no usable list: escaping
+    // rays, unknown regions).  Triangle i qualifies when |d.N~_i| <= thr_i(B) = alpha_i B
+    // + beta_i (B >= the ray's max |o_j|: K EW is affine in B), i.e. only if its unit
+    // normal lies in the band |d.n| <= s_i(B) = (thr_i(B) + 4u dinf M) / |N| around the
+    // great circle normal to d.  A BVH over the normals (folded to one hemisphere, the
+    // test being symmetric) with per-node maxima of alpha / |N| and beta' / |N| turns the
+    // scan of every triangle into a slab query.
+    {
+        const double dinf = (double)kMfDirBound;
+        std::vector<double> al((size_t)n), be((size_t)n), pt((size_t)n * 3);
+        h.gcoef.resize((size_t)n);
+        for (int i = 0; i < n; ++i) {
+            const TriInfo& t = ti[(size_t)i];
+            const Bounds b0 = bounds_for(t, 0.0);
+            // EW(B) = 2 (4 c dinf B (n1 + n2) / 2 ... ) : build_filter's form, affine in B
+            const double a = kK * 2.0 * (kC * 2.0 * dinf * (t.n1 + t.n2)) * (1.0 + 1e-9);
+            const double b = (kK * b0.EW + b0.eA + 8.0 * kU * dinf * t.M) * (1.0 + 1e-9);
+            float2 g;
+            g.x = up(a);
+            g.y = up(b);
+            h.gcoef[(size_t)i] = g;
+            al[(size_t)i] = (double)g.x / t.nlen * (1.0 + 1e-6);
+            be[(size_t)i] = ((double)g.y + 8.0 * kU * dinf * t.M) / t.nlen * (1.0 + 1e-6) + 1e-6;
+            double nn3[3] = {t.N[0] / t.nlen, t.N[1] / t.nlen, t.N[2] / t.nlen};
+            const bool flip = nn3[2] < 0.0 || (nn3[2] == 0.0 && (nn3[1] < 0.0 || (nn3[1] == 0.0 && nn3[0] < 0.0)));
+            for (int a3 = 0; a3 < 3; ++a3) pt[(size_t)i * 3 + a3] = flip ? -nn3[a3] : nn3[a3];
+        }
+        std::vector<int> id((size_t)n);
+        for (int i = 0; i < n; ++i) id[(size_t)i] = i;
+        h.nnodes.clear();
+        h.nleaf.clear();
+        // iterative median build: node record {c, alpha'}, {h, link|count, beta'} as 3 float4
+        struct Job { int node, b, e; };
+        std::vector<Job> jobs;
+        auto alloc = [&]() {
+            h.nnodes.resize(h.nnodes.size() + 3);
+            return (int)(h.nnodes.size() / 3) - 1;
+        };
+        jobs.push_back({alloc(), 0, n});
+        int nd = 0;
+        while (!jobs.empty()) {
+            const Job j = jobs.back();
+            jobs.pop_back();
+            double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX}, am = 0.0, bm = 0.0;
+            for (int k = j.b; k < j.e; ++k) {
+                const int i = id[(size_t)k];
+                for (int a3 = 0; a3 < 3; ++a3) {
+                    lo[a3] = std::min(lo[a3], pt[(size_t)i * 3 + a3]);
+                    hi[a3] = std::max(hi[a3], pt[(size_t)i * 3 + a3]);
+                }
+                am = std::max(am, al[(size_t)i]);
+                bm = std::max(bm, be[(size_t)i]);
+            }
+            float4 r0, r1, r2;
+            r0.x = (float)(0.5 * (lo[0] + hi[0])); r0.y = (float)(0.5 * (lo[1] + hi[1]));
+            r0.z = (float)(0.5 * (lo[2] + hi[2])); r0.w = up(am);
+            // half extents from the float centre, rounded up, + slack for the float test
+            r1.x = up(std::max(hi[0] - r0.x, r0.x - lo[0]) + 1e-6);
+            r1.y = up(std::max(hi[1] - r0.y, r0.y - lo[1]) + 1e-6);
+            r1.z = up(std::max(hi[2] - r0.z, r0.z - lo[2]) + 1e-6);
+            r2.x = 0.0f; r2.y = 0.0f; r2.z = up(bm);
+            const int cnt = j.e - j.b;
+            int link, cw;
+            if (cnt <= 4) {
+                link = (int)h.nleaf.size();
+                for (int k = j.b; k < j.e; ++k) h.nleaf.push_back(id[(size_t)k]);
+                cw = cnt;
+            } else {
+                int ax = 0;
+                for (int a3 = 1; a3 < 3; ++a3)
+                    if (hi[a3] - lo[a3] > hi[ax] - lo[ax]) ax = a3;
+                const int mid = j.b + cnt / 2;
+                std::nth_element(id.begin() + j.b, id.begin() + mid, id.begin() + j.e,
+                                 [&](int x, int y) { return pt[(size_t)x * 3 + ax] < pt[(size_t)y * 3 + ax]; });
+                link = alloc();
+                alloc();
+                jobs.push_back({link + 1, mid, j.e});
+                jobs.push_back({link, j.b, mid});
+                cw = 0;
+            }
+            memcpy(&r1.w, &link, 4);
+            memcpy(&r2.w, &cw, 4);
+            h.nnodes[(size_t)j.node * 3] = r0;
+            h.nnodes[(size_t)j.node * 3 + 1] = r1;
+            h.nnodes[(size_t)j.node * 3 + 2] = r2;
+            ++nd;
+        }
+        // depth of a median tree over n points: ceil(log2(n / 4)) + 1 < kBvhMaxDepth
+        if ((int)(h.nnodes.size() / 3) > 0 && n > (1 << (kBvhMaxDepth - 2)) * 4) return false;
+    }
     h.n_nodes = (int)nn;
     h.depth = bld.depth;
     h.sig_a = up(sa * (1.0 + 1e-6));
@@ -471,6 +561,39 @@ std::string bvh_check(const float4* isect, int n, const BvhHost& h) {
     for (int i = 0; i < n; ++i)
         if (seen[(size_t)i] != 1) {
             snprintf(buf, sizeof buf, "triangle %d in %d leaves", i, seen[(size_t)i]);
+            return buf;
+        }
+    // the normal-space index: every triangle in one leaf, its unit normal in the box
+    std::fill(seen.begin(), seen.end(), 0);
+    const int nn = (int)(h.nnodes.size() / 3);
+    for (int k = 0; k < nn; ++k) {
+        const float4 r0 = h.nnodes[(size_t)k * 3], r1 = h.nnodes[(size_t)k * 3 + 1], r2 = h.nnodes[(size_t)k * 3 + 2];
+        int link, cnt;
+        memcpy(&link, &r1.w, 4);
+        memcpy(&cnt, &r2.w, 4);
+        for (int j = link; cnt > 0 && j < link + cnt; ++j) {
+            const int i = h.nleaf[(size_t)j];
+            if (i < 0 || i >= n) return "normal leaf index out of range";
+            ++seen[(size_t)i];
+            const float4 E1 = isect[(size_t)i * 3 + 1], E2 = isect[(size_t)i * 3 + 2];
+            double N[3] = {(double)E1.y * E2.z - (double)E1.z * E2.y, (double)E1.z * E2.x - (double)E1.x * E2.z,
+                           (double)E1.x * E2.y - (double)E1.y * E2.x};
+            const double l = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+            const double c[3] = {r0.x, r0.y, r0.z}, hh[3] = {r1.x, r1.y, r1.z};
+            bool in_p = true, in_m = true;
+            for (int a = 0; a < 3; ++a) {
+                in_p = in_p && fabs(N[a] / l - c[a]) <= hh[a];
+                in_m = in_m && fabs(-N[a] / l - c[a]) <= hh[a];
+            }
+            if (!(in_p || in_m)) {
+                snprintf(buf, sizeof buf, "normal of triangle %d outside its leaf %d", i, k);
+                return buf;
+            }
+        }
+    }
+    for (int i = 0; i < n; ++i)
+        if (seen[(size_t)i] != 1) {
+            snprintf(buf, sizeof buf, "triangle %d in %d normal leaves", i, seen[(size_t)i]);
             return buf;
         }
     for (int k = 0; k < n; ++k) {

@@ -76,6 +76,9 @@ struct rt_scene {
     rt::BvhHost bvh;
     float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, region
     float* d_graze_full = nullptr;
+    float2* d_gcoef = nullptr;
+    float4* d_nnodes = nullptr;
+    int32_t* d_nleaf = nullptr;
     int32_t* d_gstart = nullptr;
     int2* d_glist = nullptr;
     struct CamList {
@@ -107,6 +110,14 @@ int scene_build_bvh(rt_scene* sc) {
     if (e == hipSuccess)
         e = hipMemcpy(sc->d_graze_full, b.graze_full.data(), sizeof(float) * b.graze_full.size(),
                       hipMemcpyHostToDevice);
+    auto up = [&](auto** dst, const auto& v) {
+        if (e != hipSuccess) return;
+        e = hipMalloc(dst, sizeof(v[0]) * std::max<size_t>(1, v.size()));
+        if (e == hipSuccess && !v.empty()) e = hipMemcpy(*dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice);
+    };
+    up(&sc->d_gcoef, b.gcoef);
+    up(&sc->d_nnodes, b.nnodes);
+    up(&sc->d_nleaf, b.nleaf);
     if (e == hipSuccess) e = hipMalloc(&sc->d_gstart, sizeof(int32_t) * b.gstart.size());
     if (e == hipSuccess)
         e = hipMemcpy(sc->d_gstart, b.gstart.data(), sizeof(int32_t) * b.gstart.size(), hipMemcpyHostToDevice);
@@ -126,6 +137,12 @@ void scene_free_bvh(rt_scene* sc) {
     if (sc->d_gstart) (void)hipFree(sc->d_gstart);
     if (sc->d_graze_full) (void)hipFree(sc->d_graze_full);
     sc->d_graze_full = nullptr;
+    if (sc->d_gcoef) (void)hipFree(sc->d_gcoef);
+    if (sc->d_nnodes) (void)hipFree(sc->d_nnodes);
+    if (sc->d_nleaf) (void)hipFree(sc->d_nleaf);
+    sc->d_gcoef = nullptr;
+    sc->d_nnodes = nullptr;
+    sc->d_nleaf = nullptr;
     if (sc->d_glist) (void)hipFree(sc->d_glist);
     sc->d_gstart = nullptr;
     sc->d_glist = nullptr;
@@ -150,6 +167,9 @@ rt::DeviceScene launch_scene(const rt_scene* sc, const float* cam) {
     d.bvh_tris = sc->d_bvh[1];
     d.bvh_graze = sc->d_bvh[2];
     d.bvh_graze_full = sc->d_graze_full;
+    d.bvh_gcoef = sc->d_gcoef;
+    d.bvh_nnodes = sc->d_nnodes;
+    d.bvh_nleaf = sc->d_nleaf;
     d.bvh_region = sc->d_bvh[3];
     d.bvh_gstart = sc->d_gstart;
     d.bvh_glist = sc->d_glist;

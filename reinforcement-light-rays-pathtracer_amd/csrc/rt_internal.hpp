@@ -80,6 +80,9 @@ constexpr int kBvhCand = 4;       // rule-0 candidates kept per ray (overflow: e
 struct BvhHost {
     std::vector<float4> nodes, tris, graze, region;
     std::vector<float> graze_full;
+    std::vector<float2> gcoef;   // per triangle: the full-test threshold alpha B + beta
+    std::vector<float4> nnodes;  // normal-space BVH, 3 float4 per node
+    std::vector<int32_t> nleaf;  // its leaves' triangles
     std::vector<int32_t> gstart;
     std::vector<int2> glist;
     std::vector<double> ti_cache;  // per triangle: N, w0, |N|, M, n1 + n2, vmax (camera lists)
@@ -107,6 +110,9 @@ struct DeviceScene {
     const float4* bvh_tris = nullptr;
     const float4* bvh_graze = nullptr;
     const float* bvh_graze_full = nullptr;
+    const float2* bvh_gcoef = nullptr;
+    const float4* bvh_nnodes = nullptr;
+    const int32_t* bvh_nleaf = nullptr;
     const float4* bvh_region = nullptr;
     const int32_t* bvh_gstart = nullptr;
     const int2* bvh_glist = nullptr;

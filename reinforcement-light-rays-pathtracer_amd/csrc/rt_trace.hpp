@@ -858,6 +858,14 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
     }
     // grazing pairs: the region's list, or every triangle
     const float4* __restrict__ gz = s.bvh_graze;
+#ifdef RT_BVH_TIMING_TRAVERSAL_ONLY
+    {  // timing-only build (wrong hits): the traversal alone
+        Hit hh;
+        hh.t = (RULE == 0) ? c.tmin : c.bt;
+        hh.tri = (RULE == 0) ? (c.nc ? c.ci[0] : -1) : c.bi;
+        return hh;
+    }
+#endif
     bool full = region < -1;
     if (region >= 0) {
         const float4 L = s.bvh_region[2 * region], H = s.bvh_region[2 * region + 1];
@@ -912,14 +920,41 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
             }
         }
     }
+#ifdef RT_BVH_TIMING_NO_FULL
+    full = false;  // timing-only build (wrong hits): no normal-space query
+#endif
     if (full) {
-        for (int i = 0; i < s.n_tri; ++i) {
-            const float4 g = gz[i];
-            const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-            if (fabsf(a) <= s.bvh_graze_full[i]) {
-                const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
-                if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
+        // every triangle whose |d.N| is within its threshold at B = max |o_i|: a slab
+        // query |d.n| <= alpha' B + beta' over the normal-space BVH (rt_bvh.cpp)
+        const float B = om * 1.000001f;
+        const float4* __restrict__ nn = s.bvh_nnodes;
+        const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+        int nsp = 0, nd = 0;
+        for (;;) {
+            const float4 r0 = nn[3 * nd], r1 = nn[3 * nd + 1], r2 = nn[3 * nd + 2];
+            const float band = fmaf(r0.w, B, r2.z) * 1.000001f;
+            const float dc = fmaf(d.z, r0.z, fmaf(d.y, r0.y, d.x * r0.x));
+            const float rr = fmaf(az, r1.z, fmaf(ay, r1.y, ax * r1.x));
+            const int link = __float_as_int(r1.w), cnt = __float_as_int(r2.w);
+            if (!(dc - rr > band || dc + rr < -band)) {
+                if (cnt == 0) {
+                    stk[(nsp++) * 256] = link + 1;
+                    nd = link;
+                    continue;
+                }
+                for (int k = link; k < link + cnt; ++k) {
+                    const int i = s.bvh_nleaf[k];
+                    const float4 g = gz[i];
+                    const float2 q = s.bvh_gcoef[i];
+                    const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
+                    if (fabsf(a) <= fmaf(q.x, B, q.y) * 1.000001f) {
+                        const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
+                        if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
+                    }
+                }
             }
+            if (nsp == 0) break;
+            nd = stk[(--nsp) * 256];
         }
     }
     Hit h;
