@@ -157,7 +157,7 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
 #define RT_ISECT_SCAN 0
 #define RT_ISECT_FILTER 1
 #define RT_ISECT_MFMA 2
-#define RT_ISECT_BVH 3 /* the exact BVH path (built on demand; every triangle's grazing test) */
+#define RT_ISECT_BVH 3 /* the exact BVH path (built on demand) */
 int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
                         float t_scale, int hit_rule, int method, float* out_t, int32_t* out_hit,
                         int32_t* out_cand);
@@ -167,7 +167,7 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
  * 16-141) and has no acceleration structure; Models/bunny.obj (4,968 triangles) and
  * Medieval_House.obj (2,663) make that scan the whole cost.  The BVH path returns the
  * scan's hit bit for bit (both hit rules): padded boxes that prove the exact test fails,
- * per-origin lists of the triangles a ray could graze (rt_bvh.cpp).  RT_ACCEL_AUTO (the
+ * and a second BVH over the triangles' planes for the pairs a ray could graze (rt_bvh.cpp).  RT_ACCEL_AUTO (the
  * default) builds and uses it for scenes above RT_BVH_AUTO_MIN triangles; RT_ACCEL_SCAN
  * never uses it; RT_ACCEL_BVH builds it for any scene (A/B).  Renders and rt_intersect
  * follow the mode. */
@@ -176,19 +176,13 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
 #define RT_ACCEL_BVH 2
 #define RT_BVH_AUTO_MIN 256
 int rt_scene_set_accel(rt_scene* scene, int mode);
-/* nodes, tree depth, grazing-list entries over all regions (out pointers may be NULL) */
-int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* glist_entries);
-/* rt_intersect through the BVH path with each ray's origin region: region[i] = the
- * surface triangle (rt_scene index) a bounce ray leaves, its grazing list applies while
- * the origin is within that triangle's region box; < 0 = unknown (every triangle's test).
- * region may be NULL (all unknown).  Host arrays. */
-int rt_intersect_regions(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir,
-                         const int32_t* region, int n, float t_scale, int hit_rule, float* out_t,
-                         int32_t* out_hit);
+/* nodes of the triangle BVH, its depth, nodes of the plane-space BVH (out pointers may
+ * be NULL; zeros when the scene has no BVH) */
+int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* plane_nodes);
 /* Host only (no GPU): build the BVH of n triangles (n x 9 vertices, the rt_scene_create
- * order) and check its invariants (every triangle in one leaf, boxes nested and holding
- * their triangles, grazing lists sorted and listing their own triangle).  stats
- * (optional, 4 entries): nodes, depth, grazing-list entries, leaves.  RT_E_INTERNAL with
+ * order) and check its invariants (every triangle in one leaf of each tree, boxes nested
+ * and holding their triangles, planes inside their plane-space leaves).  stats
+ * (optional, 4 entries): nodes, depth, plane-space nodes, leaves.  RT_E_INTERNAL with
  * rt_last_error() naming the first violation. */
 int rt_bvh_check(const float* tri_v, int n, int64_t* stats);
 

@@ -69,25 +69,15 @@ struct rt_scene {
     std::vector<float> albedo;   // n_surf x 3
     std::vector<float> emission; // n_light x 3
     // exact BVH path (rt_bvh.cpp): built for scenes above RT_BVH_AUTO_MIN triangles or on
-    // request (rt_scene_set_accel); camera grazing lists cached per camera position (kept
-    // until the scene is destroyed: a launch in flight may still read an older one)
+    // request (rt_scene_set_accel)
     int accel = RT_ACCEL_AUTO;
     bool has_bvh = false;
     rt::BvhHost bvh;
-    float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, region
-    float* d_graze_full = nullptr;
+    float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, nnodes
     float2* d_gcoef = nullptr;
-    float4* d_nnodes = nullptr;
-    int32_t* d_nleaf = nullptr;
-    int32_t* d_gstart = nullptr;
-    int2* d_glist = nullptr;
-    struct CamList {
-        float x, y, z;
-        int4* ptr;
-        int n;
-        float lam;
-    };
-    mutable std::vector<CamList> cams;
+    float4* d_nleaf = nullptr;
+    float4* d_unodes = nullptr;
+    float4* d_uleaf = nullptr;
 };
 
 namespace {
@@ -99,31 +89,20 @@ int scene_build_bvh(rt_scene* sc) {
         return RT_E_HIP;
     if (!rt::bvh_build(isect.data(), sc->dev.n_tri, &sc->bvh)) return RT_E_UNSUPPORTED;
     const rt::BvhHost& b = sc->bvh;
-    const std::vector<float4>* arr[4] = {&b.nodes, &b.tris, &b.graze, &b.region};
     hipError_t e = hipSuccess;
-    for (int k = 0; k < 4 && e == hipSuccess; ++k) {
-        e = hipMalloc(&sc->d_bvh[k], sizeof(float4) * arr[k]->size());
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->d_bvh[k], arr[k]->data(), sizeof(float4) * arr[k]->size(), hipMemcpyHostToDevice);
-    }
-    if (e == hipSuccess) e = hipMalloc(&sc->d_graze_full, sizeof(float) * b.graze_full.size());
-    if (e == hipSuccess)
-        e = hipMemcpy(sc->d_graze_full, b.graze_full.data(), sizeof(float) * b.graze_full.size(),
-                      hipMemcpyHostToDevice);
-    auto up = [&](auto** dst, const auto& v) {
+    auto put = [&](auto** dst, const auto& v) {
         if (e != hipSuccess) return;
         e = hipMalloc(dst, sizeof(v[0]) * std::max<size_t>(1, v.size()));
         if (e == hipSuccess && !v.empty()) e = hipMemcpy(*dst, v.data(), sizeof(v[0]) * v.size(), hipMemcpyHostToDevice);
     };
-    up(&sc->d_gcoef, b.gcoef);
-    up(&sc->d_nnodes, b.nnodes);
-    up(&sc->d_nleaf, b.nleaf);
-    if (e == hipSuccess) e = hipMalloc(&sc->d_gstart, sizeof(int32_t) * b.gstart.size());
-    if (e == hipSuccess)
-        e = hipMemcpy(sc->d_gstart, b.gstart.data(), sizeof(int32_t) * b.gstart.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMalloc(&sc->d_glist, sizeof(int2) * std::max<size_t>(1, b.glist.size()));
-    if (e == hipSuccess && !b.glist.empty())
-        e = hipMemcpy(sc->d_glist, b.glist.data(), sizeof(int2) * b.glist.size(), hipMemcpyHostToDevice);
+    put(&sc->d_bvh[0], b.nodes);
+    put(&sc->d_bvh[1], b.tris);
+    put(&sc->d_bvh[2], b.graze);
+    put(&sc->d_bvh[3], b.nnodes);
+    put(&sc->d_gcoef, b.gcoef);
+    put(&sc->d_nleaf, b.nleaf);
+    put(&sc->d_unodes, b.unodes);
+    put(&sc->d_uleaf, b.uleaf);
     if (e != hipSuccess) return RT_E_HIP;
     sc->has_bvh = true;
     return RT_OK;
@@ -134,21 +113,14 @@ void scene_free_bvh(rt_scene* sc) {
         if (p) (void)hipFree(p);
         p = nullptr;
     }
-    if (sc->d_gstart) (void)hipFree(sc->d_gstart);
-    if (sc->d_graze_full) (void)hipFree(sc->d_graze_full);
-    sc->d_graze_full = nullptr;
     if (sc->d_gcoef) (void)hipFree(sc->d_gcoef);
-    if (sc->d_nnodes) (void)hipFree(sc->d_nnodes);
     if (sc->d_nleaf) (void)hipFree(sc->d_nleaf);
+    if (sc->d_unodes) (void)hipFree(sc->d_unodes);
+    if (sc->d_uleaf) (void)hipFree(sc->d_uleaf);
     sc->d_gcoef = nullptr;
-    sc->d_nnodes = nullptr;
     sc->d_nleaf = nullptr;
-    if (sc->d_glist) (void)hipFree(sc->d_glist);
-    sc->d_gstart = nullptr;
-    sc->d_glist = nullptr;
-    for (auto& c : sc->cams)
-        if (c.ptr) (void)hipFree(c.ptr);
-    sc->cams.clear();
+    sc->d_unodes = nullptr;
+    sc->d_uleaf = nullptr;
     sc->has_bvh = false;
 }
 
@@ -158,44 +130,20 @@ bool scene_uses_bvh(const rt_scene* sc) {
     return sc->accel == RT_ACCEL_AUTO && sc->dev.n_tri > RT_BVH_AUTO_MIN;
 }
 
-// the device view of the scene for a launch from a camera at cam (BVH fields set when
-// the BVH path is on; the camera's grazing list built and cached on first use)
-rt::DeviceScene launch_scene(const rt_scene* sc, const float* cam) {
+// the device view of the scene for a launch (BVH fields set when the BVH path is on)
+rt::DeviceScene launch_scene(const rt_scene* sc) {
     rt::DeviceScene d = sc->dev;
     if (!scene_uses_bvh(sc)) return d;
     d.bvh_nodes = sc->d_bvh[0];
     d.bvh_tris = sc->d_bvh[1];
     d.bvh_graze = sc->d_bvh[2];
-    d.bvh_graze_full = sc->d_graze_full;
+    d.bvh_nnodes = sc->d_bvh[3];
     d.bvh_gcoef = sc->d_gcoef;
-    d.bvh_nnodes = sc->d_nnodes;
     d.bvh_nleaf = sc->d_nleaf;
-    d.bvh_region = sc->d_bvh[3];
-    d.bvh_gstart = sc->d_gstart;
-    d.bvh_glist = sc->d_glist;
+    d.bvh_unodes = sc->d_unodes;
+    d.bvh_uleaf = sc->d_uleaf;
     d.bvh_sig_a = sc->bvh.sig_a;
     d.bvh_sig_b = sc->bvh.sig_b;
-    d.bvh_lam_max = sc->bvh.lam_max;
-    if (cam == nullptr) return d;
-    for (const auto& c : sc->cams)
-        if (c.x == cam[0] && c.y == cam[1] && c.z == cam[2]) {
-            d.bvh_cam_glist = c.ptr;
-            d.bvh_cam_n = c.n;
-            d.bvh_cam_lam = c.lam;
-            return d;
-        }
-    std::vector<int4> list;
-    const float lam = rt::bvh_camera_list(sc->bvh, sc->dev.n_tri, cam[0], cam[1], cam[2], &list);
-    rt_scene::CamList c{cam[0], cam[1], cam[2], nullptr, (int)list.size(), lam};
-    if (hipMalloc(&c.ptr, sizeof(int4) * std::max<size_t>(1, list.size())) != hipSuccess) return d;
-    if (!list.empty() && hipMemcpy(c.ptr, list.data(), sizeof(int4) * list.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(c.ptr);
-        return d;  // no camera list: camera rays take the full grazing scan (lam 0)
-    }
-    sc->cams.push_back(c);
-    d.bvh_cam_glist = c.ptr;
-    d.bvh_cam_n = c.n;
-    d.bvh_cam_lam = c.lam;
     return d;
 }
 }  // namespace
@@ -316,7 +264,7 @@ int check_params(const rt_params* p) {
 rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p) {
     rt::RenderLaunch a;
     memset(&a, 0, sizeof(a));
-    a.scene = launch_scene(scene, cam ? cam->pos : nullptr);
+    a.scene = launch_scene(scene);
     a.width = p->width;
     a.height = p->height;
     a.spp = p->spp;
@@ -768,58 +716,50 @@ int rt_bvh_check(const float* tri_v, int n, int64_t* stats) {
         }
         stats[0] = h.n_nodes;
         stats[1] = h.depth;
-        stats[2] = (int64_t)h.glist.size();
+        stats[2] = (int64_t)(h.nnodes.size() / 4);
         stats[3] = leaves;
     }
     if (!err.empty()) return fail(RT_E_INTERNAL, "BVH invariant: %s", err.c_str());
     return RT_OK;
 }
 
-int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* glist_entries) {
+int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* plane_nodes) {
     if (!scene) return fail(RT_E_INVALID, "scene is NULL");
     if (n_nodes) *n_nodes = scene->has_bvh ? scene->bvh.n_nodes : 0;
     if (depth) *depth = scene->has_bvh ? scene->bvh.depth : 0;
-    if (glist_entries) *glist_entries = scene->has_bvh ? (int64_t)scene->bvh.glist.size() : 0;
+    if (plane_nodes) *plane_nodes = scene->has_bvh ? (int64_t)(scene->bvh.nnodes.size() / 4) : 0;
     return RT_OK;
 }
 
-int rt_intersect_regions(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir,
-                         const int32_t* region, int n, float t_scale, int hit_rule, float* out_t,
-                         int32_t* out_hit) {
-    if (!ctx || !scene) return fail(RT_E_INVALID, "ctx/scene is NULL");
-    if (n < 0) return fail(RT_E_INVALID, "n < 0");
-    if (n == 0) return RT_OK;
-    if (!orig || !dir || !out_t || !out_hit) return fail(RT_E_INVALID, "NULL buffer");
-    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
+// RT_ISECT_BVH of rt_intersect_method: the BVH path whatever the scene's mode
+static int intersect_bvh_host(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
+                              float t_scale, int hit_rule, float* out_t, int32_t* out_hit) {
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
     rc = scene_build_bvh(const_cast<rt_scene*>(scene));
     if (rc != RT_OK) return fail(rc, "BVH build failed");
-    // the BVH fields whatever the scene's mode
-    const int saved = scene->accel;
-    const_cast<rt_scene*>(scene)->accel = RT_ACCEL_BVH;
-    const rt::DeviceScene ds = launch_scene(scene, nullptr);
-    const_cast<rt_scene*>(scene)->accel = saved;
+    rt_scene* sc = const_cast<rt_scene*>(scene);
+    const int saved = sc->accel;
+    sc->accel = RT_ACCEL_BVH;
+    const rt::DeviceScene ds = launch_scene(sc);
+    sc->accel = saved;
     float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
-    int32_t *d_h = nullptr, *d_r = nullptr;
+    int32_t* d_h = nullptr;
     const size_t b3 = sizeof(float) * 3 * (size_t)n;
     hipError_t e = hipMalloc(&d_o, b3);
     if (e == hipSuccess) e = hipMalloc(&d_d, b3);
     if (e == hipSuccess) e = hipMalloc(&d_t, sizeof(float) * (size_t)n);
     if (e == hipSuccess) e = hipMalloc(&d_h, sizeof(int32_t) * (size_t)n);
-    if (e == hipSuccess && region) e = hipMalloc(&d_r, sizeof(int32_t) * (size_t)n);
     if (e == hipSuccess) e = hipMemcpy(d_o, orig, b3, hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(d_d, dir, b3, hipMemcpyHostToDevice);
-    if (e == hipSuccess && region) e = hipMemcpy(d_r, region, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = rt::launch_intersect_bvh(ds, d_o, d_d, d_r, n, t_scale, hit_rule, d_t, d_h, 0);
+    if (e == hipSuccess) e = rt::launch_intersect_bvh(ds, d_o, d_d, n, t_scale, hit_rule, d_t, d_h, 0);
     if (e == hipSuccess) e = hipMemcpy(out_t, d_t, sizeof(float) * (size_t)n, hipMemcpyDeviceToHost);
     if (e == hipSuccess) e = hipMemcpy(out_hit, d_h, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
     (void)hipFree(d_o);
     (void)hipFree(d_d);
     (void)hipFree(d_t);
     (void)hipFree(d_h);
-    if (d_r) (void)hipFree(d_r);
-    if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect_regions: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return fail(RT_E_HIP, "rt_intersect_method(BVH): %s", hipGetErrorString(e));
     return RT_OK;
 }
 
@@ -838,8 +778,8 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
     if (scene_uses_bvh(scene)) {  // the BVH path checks each ray's range itself
-        RT_HIP(rt::launch_intersect_bvh(launch_scene(scene, nullptr), d_orig, d_dir, nullptr, n, t_scale, hit_rule,
-                                        d_t, d_hit, (hipStream_t)stream));
+        RT_HIP(rt::launch_intersect_bvh(launch_scene(scene), d_orig, d_dir, n, t_scale, hit_rule, d_t, d_hit,
+                                        (hipStream_t)stream));
         return RT_OK;
     }
     // device rays of unknown range: the single-phase scan (no filter bounds to rely on)
@@ -875,8 +815,7 @@ int rt_intersect(rt_ctx* ctx, const rt_scene* scene, const float* orig, const fl
     const int use_filter = (dmax <= 2.0f) ? rt::filter_usable(scene->dev, omax, 0.0f, 0.0f, t_scale) : 0;
     if (e == hipSuccess) {
         if (scene_uses_bvh(scene))
-            e = rt::launch_intersect_bvh(launch_scene(scene, nullptr), d_o, d_d, nullptr, n, t_scale, hit_rule, d_t,
-                                         d_h, 0);
+            e = rt::launch_intersect_bvh(launch_scene(scene), d_o, d_d, n, t_scale, hit_rule, d_t, d_h, 0);
         else
             e = rt::launch_intersect(scene->dev, d_o, d_d, n, t_scale, hit_rule, use_filter, d_t, d_h, 0);
     }
@@ -900,7 +839,7 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
     if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule");
     if (method == RT_ISECT_BVH) {
         if (out_cand) return fail(RT_E_INVALID, "out_cand needs RT_ISECT_MFMA");
-        return rt_intersect_regions(ctx, scene, orig, dir, nullptr, n, t_scale, hit_rule, out_t, out_hit);
+        return intersect_bvh_host(ctx, scene, orig, dir, n, t_scale, hit_rule, out_t, out_hit);
     }
     if (method != RT_ISECT_SCAN && method != RT_ISECT_FILTER && method != RT_ISECT_MFMA)
         return fail(RT_E_INVALID, "bad method %d", method);

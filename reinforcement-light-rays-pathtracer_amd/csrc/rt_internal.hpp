@@ -63,37 +63,26 @@ constexpr int kMfGroupsPerRound = 8;
 constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
 
 // Exact BVH path for large scenes (rt_bvh.cpp, rt_trace.hpp closest_hit_bvh).
-//   nodes: 2 float4 per node {lo.xyz, link}, {hi.xyz, count} (int bits in w): count > 0 a
-//          leaf of tris [link, link + count), else children link, link + 1
-//   tris:  the kIsectF4 records in leaf order, [1].w = the original index (int bits)
-//   graze: per triangle {N (float), threshold of |d.N| for origins within the scene box};
-//          graze_full: the threshold for any origin within obound (the full scan)
-//   region: per triangle the box (2 float4) a bounce origin from it lies in, lo.w = the
-//           window up to which its list is complete;
-//   gstart/glist: per region, the triangles that can be grazed from it {index,
-//           lambda_crit}, by lambda_crit (the window from which each can matter); the
-//           camera list (per launch) {index, threshold, lambda_crit, 0}
+//   nodes:  2 float4 per node {lo.xyz, link}, {hi.xyz, count} (int bits in w): count > 0 a
+//           leaf of tris [link, link + count), else children link, link + 1
+//   tris:   the kIsectF4 records in leaf order, [1].w = the original index (int bits)
+//   graze:  per triangle {N (float), -}; gcoef: {alpha, beta} of its grazing threshold
+//           alpha B + beta (B >= the ray's max |o_i|)
+//   nnodes: the plane-space BVH, 4 float4 per node {centre n, alpha'}, {half extents,
+//           link}, {w_lo, w_hi, beta', count}, {p_a', p_b', 0, 0}; nleaf: its leaf
+//           records, 2 float4 per triangle {N~, alpha}, {beta, index, 0, 0}
+//   unodes / uleaf: the same over the normals alone (rays without a window)
 constexpr int kBvhK = 4;          // regular pairs: |A| >= K EW (barycentrics >= -1/K)
-constexpr int kBvhListMax = 4096;  // grazing-list entries per origin region
 constexpr int kBvhMaxDepth = 24;  // traversal stack entries per lane (tree depth < 24)
 constexpr int kBvhCand = 4;       // rule-0 candidates kept per ray (overflow: exact scan)
 struct BvhHost {
-    std::vector<float4> nodes, tris, graze, region;
-    std::vector<float> graze_full;
-    std::vector<float2> gcoef;   // per triangle: the full-test threshold alpha B + beta
-    std::vector<float4> nnodes;  // normal-space BVH, 3 float4 per node
-    std::vector<int32_t> nleaf;  // its leaves' triangles
-    std::vector<int32_t> gstart;
-    std::vector<int2> glist;
-    std::vector<double> ti_cache;  // per triangle: N, w0, |N|, M, n1 + n2, vmax (camera lists)
+    std::vector<float4> nodes, tris, graze, nnodes, nleaf, unodes, uleaf;
+    std::vector<float2> gcoef;
     int n_nodes = 0, depth = 0;
-    float sig_a = 0.f, sig_b = 0.f, lam_max = 0.f;
-    double B_s = 0.0, obound = 0.0;
+    float sig_a = 0.f, sig_b = 0.f;
 };
 bool bvh_build(const float4* isect, int n, BvhHost* out);
 std::string bvh_check(const float4* isect, int n, const BvhHost& h);
-// returns lambda_max of the list (the camera's window bound)
-float bvh_camera_list(const BvhHost& h, int n, float cx, float cy, float cz, std::vector<int4>* out);
 
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
@@ -105,21 +94,16 @@ struct DeviceScene {
     float origin_bound = 0.0f; // |o_i| bound the filter records were built for
     int32_t* code_cpu = nullptr;  // n_tri packed hit codes under hit rule CPU
     int32_t* code_gpu = nullptr;  // ... under hit rule GPU
-    // BVH path (nullptr: none); cam_glist is set per launch (bvh_camera_list)
+    // BVH path (nullptr: none)
     const float4* bvh_nodes = nullptr;
     const float4* bvh_tris = nullptr;
     const float4* bvh_graze = nullptr;
-    const float* bvh_graze_full = nullptr;
     const float2* bvh_gcoef = nullptr;
     const float4* bvh_nnodes = nullptr;
-    const int32_t* bvh_nleaf = nullptr;
-    const float4* bvh_region = nullptr;
-    const int32_t* bvh_gstart = nullptr;
-    const int2* bvh_glist = nullptr;
-    const int4* bvh_cam_glist = nullptr;
-    int bvh_cam_n = 0;
-    float bvh_cam_lam = 0.0f;  // lambda_max of the camera list
-    float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f, bvh_lam_max = 0.0f;
+    const float4* bvh_nleaf = nullptr;
+    const float4* bvh_unodes = nullptr;
+    const float4* bvh_uleaf = nullptr;
+    float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f;
     int n_surf = 0;
     int n_tri = 0;
 };
@@ -344,10 +328,9 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float* dir, int n,
                             float t_scale, int hit_rule, int use_filter, float* out_t,
                             int32_t* out_hit, hipStream_t stream);
-// the exact BVH path on caller rays; region: optional origin triangle per ray (< 0: unknown)
-hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, const int32_t* region,
-                                int n, float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
-                                hipStream_t stream);
+// the exact BVH path on caller rays
+hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
+                                int hit_rule, float* out_t, int32_t* out_hit, hipStream_t stream);
 // the matrix-core filter (closest_hit_mf) on caller rays; cand: optional candidates per ray
 hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
                                int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream);

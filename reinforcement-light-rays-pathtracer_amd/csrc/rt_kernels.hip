@@ -72,22 +72,18 @@ __global__ __launch_bounds__(256) void k_intersect_mf(const DeviceScene s, const
     if (cand != nullptr) cand[r] = nc;
 }
 
-// The exact BVH path on caller rays (large scenes): region[r] >= 0 the surface triangle
-// the ray leaves (its grazing list), otherwise (or region == nullptr) every triangle's
-// grazing test.
+// The exact BVH path on caller rays (large scenes).
 template <int RULE>
 __global__ __launch_bounds__(256) void k_intersect_bvh(const DeviceScene s, const int32_t* __restrict__ code,
                                                        const float* __restrict__ orig, const float* __restrict__ dir,
-                                                       const int32_t* __restrict__ region, int n, float t_scale,
-                                                       float* __restrict__ out_t, int32_t* __restrict__ out_hit) {
+                                                       int n, float t_scale, float* __restrict__ out_t,
+                                                       int32_t* __restrict__ out_hit) {
     __shared__ int stk[kBvhMaxDepth * 256];
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const f3 o = make3(orig[3 * r + 0], orig[3 * r + 1], orig[3 * r + 2]);
     const f3 d = make3(dir[3 * r + 0], dir[3 * r + 1], dir[3 * r + 2]);
-    int reg = (region != nullptr) ? region[r] : -2;
-    if (reg < 0 || reg >= s.n_tri) reg = -2;
-    const Hit h = closest_hit_bvh<RULE>(s, o, d, t_scale, reg, stk + threadIdx.x);
+    const Hit h = closest_hit_bvh<RULE>(s, o, d, t_scale, stk + threadIdx.x);
     out_t[r] = (h.tri >= 0) ? h.t : __builtin_inff();
     out_hit[r] = (h.tri >= 0) ? code[h.tri] : -1;
 }
@@ -107,7 +103,7 @@ __global__ __launch_bounds__(256) void k_intersect_bvh(const DeviceScene s, cons
 // chunk sum of the fixed assignment, so the image is bit-identical.
 //
 // BVH: large scenes cast through closest_hit_bvh (the exact BVH path: same hits as the
-// scan), with the lane's origin region: the camera, or the surface a bounce leaves.
+// scan).
 template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1
@@ -115,7 +111,6 @@ template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH>
 __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch a) {
     extern __shared__ float s_val[];  // STEAL: [pixel of the workgroup][spp][3]
     __shared__ int s_stk[BVH ? kBvhMaxDepth * 256 : 1];
-    int reg = -1;  // BVH: origin region of the current ray (-1: the camera)
     // workgroup -> (16x16 block, part); lane -> (pixel of the block, sample chunk)
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -158,7 +153,7 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
         if (__ballot(active) == 0ull) break;
         if (!active) continue;
 
-        const Hit h = BVH ? closest_hit_bvh<RULE>(a.scene, o, d, a.t_scale, reg, s_stk + threadIdx.x)
+        const Hit h = BVH ? closest_hit_bvh<RULE>(a.scene, o, d, a.t_scale, s_stk + threadIdx.x)
                           : closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
         ++n_casts;
 
@@ -241,7 +236,6 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
             }
             o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
             d = normalize(sd);
-            reg = h.tri;
             ++depth;
             if (PRESET == 1 && depth == a.max_bounces) terminal = true;  // loop exhausted -> 0
         }
@@ -264,7 +258,6 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
                 ++s;
             }
             depth = 0;
-            reg = -1;
             tp = make3(1.0f, 1.0f, 1.0f);
             o = make3(a.cam_x, a.cam_y, a.cam_z);
             if (s < s_end) {
@@ -827,18 +820,17 @@ hipError_t launch_intersect(const DeviceScene& s, const float* orig, const float
     return hipGetLastError();
 }
 
-hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, const int32_t* region,
-                                int n, float t_scale, int hit_rule, float* out_t, int32_t* out_hit,
-                                hipStream_t stream) {
+hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
+                                int hit_rule, float* out_t, int32_t* out_hit, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     if (s.bvh_nodes == nullptr) return hipErrorInvalidValue;
     const dim3 block(256), grid((unsigned)((n + 255) / 256));
     if (hit_rule == 0)
-        hipLaunchKernelGGL(k_intersect_bvh<0>, grid, block, 0, stream, s, s.code_cpu, orig, dir, region, n, t_scale,
-                           out_t, out_hit);
+        hipLaunchKernelGGL(k_intersect_bvh<0>, grid, block, 0, stream, s, s.code_cpu, orig, dir, n, t_scale, out_t,
+                           out_hit);
     else
-        hipLaunchKernelGGL(k_intersect_bvh<1>, grid, block, 0, stream, s, s.code_gpu, orig, dir, region, n, t_scale,
-                           out_t, out_hit);
+        hipLaunchKernelGGL(k_intersect_bvh<1>, grid, block, 0, stream, s, s.code_gpu, orig, dir, n, t_scale, out_t,
+                           out_hit);
     return hipGetLastError();
 }
 

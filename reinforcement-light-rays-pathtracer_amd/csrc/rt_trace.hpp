@@ -788,10 +788,9 @@ __device__ __forceinline__ float bvh_lam_hi(const BvhCand& c, const DeviceScene&
     return ((cut * t_scale + s.bvh_sig_a) / (1.0f - s.bvh_sig_b)) * 1.0000002f;
 }
 
-// region: >= 0 the surface triangle a bounce ray leaves, -1 the launch's camera,
-// -2 unknown (every triangle's grazing test).  stk: the lane's LDS stack, stride 256.
+// stk: the lane's LDS stack, stride 256.
 template <int RULE>
-__device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, int region, int* stk) {
+__device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, int* stk) {
     const float nDx = -(d.x * t_scale), nDy = -(d.y * t_scale), nDz = -(d.z * t_scale);
     const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
@@ -856,7 +855,9 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         if (sp == 0) break;
         node = stk[(--sp) * 256];
     }
-    // grazing pairs: the region's list, or every triangle
+    // grazing pairs: the plane-space query (rt_bvh.cpp) — triangles whose normal lies
+    // in the band |d.n| <= alpha' B + beta' and whose plane passes within p(B) + s lambda
+    // of the origin (lambda: the window found so far; unbounded for a ray that hit nothing)
     const float4* __restrict__ gz = s.bvh_graze;
 #ifdef RT_BVH_TIMING_TRAVERSAL_ONLY
     {  // timing-only build (wrong hits): the traversal alone
@@ -866,88 +867,45 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         return hh;
     }
 #endif
-    bool full = region < -1;
-    if (region >= 0) {
-        const float4 L = s.bvh_region[2 * region], H = s.bvh_region[2 * region + 1];
-        full = !(o.x >= L.x && o.x <= H.x && o.y >= L.y && o.y <= H.y && o.z >= L.z && o.z <= H.z);
-    }
-    if (!full) {
-        // the list is complete up to window lam_k (entries by lambda_crit): a ray with a
-        // wider window scans every triangle; otherwise the entries up to its window
+    {
         const float cut = (RULE == 0) ? c.cut : c.bt;
         const float lam_cut = cut * t_scale * 1.0000002f;
-        const float lam_k = (region >= 0) ? s.bvh_region[2 * region].w : s.bvh_cam_lam;
-        full = !(lam_cut <= lam_k);
-        if (!full && region >= 0) {
-            // four entries per step, all loads in flight before the tests (the list is
-            // sorted: an entry past the window ends it; past-the-end reads stay inside
-            // the padded array)
-            const int2* gl = s.bvh_glist + s.bvh_gstart[region];
-            const int gn = s.bvh_gstart[region + 1] - s.bvh_gstart[region];
-            for (int k = 0; k < gn; k += 4) {
-                const int4 e01 = *reinterpret_cast<const int4*>(gl + k);
-                const int4 e23 = *reinterpret_cast<const int4*>(gl + k + 2);
-                const int idx[4] = {e01.x, e01.z, e23.x, e23.z};
-                const float lc[4] = {__int_as_float(e01.y), __int_as_float(e01.w), __int_as_float(e23.y),
-                                     __int_as_float(e23.w)};
-                float4 g[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) g[j] = gz[(k + j < gn) ? idx[j] : 0];
-                bool stop = false;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const bool in = (k + j < gn) && !(lc[j] > lam_cut);
-                    stop = stop || !in;
-                    const float a = fmaf(d.z, g[j].z, fmaf(d.y, g[j].y, d.x * g[j].x));
-                    if (!stop && fabsf(a) <= g[j].w) {
-                        const float t = exact_tv<RULE>(s.isect, idx[j], o, nDx, nDy, nDz);
-                        if (t <= FLT_MAX) bvh_insert<RULE>(c, t, idx[j]);
-                    }
-                }
-                if (stop) break;
-            }
-        } else if (!full) {
-            const int4* gl = s.bvh_cam_glist;
-            for (int k = 0; k < s.bvh_cam_n; ++k) {
-                const int4 e = gl[k];
-                if (__int_as_float(e.z) > lam_cut) break;
-                const float4 g = gz[e.x];
-                const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-                if (fabsf(a) <= __int_as_float(e.y)) {
-                    const float t = exact_tv<RULE>(s.isect, e.x, o, nDx, nDy, nDz);
-                    if (t <= FLT_MAX) bvh_insert<RULE>(c, t, e.x);
-                }
-            }
-        }
-    }
-#ifdef RT_BVH_TIMING_NO_FULL
-    full = false;  // timing-only build (wrong hits): no normal-space query
-#endif
-    if (full) {
-        // every triangle whose |d.N| is within its threshold at B = max |o_i|: a slab
-        // query |d.n| <= alpha' B + beta' over the normal-space BVH (rt_bvh.cpp)
+        const bool bounded = lam_cut <= 3.0e38f;
         const float B = om * 1.000001f;
-        const float4* __restrict__ nn = s.bvh_nnodes;
+#ifdef RT_BVH_TIMING_SKIP_UNBOUNDED
+        if (!bounded) goto resolve;  // timing-only build (wrong hits)
+#endif
+        const float4* __restrict__ nn = bounded ? s.bvh_nnodes : s.bvh_unodes;
+        const float4* __restrict__ lf = bounded ? s.bvh_nleaf : s.bvh_uleaf;
         const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+        const float bx = fabsf(o.x), by = fabsf(o.y), bz = fabsf(o.z);
         int nsp = 0, nd = 0;
         for (;;) {
-            const float4 r0 = nn[3 * nd], r1 = nn[3 * nd + 1], r2 = nn[3 * nd + 2];
+            const float4 r0 = nn[4 * nd], r1 = nn[4 * nd + 1], r2 = nn[4 * nd + 2];
             const float band = fmaf(r0.w, B, r2.z) * 1.000001f;
             const float dc = fmaf(d.z, r0.z, fmaf(d.y, r0.y, d.x * r0.x));
             const float rr = fmaf(az, r1.z, fmaf(ay, r1.y, ax * r1.x));
-            const int link = __float_as_int(r1.w), cnt = __float_as_int(r2.w);
-            if (!(dc - rr > band || dc + rr < -band)) {
+            bool ok = !(dc - rr > band || dc + rr < -band);
+            if (ok && bounded) {
+                const float4 r3 = nn[4 * nd + 3];
+                const float r = fmaf(band, lam_cut, fmaf(r3.x, B, r3.y)) * 1.00001f +
+                                1e-6f * (1.0f + B + fabsf(r2.x) + fabsf(r2.y));
+                const float oc = fmaf(o.z, r0.z, fmaf(o.y, r0.y, o.x * r0.x));
+                const float ro = fmaf(bz, r1.z, fmaf(by, r1.y, bx * r1.x));
+                ok = !(oc - ro - r > r2.y || oc + ro + r < r2.x);
+            }
+            if (ok) {
+                const int link = __float_as_int(r1.w), cnt = __float_as_int(r2.w);
                 if (cnt == 0) {
                     stk[(nsp++) * 256] = link + 1;
                     nd = link;
                     continue;
                 }
                 for (int k = link; k < link + cnt; ++k) {
-                    const int i = s.bvh_nleaf[k];
-                    const float4 g = gz[i];
-                    const float2 q = s.bvh_gcoef[i];
+                    const float4 g = lf[2 * k], q = lf[2 * k + 1];
                     const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-                    if (fabsf(a) <= fmaf(q.x, B, q.y) * 1.000001f) {
+                    if (fabsf(a) <= fmaf(g.w, B, q.x) * 1.000001f) {
+                        const int i = __float_as_int(q.y);
                         const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
                         if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
                     }
@@ -957,6 +915,9 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
             nd = stk[(--nsp) * 256];
         }
     }
+#ifdef RT_BVH_TIMING_SKIP_UNBOUNDED
+resolve:
+#endif
     Hit h;
     if (RULE == 1) {
         h.t = c.bt;

@@ -9,7 +9,7 @@ from ._lib import (LIB_PATH, RT_HIT_NONE, RT_HIT_RULE_CPU, RT_HIT_RULE_GPU, RT_H
                    RT_SAMPLER_UNIFORM, RtCamera, RtError, RtParams, lib)
 from .api import (CAMERAS, OBJ_KINDS, Context, Geometry, Scene, camera, cornell_geometry,
                   default_params, filter_records, intersect, intersect_device, intersect_method, ISECT_SCAN,
-                  ISECT_FILTER, ISECT_MFMA, ISECT_BVH, ACCEL_AUTO, ACCEL_SCAN, ACCEL_BVH, intersect_regions,
+                  ISECT_FILTER, ISECT_MFMA, ISECT_BVH, ACCEL_AUTO, ACCEL_SCAN, ACCEL_BVH,
                   obj_geometry, pack_argb,
                   rect_candidates, render, render_tiles_device, save_bmp, save_png)
 from . import dist, dqn, metrics, sarsa, tiles

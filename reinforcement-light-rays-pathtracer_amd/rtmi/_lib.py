@@ -49,7 +49,7 @@ EXPORTS = (
     "rt_dqn_save_selected",
     "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
     "rt_dqn_td_targets_device",
-    "rt_scene_set_accel", "rt_scene_accel_info", "rt_intersect_regions", "rt_bvh_check",
+    "rt_scene_set_accel", "rt_scene_accel_info", "rt_bvh_check",
 )
 
 
@@ -102,7 +102,6 @@ def _declare(lib):
         "rt_intersect_method": (i, [_P, _P, _FP, _FP, i, f, i, i, _FP, _IP, _IP]),
         "rt_scene_set_accel": (i, [_P, i]),
         "rt_scene_accel_info": (i, [_P, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(ctypes.c_int64)]),
-        "rt_intersect_regions": (i, [_P, _P, _FP, _FP, _IP, i, f, i, _FP, _IP]),
         "rt_bvh_check": (i, [_FP, i, ctypes.POINTER(ctypes.c_int64)]),
         "rt_render": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
                           _FP, _U64P]),

@@ -174,7 +174,7 @@ class Scene:
     def accel_info(self) -> dict:
         nodes, depth, gl = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int64(0)
         check(lib().rt_scene_accel_info(self._h, ctypes.byref(nodes), ctypes.byref(depth), ctypes.byref(gl)))
-        return {"nodes": nodes.value, "depth": depth.value, "glist_entries": gl.value}
+        return {"nodes": nodes.value, "depth": depth.value, "plane_nodes": gl.value}
 
     def normals(self) -> np.ndarray:
         out = np.zeros((self.geom.n_tri, 3), np.float32)
@@ -207,20 +207,6 @@ def intersect(ctx: Context, scene: Scene, orig: np.ndarray, direction: np.ndarra
 
 ISECT_SCAN, ISECT_FILTER, ISECT_MFMA, ISECT_BVH = 0, 1, 2, 3
 ACCEL_AUTO, ACCEL_SCAN, ACCEL_BVH = 0, 1, 2
-
-
-def intersect_regions(ctx: Context, scene: Scene, orig: np.ndarray, direction: np.ndarray,
-                      region: Optional[np.ndarray], t_scale: float, hit_rule: int):
-    """rt_intersect_regions: the BVH path with each ray's origin triangle (< 0: unknown)."""
-    o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
-    d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
-    n = o.shape[0]
-    r = None if region is None else np.ascontiguousarray(region, np.int32)
-    t = np.zeros(n, np.float32)
-    h = np.zeros(n, np.int32)
-    check(lib().rt_intersect_regions(ctx.handle, scene.handle, _fp(o), _fp(d), _ip(r) if r is not None else None,
-                                     n, float(t_scale), hit_rule, _fp(t), _ip(h)))
-    return t, h
 
 
 def intersect_method(ctx: Context, scene: Scene, orig: np.ndarray, direction: np.ndarray, t_scale: float,

@@ -5,9 +5,8 @@ GPU/rays/ray.cu:16-141); Models/bunny.obj (4,968 triangles) and Medieval_House.o
 make that scan the whole cost.  The BVH path must return the scan's hit bit for bit under
 both hit rules, so it is checked against the exact scan (RT_ISECT_SCAN, itself bit-exact
 against the CPU restatement in test_gpu_parity.py) and against the restatement directly:
-random rays, rays from surface points with and without their origin region, rays aimed
-at edges and vertices, rays lying in a triangle's plane (the grazing pairs a box test
-cannot see), and whole renders of the bunny in the Cornell box with both presets.
+random rays, rays from surface points, rays aimed at edges and vertices, rays lying in a
+triangle's plane (the grazing pairs a box test cannot see), and whole renders of the bunny in the Cornell box with both presets.
 """
 import os
 
@@ -41,7 +40,7 @@ def house(rtmi):
 
 def surface_rays(tri, n, seed, hemisphere=False):
     """Origins on random triangles + 1e-5 along the direction (the bounce loop's offset),
-    with the triangle index as the origin region."""
+    and the triangle of each origin."""
     rng = np.random.default_rng(seed)
     t = tri.reshape(-1, 3, 3).astype(np.float32)
     i = rng.integers(0, t.shape[0], n)
@@ -96,6 +95,10 @@ def _scan(rtmi, ctx, sc, o, d, ts, rule):
     return rtmi.intersect_method(ctx, sc, o, d, ts, rule, rtmi.ISECT_SCAN)
 
 
+def _bvh(rtmi, ctx, sc, o, d, ts, rule):
+    return rtmi.intersect_method(ctx, sc, o, d, ts, rule, rtmi.ISECT_BVH)
+
+
 def _same(a, b):
     ta, ha = a
     tb, hb = b
@@ -109,7 +112,7 @@ def test_bvh_built_for_large_scene(rtmi_mod, gpu_ctx, rule):
     with rtmi_mod.Scene(gpu_ctx, g) as sc:
         info = sc.accel_info()
         assert info["nodes"] > g.n_tri // 4 and 0 < info["depth"] < 24
-        assert info["glist_entries"] >= g.n_tri  # every region lists at least itself
+        assert info["plane_nodes"] >= g.n_tri // 4
 
 
 @pytest.mark.parametrize("rule", [0, 1])
@@ -120,12 +123,7 @@ def test_bvh_matches_scan_surface_rays(rtmi_mod, gpu_ctx, rule):
         for seed, hemi in ((1, False), (2, True)):
             o, d, reg = surface_rays(g.all_triangles(), 200_000, seed, hemi)
             ref = _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule)
-            _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, reg, ts, rule), ref)
-            _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o[:50_000], d[:50_000], None, ts, rule),
-                  (ref[0][:50_000], ref[1][:50_000]))
-            # a wrong region: the origin is outside its box, the kernel falls back
-            _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o[:20_000], d[:20_000], (reg[:20_000] + 7) % g.n_tri,
-                                             ts, rule), (ref[0][:20_000], ref[1][:20_000]))
+            _same(_bvh(rtmi_mod, gpu_ctx, sc, o, d, ts, rule), ref)
 
 
 @pytest.mark.parametrize("rule", [0, 1])
@@ -135,17 +133,16 @@ def test_bvh_matches_scan_hard_rays(rtmi_mod, gpu_ctx, rule):
     rng = np.random.default_rng(7)
     with rtmi_mod.Scene(gpu_ctx, g) as sc:
         o, d, reg = edge_rays(g.all_triangles(), 100_000, 3)
-        _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, reg, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
+        _same(_bvh(rtmi_mod, gpu_ctx, sc, o, d, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
         o, d, reg = in_plane_rays(g.all_triangles(), 100_000, 4)
-        _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, reg, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
-        _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, None, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
+        _same(_bvh(rtmi_mod, gpu_ctx, sc, o, d, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
         # random rays inside and outside the box, and rays the BVH must hand to the scan
         o = rng.uniform(-3, 3, (50_000, 3)).astype(np.float32)
         d = _unit(rng.normal(size=(50_000, 3)))
         d[:10] = np.nan
         o[10:20] = 100.0
         d[20:30] = np.array([1.0, 0.0, 0.0], np.float32)
-        _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, None, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
+        _same(_bvh(rtmi_mod, gpu_ctx, sc, o, d, ts, rule), _scan(rtmi_mod, gpu_ctx, sc, o, d, ts, rule))
 
 
 @pytest.mark.parametrize("rule", [0, 1])
@@ -166,7 +163,7 @@ def test_bvh_house_matches_scan(rtmi_mod, gpu_ctx):
         assert sc.accel_info()["nodes"] > 0
         for rule in (0, 1):
             o, d, reg = surface_rays(g.all_triangles(), 50_000, 5 + rule, True)
-            _same(rtmi_mod.intersect_regions(gpu_ctx, sc, o, d, reg, 720.0, rule),
+            _same(_bvh(rtmi_mod, gpu_ctx, sc, o, d, 720.0, rule),
                   _scan(rtmi_mod, gpu_ctx, sc, o, d, 720.0, rule))
 
 

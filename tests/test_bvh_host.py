@@ -1,7 +1,7 @@
 """Host build of the exact BVH path (rt_bvh.cpp) without a GPU: rt_bvh_check builds the
 tree and grazing lists of a scene and checks their invariants (every triangle in one
-leaf, nested boxes holding their triangles, regions holding their triangle, grazing lists
-sorted by critical window and listing their own triangle).  The bit-exactness of the
+leaf of each tree, nested boxes holding their triangles, planes inside their plane-space
+leaves).  The bit-exactness of the
 device path is in test_bvh.py (-m gpu)."""
 import ctypes
 import os
@@ -30,9 +30,9 @@ def test_bvh_host_invariants(rtmi_mod, scene):
     else:
         kind = scene if scene == "complex_light_room" else "generic"
         g = rtmi_mod.obj_geometry(os.path.join(MODELS, f"{scene}.obj"), kind)
-    nodes, depth, glist, leaves = _check(rtmi_mod, g.all_triangles())
+    nodes, depth, pnodes, leaves = _check(rtmi_mod, g.all_triangles())
     assert 0 < depth < 24 and leaves * 4 >= g.n_tri and nodes == 2 * leaves - 1
-    assert glist >= g.n_tri
+    assert pnodes >= g.n_tri // 4
 
 
 def test_bvh_host_degenerate_inputs(rtmi_mod):
