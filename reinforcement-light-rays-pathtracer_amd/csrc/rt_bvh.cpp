@@ -281,7 +281,7 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         memcpy(&h.tris[(size_t)k * 3 + 1].w, &i, 4);  // original index (the record's w is 0)
     }
     // grazing data: the normal as a float (w: the threshold for origins within the scene
-    // box, informational; the kernel uses alpha B + beta, gcoef)
+    // box, informational; the kernel uses grec)
     h.graze.resize((size_t)n);
     for (int i = 0; i < n; ++i) {
         const TriInfo& t = ti[(size_t)i];
@@ -290,128 +290,85 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         g.w = graze_threshold(t, bounds_for(t, B_s));
         h.graze[(size_t)i] = g;
     }
-    // Plane-space index of the grazing pairs.  Triangle i can pass the exact test
+    // Direction-binned index of the grazing pairs.  Triangle i can pass the exact test
     // outside its padded box only when (1) |d.N~_i| <= thr_i(B) = alpha_i B + beta_i
-    // (B >= the ray's max |o_j|; K EW is affine in B): its unit normal n lies in the band
-    // |d.n| <= s_i(B) = (thr_i(B) + 4u dinf M) / |N| around the great circle normal to
-    // d; and (2) for a pass with t below the window lambda: |T| <= lambda (K EW + eA) +
-    // ET, i.e. |n.o - w| <= p_i(B) + s_i(B) lambda (w = n.v0 the plane's offset, p = ET/|N|
-    // affine in B).  A BVH over the points (n, w) (folded to n_z >= 0: both tests are
-    // symmetric) with per-node maxima of the coefficients; a node is visited only if its
-    // box meets both slabs (the second skipped for an unbounded window).
+    // (B >= the ray's max |o_j|; K EW is affine in B): its unit normal n within
+    // s_i(B) = (thr_i(B) + 4u dinf M) / |N| of the great circle normal to d; and (2) for a
+    // pass with t below the window lambda, |T| <= lambda (K EW + eA) + ET: in N units
+    // |N~.o - W| <= (PA B + PB) + thr_i(B) lambda (W = N.v0, PA/PB: ET affine in B plus
+    // the float evaluation's rounding).  The directions are cut into the cells of a cube
+    // map (6 x G x G); cell c lists every triangle with |d_c.n| <= s_i(B_L) + chord_c
+    // (d_c the cell's centre direction, chord_c >= |d - d_c| over the cell: its image is a
+    // spherical quad bounded by great-circle arcs, farthest from d_c at a corner).  Two
+    // list sets: B_L = the scene box (bounce rays) and B_L = obound (camera rays).  The
+    // kernel walks the ray's cell list and applies (1) and (2) exactly per triangle.
     {
         const double dinf = (double)kMfDirBound;
-        std::vector<double> al((size_t)n), be((size_t)n), pa((size_t)n), pb((size_t)n), pt((size_t)n * 4);
-        h.gcoef.resize((size_t)n);
-        double wscale = 1e-30;
+        h.grec.resize((size_t)n * 2);
+        std::vector<double> s_a((size_t)n), s_b((size_t)n), un((size_t)n * 3);
         for (int i = 0; i < n; ++i) {
             const TriInfo& t = ti[(size_t)i];
             const Bounds b0 = bounds_for(t, 0.0);
             const double a = kK * 2.0 * (kC * 2.0 * dinf * (t.n1 + t.n2)) * (1.0 + 1e-9);
-            const double b = (kK * b0.EW + b0.eA + 8.0 * kU * dinf * t.M) * (1.0 + 1e-9);
-            float2 g;
-            g.x = up(a);
-            g.y = up(b);
-            h.gcoef[(size_t)i] = g;
-            al[(size_t)i] = (double)g.x / t.nlen * (1.0 + 1e-6);
-            be[(size_t)i] = ((double)g.y + 8.0 * kU * dinf * t.M) / t.nlen * (1.0 + 1e-6) + 1e-6;
-            // ET(B) = c (B + vmax) M + 2 eps ts_max eA + F
-            pa[(size_t)i] = kC * t.M / t.nlen * (1.0 + 1e-6);
-            pb[(size_t)i] = (kC * t.vmax * t.M + 2.0 * 1e-5 * (double)kFiltMaxTScale * b0.eA + ldexp(1.0, -90)) /
-                                t.nlen * (1.0 + 1e-6) + ldexp(1.0, -40);
-            double nn3[3] = {t.N[0] / t.nlen, t.N[1] / t.nlen, t.N[2] / t.nlen};
-            double w = t.w0 / t.nlen;
-            const bool flip = nn3[2] < 0.0 || (nn3[2] == 0.0 && (nn3[1] < 0.0 || (nn3[1] == 0.0 && nn3[0] < 0.0)));
-            for (int a3 = 0; a3 < 3; ++a3) pt[(size_t)i * 4 + a3] = flip ? -nn3[a3] : nn3[a3];
-            pt[(size_t)i * 4 + 3] = flip ? -w : w;
-            wscale = std::max(wscale, fabs(w));
+            const double bb = (kK * b0.EW + b0.eA + 8.0 * kU * dinf * t.M) * (1.0 + 1e-9);
+            const double n1 = fabs(t.N[0]) + fabs(t.N[1]) + fabs(t.N[2]);
+            const float Wf = (float)t.w0;
+            // ET(B) = c (B + vmax) M + 2 eps ts_max eA + F, plus the rounding of N~.o - W
+            const double PA = (kC * t.M + 8.0 * kU * n1) * (1.0 + 1e-6);
+            const double PB = (kC * t.vmax * t.M + 2.0 * 1e-5 * (double)kFiltMaxTScale * b0.eA + ldexp(1.0, -90) +
+                               8.0 * kU * fabs((double)Wf) + fabs((double)Wf - t.w0)) * (1.0 + 1e-6) + ldexp(1.0, -100);
+            float4 r0, r1;
+            r0.x = h.graze[(size_t)i].x; r0.y = h.graze[(size_t)i].y; r0.z = h.graze[(size_t)i].z; r0.w = up(a);
+            r1.x = up(bb); r1.y = Wf; r1.z = up(PA); r1.w = up(PB);
+            h.grec[(size_t)i * 2] = r0;
+            h.grec[(size_t)i * 2 + 1] = r1;
+            s_a[(size_t)i] = (double)r0.w / t.nlen * (1.0 + 1e-6);
+            s_b[(size_t)i] = ((double)r1.x + 8.0 * kU * dinf * t.M) / t.nlen * (1.0 + 1e-6);
+            for (int k = 0; k < 3; ++k) un[(size_t)i * 3 + k] = t.N[k] / t.nlen;
         }
-        // leaf records, 2 float4 per triangle: {N~, alpha}, {beta, index, 0, 0}
-        auto leaf_rec = [&](int i, std::vector<float4>* out) {
-            const float4 g = h.graze[(size_t)i];
-            float4 a0, a1;
-            a0.x = g.x; a0.y = g.y; a0.z = g.z; a0.w = h.gcoef[(size_t)i].x;
-            a1.x = h.gcoef[(size_t)i].y; memcpy(&a1.y, &i, 4); a1.z = 0.0f; a1.w = 0.0f;
-            out->push_back(a0);
-            out->push_back(a1);
+        const int G = kBvhDirGrid;
+        const int cells = 6 * G * G;
+        auto cell_dir = [&](int f, double u, double v, double* out) {  // face f: axis f/2, sign
+            const int ax = f >> 1;
+            const double sg = (f & 1) ? -1.0 : 1.0;
+            double p[3];
+            p[ax] = sg;
+            p[(ax + 1) % 3] = u;
+            p[(ax + 2) % 3] = v;
+            const double l = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
+            for (int k = 0; k < 3; ++k) out[k] = p[k] / l;
         };
-        // median BVH over the points (dims 4: plane space (n, w); dims 3: normals only)
-        auto build_tree = [&](int dims, int leaf_max, std::vector<float4>* nodes, std::vector<float4>* leaves) {
-            std::vector<int> id((size_t)n);
-            for (int i = 0; i < n; ++i) id[(size_t)i] = i;
-            nodes->clear();
-            leaves->clear();
-            struct Job { int node, b, e; };
-            std::vector<Job> jobs;
-            auto alloc = [&]() {
-                nodes->resize(nodes->size() + 4);
-                return (int)(nodes->size() / 4) - 1;
-            };
-            jobs.push_back({alloc(), 0, n});
-            while (!jobs.empty()) {
-                const Job j = jobs.back();
-                jobs.pop_back();
-                double lo[4] = {DBL_MAX, DBL_MAX, DBL_MAX, DBL_MAX}, hi[4] = {-DBL_MAX, -DBL_MAX, -DBL_MAX, -DBL_MAX};
-                double am = 0.0, bm = 0.0, pam = 0.0, pbm = 0.0;
-                for (int k = j.b; k < j.e; ++k) {
-                    const int i = id[(size_t)k];
-                    for (int a4 = 0; a4 < 4; ++a4) {
-                        lo[a4] = std::min(lo[a4], pt[(size_t)i * 4 + a4]);
-                        hi[a4] = std::max(hi[a4], pt[(size_t)i * 4 + a4]);
+        const double BL[2] = {B_s, obound};
+        for (int set = 0; set < 2; ++set) {
+            std::vector<int32_t>& start = set ? h.dstart_cam : h.dstart;
+            std::vector<int32_t>& list = set ? h.dlist_cam : h.dlist;
+            start.assign((size_t)cells + 1, 0);
+            list.clear();
+            for (int c = 0; c < cells; ++c) {
+                const int f = c / (G * G), iu = (c / G) % G, iv = c % G;
+                const double u0 = -1.0 + 2.0 * iu / G, u1 = -1.0 + 2.0 * (iu + 1) / G;
+                const double v0 = -1.0 + 2.0 * iv / G, v1 = -1.0 + 2.0 * (iv + 1) / G;
+                double dc[3], q[3];
+                cell_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1), dc);
+                double chord = 0.0;
+                const double us[2] = {u0, u1}, vs[2] = {v0, v1};
+                for (int ku = 0; ku < 2; ++ku)
+                    for (int kv = 0; kv < 2; ++kv) {
+                        cell_dir(f, us[ku], vs[kv], q);
+                        chord = std::max(chord, sqrt((q[0] - dc[0]) * (q[0] - dc[0]) + (q[1] - dc[1]) * (q[1] - dc[1]) +
+                                                     (q[2] - dc[2]) * (q[2] - dc[2])));
                     }
-                    am = std::max(am, al[(size_t)i]);
-                    bm = std::max(bm, be[(size_t)i]);
-                    pam = std::max(pam, pa[(size_t)i]);
-                    pbm = std::max(pbm, pb[(size_t)i]);
+                chord = chord * (1.0 + 1e-6) + 1e-6;  // + the kernel's rounding of the cell choice
+                for (int i = 0; i < n; ++i) {
+                    const double* nn3 = &un[(size_t)i * 3];
+                    const double dn = fabs(dc[0] * nn3[0] + dc[1] * nn3[1] + dc[2] * nn3[2]);
+                    // (|d| >= 1 - 2^-10 for the ray's unit-length direction: 0.2% on s)
+                    if (dn <= (s_a[(size_t)i] * BL[set] + s_b[(size_t)i]) * 1.002 + chord) list.push_back(i);
                 }
-                float4 r0, r1, r2, r3;
-                r0.x = (float)(0.5 * (lo[0] + hi[0])); r0.y = (float)(0.5 * (lo[1] + hi[1]));
-                r0.z = (float)(0.5 * (lo[2] + hi[2])); r0.w = up(am);
-                // half extents from the float centre, rounded up, + slack for the float tests
-                r1.x = up(std::max(hi[0] - r0.x, r0.x - lo[0]) + 1e-6);
-                r1.y = up(std::max(hi[1] - r0.y, r0.y - lo[1]) + 1e-6);
-                r1.z = up(std::max(hi[2] - r0.z, r0.z - lo[2]) + 1e-6);
-                r2.x = down(lo[3] - 1e-6 * (1.0 + fabs(lo[3])));
-                r2.y = up(hi[3] + 1e-6 * (1.0 + fabs(hi[3])));
-                r2.z = up(bm);
-                r3.x = up(pam); r3.y = up(pbm); r3.z = 0.0f; r3.w = 0.0f;
-                const int cnt = j.e - j.b;
-                int link, cw;
-                if (cnt <= leaf_max) {
-                    link = (int)(leaves->size() / 2);
-                    for (int k = j.b; k < j.e; ++k) leaf_rec(id[(size_t)k], leaves);
-                    cw = cnt;
-                } else {
-                    int ax = 0;
-                    double ext = -1.0;
-                    for (int a4 = 0; a4 < dims; ++a4) {
-                        const double e = (hi[a4] - lo[a4]) / (a4 == 3 ? wscale : 1.0);
-                        if (e > ext) {
-                            ext = e;
-                            ax = a4;
-                        }
-                    }
-                    const int mid = j.b + cnt / 2;
-                    std::nth_element(id.begin() + j.b, id.begin() + mid, id.begin() + j.e,
-                                     [&](int x, int y) { return pt[(size_t)x * 4 + ax] < pt[(size_t)y * 4 + ax]; });
-                    link = alloc();
-                    alloc();
-                    jobs.push_back({link + 1, mid, j.e});
-                    jobs.push_back({link, j.b, mid});
-                    cw = 0;
-                }
-                memcpy(&r1.w, &link, 4);
-                memcpy(&r2.w, &cw, 4);
-                (*nodes)[(size_t)j.node * 4] = r0;
-                (*nodes)[(size_t)j.node * 4 + 1] = r1;
-                (*nodes)[(size_t)j.node * 4 + 2] = r2;
-                (*nodes)[(size_t)j.node * 4 + 3] = r3;
+                start[(size_t)c + 1] = (int32_t)list.size();
             }
-        };
-        build_tree(4, 4, &h.nnodes, &h.nleaf);   // rays with a window: both slabs
-        build_tree(3, 2, &h.unodes, &h.uleaf);   // rays without one: the band alone
-        // a median tree over n points has depth ceil(log2(n / 2)) + 1 < kBvhMaxDepth
-        if (n > (1 << (kBvhMaxDepth - 2)) * 2) return false;
+        }
+        h.B_lists = down(B_s);
     }
     h.n_nodes = (int)nn;
     h.depth = bld.depth;
@@ -465,48 +422,18 @@ std::string bvh_check(const float4* isect, int n, const BvhHost& h) {
             snprintf(buf, sizeof buf, "triangle %d in %d leaves", i, seen[(size_t)i]);
             return buf;
         }
-    // the grazing trees: every triangle in one leaf of each, its folded plane in the box
-    auto check_tree = [&](const std::vector<float4>& nodes, const std::vector<float4>& leaves, bool use_w,
-                          const char* name) -> std::string {
-        std::fill(seen.begin(), seen.end(), 0);
-        const int nn = (int)(nodes.size() / 4);
-        for (int k = 0; k < nn; ++k) {
-            const float4 r0 = nodes[(size_t)k * 4], r1 = nodes[(size_t)k * 4 + 1], r2 = nodes[(size_t)k * 4 + 2];
-            int link, cnt;
-            memcpy(&link, &r1.w, 4);
-            memcpy(&cnt, &r2.w, 4);
-            for (int j = link; cnt > 0 && j < link + cnt; ++j) {
-                int i;
-                memcpy(&i, &leaves[(size_t)j * 2 + 1].y, 4);
-                if (i < 0 || i >= n) return std::string(name) + ": leaf index out of range";
-                ++seen[(size_t)i];
-                const float4 P0 = isect[(size_t)i * 3], E1 = isect[(size_t)i * 3 + 1], E2 = isect[(size_t)i * 3 + 2];
-                double N[3] = {(double)E1.y * E2.z - (double)E1.z * E2.y, (double)E1.z * E2.x - (double)E1.x * E2.z,
-                               (double)E1.x * E2.y - (double)E1.y * E2.x};
-                const double l = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-                const double w = (N[0] * P0.x + N[1] * P0.y + N[2] * P0.z) / l;
-                const double c[3] = {r0.x, r0.y, r0.z}, hh[3] = {r1.x, r1.y, r1.z};
-                bool in_p = !use_w || (r2.x <= w && w <= r2.y), in_m = !use_w || (r2.x <= -w && -w <= r2.y);
-                for (int a = 0; a < 3; ++a) {
-                    in_p = in_p && fabs(N[a] / l - c[a]) <= hh[a];
-                    in_m = in_m && fabs(-N[a] / l - c[a]) <= hh[a];
-                }
-                if (!(in_p || in_m)) {
-                    snprintf(buf, sizeof buf, "%s: plane of triangle %d outside its leaf %d", name, i, k);
-                    return buf;
-                }
-            }
+    // the direction lists: sorted, in range, the start arrays monotone
+    for (int set = 0; set < 2; ++set) {
+        const std::vector<int32_t>& start = set ? h.dstart_cam : h.dstart;
+        const std::vector<int32_t>& list = set ? h.dlist_cam : h.dlist;
+        if (start.empty() || start.back() != (int32_t)list.size()) return "direction list bounds";
+        for (size_t c = 0; c + 1 < start.size(); ++c) {
+            if (start[c] > start[c + 1]) return "direction list starts";
+            for (int32_t j = start[c]; j < start[c + 1]; ++j)
+                if (list[(size_t)j] < 0 || list[(size_t)j] >= n || (j > start[c] && list[(size_t)j] <= list[(size_t)j - 1]))
+                    return "direction list entries";
         }
-        for (int i = 0; i < n; ++i)
-            if (seen[(size_t)i] != 1) {
-                snprintf(buf, sizeof buf, "%s: triangle %d in %d leaves", name, i, seen[(size_t)i]);
-                return buf;
-            }
-        return std::string();
-    };
-    std::string e = check_tree(h.nnodes, h.nleaf, true, "plane tree");
-    if (e.empty()) e = check_tree(h.unodes, h.uleaf, false, "normal tree");
-    if (!e.empty()) return e;
+    }
     return std::string();
 }
 

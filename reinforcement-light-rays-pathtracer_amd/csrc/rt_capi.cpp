@@ -73,11 +73,8 @@ struct rt_scene {
     int accel = RT_ACCEL_AUTO;
     bool has_bvh = false;
     rt::BvhHost bvh;
-    float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, nnodes
-    float2* d_gcoef = nullptr;
-    float4* d_nleaf = nullptr;
-    float4* d_unodes = nullptr;
-    float4* d_uleaf = nullptr;
+    float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, grec
+    int32_t* d_dir[3] = {nullptr, nullptr, nullptr};           // starts (2 sets), list, camera list
 };
 
 namespace {
@@ -98,11 +95,12 @@ int scene_build_bvh(rt_scene* sc) {
     put(&sc->d_bvh[0], b.nodes);
     put(&sc->d_bvh[1], b.tris);
     put(&sc->d_bvh[2], b.graze);
-    put(&sc->d_bvh[3], b.nnodes);
-    put(&sc->d_gcoef, b.gcoef);
-    put(&sc->d_nleaf, b.nleaf);
-    put(&sc->d_unodes, b.unodes);
-    put(&sc->d_uleaf, b.uleaf);
+    put(&sc->d_bvh[3], b.grec);
+    std::vector<int32_t> starts(b.dstart);
+    starts.insert(starts.end(), b.dstart_cam.begin(), b.dstart_cam.end());
+    put(&sc->d_dir[0], starts);
+    put(&sc->d_dir[1], b.dlist);
+    put(&sc->d_dir[2], b.dlist_cam);
     if (e != hipSuccess) return RT_E_HIP;
     sc->has_bvh = true;
     return RT_OK;
@@ -113,14 +111,10 @@ void scene_free_bvh(rt_scene* sc) {
         if (p) (void)hipFree(p);
         p = nullptr;
     }
-    if (sc->d_gcoef) (void)hipFree(sc->d_gcoef);
-    if (sc->d_nleaf) (void)hipFree(sc->d_nleaf);
-    if (sc->d_unodes) (void)hipFree(sc->d_unodes);
-    if (sc->d_uleaf) (void)hipFree(sc->d_uleaf);
-    sc->d_gcoef = nullptr;
-    sc->d_nleaf = nullptr;
-    sc->d_unodes = nullptr;
-    sc->d_uleaf = nullptr;
+    for (auto& p : sc->d_dir) {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+    }
     sc->has_bvh = false;
 }
 
@@ -137,11 +131,11 @@ rt::DeviceScene launch_scene(const rt_scene* sc) {
     d.bvh_nodes = sc->d_bvh[0];
     d.bvh_tris = sc->d_bvh[1];
     d.bvh_graze = sc->d_bvh[2];
-    d.bvh_nnodes = sc->d_bvh[3];
-    d.bvh_gcoef = sc->d_gcoef;
-    d.bvh_nleaf = sc->d_nleaf;
-    d.bvh_unodes = sc->d_unodes;
-    d.bvh_uleaf = sc->d_uleaf;
+    d.bvh_grec = sc->d_bvh[3];
+    d.bvh_dstart = sc->d_dir[0];
+    d.bvh_dlist = sc->d_dir[1];
+    d.bvh_dlist_cam = sc->d_dir[2];
+    d.bvh_B_lists = sc->bvh.B_lists;
     d.bvh_sig_a = sc->bvh.sig_a;
     d.bvh_sig_b = sc->bvh.sig_b;
     return d;
@@ -716,18 +710,18 @@ int rt_bvh_check(const float* tri_v, int n, int64_t* stats) {
         }
         stats[0] = h.n_nodes;
         stats[1] = h.depth;
-        stats[2] = (int64_t)(h.nnodes.size() / 4);
+        stats[2] = (int64_t)h.dlist.size();
         stats[3] = leaves;
     }
     if (!err.empty()) return fail(RT_E_INTERNAL, "BVH invariant: %s", err.c_str());
     return RT_OK;
 }
 
-int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* plane_nodes) {
+int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* dir_entries) {
     if (!scene) return fail(RT_E_INVALID, "scene is NULL");
     if (n_nodes) *n_nodes = scene->has_bvh ? scene->bvh.n_nodes : 0;
     if (depth) *depth = scene->has_bvh ? scene->bvh.depth : 0;
-    if (plane_nodes) *plane_nodes = scene->has_bvh ? (int64_t)(scene->bvh.nnodes.size() / 4) : 0;
+    if (dir_entries) *dir_entries = scene->has_bvh ? (int64_t)scene->bvh.dlist.size() : 0;
     return RT_OK;
 }
 

@@ -66,18 +66,29 @@ constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
 //   nodes:  2 float4 per node {lo.xyz, link}, {hi.xyz, count} (int bits in w): count > 0 a
 //           leaf of tris [link, link + count), else children link, link + 1
 //   tris:   the kIsectF4 records in leaf order, [1].w = the original index (int bits)
-//   graze:  per triangle {N (float), -}; gcoef: {alpha, beta} of its grazing threshold
-//           alpha B + beta (B >= the ray's max |o_i|)
-//   nnodes: the plane-space BVH, 4 float4 per node {centre n, alpha'}, {half extents,
-//           link}, {w_lo, w_hi, beta', count}, {p_a', p_b', 0, 0}; nleaf: its leaf
-//           records, 2 float4 per triangle {N~, alpha}, {beta, index, 0, 0}
-//   unodes / uleaf: the same over the normals alone (rays without a window)
-constexpr int kBvhK = 4;          // regular pairs: |A| >= K EW (barycentrics >= -1/K)
+//   graze:  per triangle {N (float), the grazing threshold at the scene box}
+//   grec:   per triangle the grazing tests, 2 float4 {N~, alpha}, {beta, W, PA, PB}:
+//           |d.N~| <= alpha B + beta, |N~.o - W| <= PA B + PB + (alpha B + beta) lambda
+//   dstart/dlist: per cube-map cell of directions (6 x G x G), the triangles a ray in it
+//           may graze (origins within the scene box); dstart_cam/dlist_cam: any origin
+//           within obound
+#ifndef RT_BVH_K
+#define RT_BVH_K 4
+#endif
+#ifndef RT_BVH_PLANE_LEAF
+#define RT_BVH_PLANE_LEAF 4
+#endif
+constexpr int kBvhK = RT_BVH_K;   // regular pairs: |A| >= K EW (barycentrics >= -1/K)
+#ifndef RT_BVH_DIR_GRID
+#define RT_BVH_DIR_GRID 48
+#endif
+constexpr int kBvhDirGrid = RT_BVH_DIR_GRID;  // cube-map cells per face edge
 constexpr int kBvhMaxDepth = 24;  // traversal stack entries per lane (tree depth < 24)
 constexpr int kBvhCand = 4;       // rule-0 candidates kept per ray (overflow: exact scan)
 struct BvhHost {
-    std::vector<float4> nodes, tris, graze, nnodes, nleaf, unodes, uleaf;
-    std::vector<float2> gcoef;
+    std::vector<float4> nodes, tris, graze, grec;
+    std::vector<int32_t> dstart, dlist, dstart_cam, dlist_cam;
+    float B_lists = 0.f;
     int n_nodes = 0, depth = 0;
     float sig_a = 0.f, sig_b = 0.f;
 };
@@ -98,11 +109,11 @@ struct DeviceScene {
     const float4* bvh_nodes = nullptr;
     const float4* bvh_tris = nullptr;
     const float4* bvh_graze = nullptr;
-    const float2* bvh_gcoef = nullptr;
-    const float4* bvh_nnodes = nullptr;
-    const float4* bvh_nleaf = nullptr;
-    const float4* bvh_unodes = nullptr;
-    const float4* bvh_uleaf = nullptr;
+    const float4* bvh_grec = nullptr;
+    const int32_t* bvh_dstart = nullptr;      // [2][cells + 1]: scene-box origins, any origin
+    const int32_t* bvh_dlist = nullptr;
+    const int32_t* bvh_dlist_cam = nullptr;
+    float bvh_B_lists = 0.0f;
     float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f;
     int n_surf = 0;
     int n_tri = 0;

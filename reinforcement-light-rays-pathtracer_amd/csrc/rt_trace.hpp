@@ -855,10 +855,9 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         if (sp == 0) break;
         node = stk[(--sp) * 256];
     }
-    // grazing pairs: the plane-space query (rt_bvh.cpp) — triangles whose normal lies
-    // in the band |d.n| <= alpha' B + beta' and whose plane passes within p(B) + s lambda
-    // of the origin (lambda: the window found so far; unbounded for a ray that hit nothing)
-    const float4* __restrict__ gz = s.bvh_graze;
+    // grazing pairs (rt_bvh.cpp): the list of the ray's cube-map cell of directions, each
+    // triangle tested for |d.N~| <= alpha B + beta and, with a window lambda, for its plane
+    // within PA B + PB + (alpha B + beta) lambda of the origin (N units)
 #ifdef RT_BVH_TIMING_TRAVERSAL_ONLY
     {  // timing-only build (wrong hits): the traversal alone
         Hit hh;
@@ -871,48 +870,46 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
         const float cut = (RULE == 0) ? c.cut : c.bt;
         const float lam_cut = cut * t_scale * 1.0000002f;
         const bool bounded = lam_cut <= 3.0e38f;
-        const float B = om * 1.000001f;
 #ifdef RT_BVH_TIMING_SKIP_UNBOUNDED
         if (!bounded) goto resolve;  // timing-only build (wrong hits)
 #endif
-        const float4* __restrict__ nn = bounded ? s.bvh_nnodes : s.bvh_unodes;
-        const float4* __restrict__ lf = bounded ? s.bvh_nleaf : s.bvh_uleaf;
+        const float B = om * 1.000001f;
+        // the cube-map cell of d (the host lists hold for any direction of the cell, plus
+        // the rounding of this choice)
         const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
-        const float bx = fabsf(o.x), by = fabsf(o.y), bz = fabsf(o.z);
-        int nsp = 0, nd = 0;
-        for (;;) {
-            const float4 r0 = nn[4 * nd], r1 = nn[4 * nd + 1], r2 = nn[4 * nd + 2];
-            const float band = fmaf(r0.w, B, r2.z) * 1.000001f;
-            const float dc = fmaf(d.z, r0.z, fmaf(d.y, r0.y, d.x * r0.x));
-            const float rr = fmaf(az, r1.z, fmaf(ay, r1.y, ax * r1.x));
-            bool ok = !(dc - rr > band || dc + rr < -band);
-            if (ok && bounded) {
-                const float4 r3 = nn[4 * nd + 3];
-                const float r = fmaf(band, lam_cut, fmaf(r3.x, B, r3.y)) * 1.00001f +
-                                1e-6f * (1.0f + B + fabsf(r2.x) + fabsf(r2.y));
-                const float oc = fmaf(o.z, r0.z, fmaf(o.y, r0.y, o.x * r0.x));
-                const float ro = fmaf(bz, r1.z, fmaf(by, r1.y, bx * r1.x));
-                ok = !(oc - ro - r > r2.y || oc + ro + r < r2.x);
+        int f;
+        float u, v, m;
+        if (ax >= ay && ax >= az) {
+            f = d.x >= 0.0f ? 0 : 1; m = ax; u = d.y; v = d.z;
+        } else if (ay >= az) {
+            f = d.y >= 0.0f ? 2 : 3; m = ay; u = d.z; v = d.x;
+        } else {
+            f = d.z >= 0.0f ? 4 : 5; m = az; u = d.x; v = d.y;
+        }
+        const float G = (float)kBvhDirGrid;
+        const int iu = min(kBvhDirGrid - 1, max(0, (int)((u / m + 1.0f) * 0.5f * G)));
+        const int iv = min(kBvhDirGrid - 1, max(0, (int)((v / m + 1.0f) * 0.5f * G)));
+        const int cell = (f * kBvhDirGrid + iu) * kBvhDirGrid + iv;
+        const bool cam = !(B <= s.bvh_B_lists);
+        const int32_t* st = s.bvh_dstart + (cam ? 6 * kBvhDirGrid * kBvhDirGrid + 1 : 0);
+        const int32_t* __restrict__ dl = cam ? s.bvh_dlist_cam : s.bvh_dlist;
+        const float4* __restrict__ gr = s.bvh_grec;
+        const int j0 = st[cell], j1 = st[cell + 1];
+        for (int j = j0; j < j1; ++j) {
+            const int i = dl[j];
+            const float4 g = gr[2 * i];
+            const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
+            const float4 q = gr[2 * i + 1];
+            const float thr = fmaf(g.w, B, q.x) * 1.000001f;
+            bool cand = fabsf(a) <= thr;
+            if (cand && bounded) {
+                const float w = fmaf(o.z, g.z, fmaf(o.y, g.y, o.x * g.x)) - q.y;
+                cand = fabsf(w) <= fmaf(thr, lam_cut, fmaf(q.z, B, q.w)) * 1.00001f;
             }
-            if (ok) {
-                const int link = __float_as_int(r1.w), cnt = __float_as_int(r2.w);
-                if (cnt == 0) {
-                    stk[(nsp++) * 256] = link + 1;
-                    nd = link;
-                    continue;
-                }
-                for (int k = link; k < link + cnt; ++k) {
-                    const float4 g = lf[2 * k], q = lf[2 * k + 1];
-                    const float a = fmaf(d.z, g.z, fmaf(d.y, g.y, d.x * g.x));
-                    if (fabsf(a) <= fmaf(g.w, B, q.x) * 1.000001f) {
-                        const int i = __float_as_int(q.y);
-                        const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
-                        if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
-                    }
-                }
+            if (cand) {
+                const float t = exact_tv<RULE>(s.isect, i, o, nDx, nDy, nDz);
+                if (t <= FLT_MAX) bvh_insert<RULE>(c, t, i);
             }
-            if (nsp == 0) break;
-            nd = stk[(--nsp) * 256];
         }
     }
 #ifdef RT_BVH_TIMING_SKIP_UNBOUNDED
