@@ -83,9 +83,16 @@ def lib_sha256() -> str:
     return hashlib.sha256(open(rtmi.LIB_PATH, "rb").read()).hexdigest()
 
 
+def render_obj_sha256() -> str:
+    path = os.path.join(os.path.dirname(rtmi.LIB_PATH), "rt_kernels.o")
+    return hashlib.sha256(open(path, "rb").read()).hexdigest() if os.path.exists(path) else ""
+
+
 def load_profile():
-    """The newest bench PMC profile whose library hash equals the loaded librtmi.so."""
-    sha = lib_sha256()
+    """The newest bench PMC profile of this build: its library hash equals the loaded
+    librtmi.so, or its render-kernel object (build/rt_kernels.o, which holds k_render_ps and
+    nothing the other sources contribute) equals the one this library was linked from."""
+    sha, osha = lib_sha256(), render_obj_sha256()
     newest = None
     for path in sorted(glob.glob(PMC_GLOB), key=os.path.getmtime):
         try:
@@ -93,7 +100,7 @@ def load_profile():
         except (OSError, ValueError):
             continue
         newest = (os.path.relpath(path, ROOT), prof)
-        if prof.get("lib_sha256") == sha:
+        if prof.get("lib_sha256") == sha or (osha and prof.get("render_obj_sha256") == osha):
             return newest[0], prof, True
     return (newest[0], newest[1], False) if newest else (None, None, False)
 

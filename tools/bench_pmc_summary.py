@@ -2,7 +2,9 @@
 """Summarise tools/gpu_bench_pmc.sh into profiles/<tag>_bench_pmc.json: per kernel of the
 bench workload, the average duration (rocprofv3 --kernel-trace --stats) and every PMC
 counter per dispatch (mean over the dispatches of each pass), plus the sha256 of the
-librtmi.so that was profiled (bench.py checks it against the library it loads).
+librtmi.so that was profiled and of its render-kernel object build/rt_kernels.o (bench.py
+accepts the profile when either equals the build it loads: a change elsewhere in the
+library leaves the render kernel's code, and so its counters, unchanged).
 
     python tools/bench_pmc_summary.py gpurun_out/pmc_<tag> <tag>
 
@@ -20,13 +22,15 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", "build", "librtmi.so")
+RENDER_OBJ = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", "build", "rt_kernels.o")
 KEYS = ("k_render", "k_cull")
 
 
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     out = {"tag": tag, "workload": "bench.py --steps 10 --warmup 2 (Cornell 512x512, 256 spp, spp_split 64)",
-           "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(), "kernels": {}}
+           "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
+           "render_obj_sha256": hashlib.sha256(open(RENDER_OBJ, "rb").read()).hexdigest(), "kernels": {}}
     stats = glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_bench_kernel_stats.csv"))
