@@ -171,11 +171,13 @@ def cpu_baseline(geom, params, cam_pos, seconds):
     rate = casts / max(time.perf_counter() - t0, 1e-9)
     per_row = casts / rows
     rows = int(max(4, min(params.height, seconds * rate / max(per_row, 1.0))))
+    if rows >= 0.6 * params.height:  # most of the frame anyway: take all of it (a full-frame parity check)
+        rows = params.height
     y0 = max(0, params.height // 2 - rows // 2)
-    best = None
+    best, strip = None, None
     for _ in range(3):
         t0 = time.perf_counter()
-        _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
+        strip, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
     oracle.set_threads(1)
@@ -193,7 +195,21 @@ def cpu_baseline(geom, params, cam_pos, seconds):
                   f"({casts} ray casts, best of 3: {best:.2f} s, OpenMP over rows)",
         "value_1thread": round(casts1 / max(dt1, 1e-9) / 1e6, 3),
         "sample_1thread": f"rows {y1}..{y1 + 1} ({casts1} ray casts, {dt1:.2f} s, 1 thread)",
-    }
+    }, (y0, rows, strip, casts)
+
+
+def parity_strip(ctx, scene, cam, params, image, strip_run):
+    """The CPU baseline's own render (rows y0..y0+rows-1, the whole frame when the time budget
+    allows) against the same rows of the GPU frame: bits, MAPE, and the ray casts of a
+    separate GPU render of the strip.  No extra CPU work."""
+    y0, rows, ref, ref_casts = strip_run
+    got = image[y0:y0 + rows]
+    _, gpu_casts = rtmi.render(ctx, scene, cam, params, (0, y0, params.width, rows))
+    return {"rows": [y0, y0 + rows - 1], "pixels": int(rows * params.width),
+            "frac_of_frame": round(rows / params.height, 4),
+            "mape_vs_cpu": rtmi.metrics.mape_f(ref, got),
+            "bit_exact": bool(np.array_equal(ref.view(np.uint32), got.view(np.uint32))),
+            "ray_casts_equal": gpu_casts == ref_casts, "ray_casts": int(ref_casts)}
 
 
 def parity_tiles(ctx, scene, geom, params, cam, cam_pos, image):
@@ -355,7 +371,9 @@ def main():
         if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
             line["parity"] = parity_tiles(ctx, scene, geom, params, cam, cam_pos, image)
         if args.cpu_seconds > 0 and world == 1 and sampler == "uniform":  # the CPU baseline is an N=1 figure
-            line["cpu_baseline"] = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
+            line["cpu_baseline"], strip_run = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
+            if "parity" in line:  # the baseline's strip is the same frame: check it too
+                line["parity"]["cpu_strip"] = parity_strip(ctx, scene, cam, params, image, strip_run)
         print(json.dumps(line), flush=True)
 
     for o in extra:

@@ -55,6 +55,13 @@ constexpr int slots(int tiles) { return (tiles + kMlpWaves - 1) / kMlpWaves; }
 // hits 16 distinct 16-B slots (conflict-free; the padded 328 / 232 rows were 2-way) and
 // the 8-B epilogue stores are 2-way (bank rule of MI355X_MICROARCH.md §LDS, brute-forced
 // over strides and swizzles)
+#ifndef RT_MLP_RING_VGPRS
+#define RT_MLP_RING_VGPRS 60  // VGPRs of the weight-fragment ring (60: 3 K steps of layer 1's 5 fragments)
+#endif
+constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
+#ifndef RT_MLP_PROLOGUE_GROUP
+#define RT_MLP_PROLOGUE_GROUP 1
+#endif
 constexpr int kStrideA = 336;
 constexpr int kStrideB = 272;
 __device__ __forceinline__ int swz(int row, int k, int stride) {
@@ -153,24 +160,36 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     if constexpr (KS > 0) {
         // K known at compile time (the reference's 200-300-200 shape): the weight
-        // fragments of step k+2 and the activations of step k+1 are in flight while the
-        // MFMAs of step k run (a 3-deep register ring, fully unrolled: no copies)
-        bf16x8 bw[3][NT], a[2][MT];
+        // fragments of steps k+1 .. k+R-1 and the activations of step k+1 are in flight
+        // while the MFMAs of step k run (an R-deep register ring, fully unrolled: no
+        // copies).  R is set by the register budget: the kernel is held to two waves per
+        // SIMD by its LDS anyway, so VGPRs up to 256 are free, and an L2 fragment load
+        // (~1 us under load) needs several K steps of MFMAs (NT*MT*16 clk each) to hide.
+        constexpr int R = (kMlpRingVgprs / (4 * NT)) < 2 ? 2 : (kMlpRingVgprs / (4 * NT));
+        bf16x8 bw[R][NT], a[2][MT];
 #pragma unroll
-        for (int j = 0; j < NT; ++j) bw[0][j] = *reinterpret_cast<const bf16x8*>(wrow[j]);
-        if (KS > 1) {
+        for (int s = 0; s < R - 1; ++s) {
+            if (s < KS) {
 #pragma unroll
-            for (int j = 0; j < NT; ++j) bw[1][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + 32 * 16);
+                for (int j = 0; j < NT; ++j) bw[s][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + s * 32 * 16);
+            }
         }
 #pragma unroll
         for (int m = 0; m < MT; ++m)
             a[0][m] = *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, kg, in_stride));
+#if RT_MLP_PROLOGUE_GROUP
+        // the prologue's loads as their own groups: each step's groups below then claim
+        // that step's own loads (without this the scheduler pairs step k's MFMAs with the
+        // prologue's second step, and the ring is one step shallower than written)
+        __builtin_amdgcn_sched_group_barrier(0x020, (R - 1 < KS ? R - 1 : KS) * NT, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);
+#endif
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-            if (ks + 2 < KS) {
+            if (ks + R - 1 < KS) {
 #pragma unroll
                 for (int j = 0; j < NT; ++j)
-                    bw[(ks + 2) % 3][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + (ks + 2) * 32 * 16);
+                    bw[(ks + R - 1) % R][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + (ks + R - 1) * 32 * 16);
             }
             if (ks + 1 < KS) {
 #pragma unroll
@@ -182,9 +201,14 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
             for (int j = 0; j < NT; ++j)
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % 3][j], a[ks & 1][m], acc[m][j], 0, 0, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);       // VMEM reads
-            __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);       // LDS reads
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % R][j], a[ks & 1][m], acc[m][j], 0, 0, 0);
+#if RT_MLP_PROLOGUE_GROUP
+            if (ks + R - 1 < KS) __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);  // VMEM reads
+            if (ks + 1 < KS) __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);      // LDS reads
+#else
+            __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);
+#endif
             __builtin_amdgcn_sched_group_barrier(0x008, NT * MT, 0);  // MFMA
         }
     } else {
