@@ -365,8 +365,8 @@ def main():
             },
             "ray_casts_per_step": total_casts // args.steps,
             "roofline": roofline(geom, rank_casts / args.steps, kernel_ms, default, {
-                "uniform": "k_render_ps<0,0,MF>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal>",
-                "sarsa": "k_sarsa_render + k_sarsa_apply", "dqn": "k_dqn_mlp + k_dqn_bounce (wavefront)"}[sampler]),
+                "uniform": "k_render_ps<0,0,MF>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal,MF>",
+                "sarsa": "k_sarsa_render<1,MF> + k_sarsa_apply", "dqn": "k_dqn_mlp + k_dqn_bounce<MF> (wavefront)"}[sampler]),
         }
         if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
             line["parity"] = parity_tiles(ctx, scene, geom, params, cam, cam_pos, image)

@@ -428,11 +428,21 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
 
 // trace_ray (pre_trained_pathtracer.cu:413-491): Ray(pos + dir*1e-5, dir), GPU hit rule.
 // Returns true if the ray continues (hit a surface).
-__device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, f3* loc_out, int* tri_out,
-                                          f3* tp) {
+// MF > 0: the cast on the matrix-core filter (closest_hit_mf: every lane of the wave
+// calls, `active` false for a lane without a ray, which then returns false untouched).
+template <int MF>
+__device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bool active, float* wl, f3* loc_out,
+                                          int* tri_out, f3* tp) {
     const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
     const f3 d = normalize(dir);
-    const Hit h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
+    Hit h;
+    if constexpr (MF > 0) {
+        h = closest_hit_mf<1, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+        if (!active) return false;
+    } else {
+        if (!active) return false;
+        h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
+    }
     if (h.tri < 0) {
         *tp = make3(tp->x * a.env_light, tp->y * a.env_light, tp->z * a.env_light);
         return false;
@@ -493,29 +503,39 @@ __device__ __forceinline__ f3 dqn_camera_dir(const DqnLaunch& a, float x, float 
 }
 
 // initialise_ray + the first trace_ray (bounce 0: no Q evaluation)
-__global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a) {
+#ifndef RT_MF_DQN_WAVES
+#define RT_MF_DQN_WAVES 4  // occupancy floor of the MF variants
+#endif
+template <int MF>
+__global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camera(const DqnLaunch a) {
+    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
     const int rid = blockIdx.x * 256 + threadIdx.x;
     bool keep = false;
     unsigned casts = 0;
+    bool valid = false;
+    f3 d = make3(0.0f, 0.0f, 1.0f), tp = make3(0.0f, 0.0f, 0.0f);
     if (rid < a.rays.n) {
         const int slot = rid / a.rays.n_pix, pi = rid - slot * a.rays.n_pix;
         const int sample = a.rays.s0 + slot;
         int px, py;
-        const bool valid = ray_pixel(a, pi, &px, &py);
-        f3 tp = make3(valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f);
+        valid = ray_pixel(a, pi, &px, &py);
+        tp = make3(valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f, valid ? 1.0f : 0.0f);
         if (valid) {
             float r1, r2;
             draw2(a.rays.pix[pi], (uint32_t)sample, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
             const float x = (float)px + r1, y = (float)py + r2;
-            const f3 d = dqn_camera_dir(a, x, y);
-            f3 loc;
-            int tri = 0;
-            keep = dqn_trace(a, make3(a.cam_x, a.cam_y, a.cam_z), d, &loc, &tri, &tp);
+            d = dqn_camera_dir(a, x, y);
             casts = 1;
-            if (keep) {
-                st3(a.rays.loc, rid, loc);
-                a.rays.tri[rid] = tri;
-            }
+        }
+    }
+    f3 loc;
+    int tri = 0;
+    keep = dqn_trace<MF>(a, make3(a.cam_x, a.cam_y, a.cam_z), d, valid, s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats,
+                         &loc, &tri, &tp);
+    if (rid < a.rays.n) {
+        if (keep) {
+            st3(a.rays.loc, rid, loc);
+            a.rays.tri[rid] = tri;
         }
         st3(a.rays.tp, rid, tp);
     }
@@ -525,7 +545,9 @@ __global__ __launch_bounds__(256) void k_dqn_camera(const DqnLaunch a) {
 }
 
 // one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
-__global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int bounce) {
+template <int MF>
+__global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounce(const DqnLaunch a, int bounce) {
+    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int n_act = a.rays.count[cur];
@@ -533,14 +555,18 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int bounc
     bool keep = false;
     unsigned casts = 0;
     int rid = 0;
+    bool want = false;  // the lane casts a ray (wave-level filter below)
+    f3 pos = make3(0.0f, 0.0f, 0.0f), dir = make3(0.0f, 0.0f, 1.0f), tp = make3(0.0f, 0.0f, 0.0f);
+    f3 loc = pos;
+    int ntri = 0;
     if (i < n_act) {
         rid = a.rays.list[cur][i];
         const int slot = rid / a.rays.n_pix;
         const int sample = a.rays.s0 + slot;
         const uint32_t pixid = a.rays.pix[rid - slot * a.rays.n_pix];
         const int tri = a.rays.tri[rid];
-        const f3 pos = ld3(a.rays.loc, rid);
-        f3 tp = ld3(a.rays.tp, rid);
+        pos = ld3(a.rays.loc, rid);
+        tp = ld3(a.rays.tp, rid);
         const float4 N4 = a.scene.shade[tri * kShadeF4 + 0];
         const float4 T4 = a.scene.shade[tri * kShadeF4 + 1];
         const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
@@ -549,14 +575,18 @@ __global__ __launch_bounds__(256) void k_dqn_bounce(const DqnLaunch a, int bounc
                           make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                           1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
-        f3 loc = pos;
-        int ntri = tri;
+        loc = pos;
+        ntri = tri;
         if (so.action >= 0) {
-            keep = dqn_trace(a, pos, so.dir, &loc, &ntri, &tp);
+            want = true;
+            dir = so.dir;
         } else {
             // zero direction: the reference's ray is NaN and hits nothing
             tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
         }
+    }
+    keep = dqn_trace<MF>(a, pos, dir, want, s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats, &loc, &ntri, &tp);
+    if (i < n_act) {
         if (keep) {
             st3(a.rays.loc, rid, loc);
             a.rays.tri[rid] = ntri;
@@ -834,8 +864,25 @@ hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#ifndef RT_MF_DQN
+#define RT_MF_DQN 1  // 0: the casts on the fp32 filter (A/B builds)
+#endif
+// 64-triangle blocks of the matrix-core filter for this launch (0: the fp32 filter): the
+// image present and the camera inside its origin bound (as launch_render_t)
+static int dqn_mf(const DqnLaunch& a) {
+    const float cb = a.scene.mf_bound;
+    const bool mf = RT_MF_DQN && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
+                    a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
+                    fabsf(a.cam_z) <= cb;
+    return mf ? (a.scene.n_tri <= 64 ? 1 : 4) : 0;
+}
+
 hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
-    hipLaunchKernelGGL(k_dqn_camera, dim3(ray_blocks(a)), dim3(256), 0, stream, a);
+    switch (dqn_mf(a)) {
+        case 1: hipLaunchKernelGGL(k_dqn_camera<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
+        case 4: hipLaunchKernelGGL(k_dqn_camera<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
+        default: hipLaunchKernelGGL(k_dqn_camera<0>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
+    }
     return hipGetLastError();
 }
 
@@ -844,7 +891,11 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
     hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
                                   a.rays.q, a.rays.ldq, stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_dqn_bounce, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce);
+    switch (dqn_mf(a)) {
+        case 1: hipLaunchKernelGGL(k_dqn_bounce<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
+        case 4: hipLaunchKernelGGL(k_dqn_bounce<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
+        default: hipLaunchKernelGGL(k_dqn_bounce<0>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
+    }
     return hipGetLastError();
 }
 

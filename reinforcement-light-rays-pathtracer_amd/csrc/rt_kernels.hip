@@ -104,13 +104,22 @@ __global__ __launch_bounds__(256) void k_intersect_bvh(const DeviceScene s, cons
 //
 // BVH: large scenes cast through closest_hit_bvh (the exact BVH path: same hits as the
 // scan).
-template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH>
+//
+// MF (> 0: 64-triangle blocks per super-block): every cast on the matrix-core filter
+// (closest_hit_mf, wave-level: lanes without a live sample take part with no
+// candidates), as the bounce casts of k_render_ps; the launcher picks it when the camera
+// lies inside the image's origin bound (else every camera ray would keep every triangle).
+template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH, int MF = 0>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1
 #endif
-__global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch a) {
+#ifndef RT_MF_RENDER_WAVES
+#define RT_MF_RENDER_WAVES 4  // occupancy floor of the MF variants (<= 128 VGPRs; 1: the compiler's 142-150)
+#endif
+__global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) void k_render(const RenderLaunch a) {
     extern __shared__ float s_val[];  // STEAL: [pixel of the workgroup][spp][3]
     __shared__ int s_stk[BVH ? kBvhMaxDepth * 256 : 1];
+    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];  // MF: the waves' exact-phase LDS
     // workgroup -> (16x16 block, part); lane -> (pixel of the block, sample chunk)
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -151,10 +160,16 @@ __global__ __launch_bounds__(256, RT_MIN_WAVES) void k_render(const RenderLaunch
     for (;;) {
         const bool active = s < s_end;
         if (__ballot(active) == 0ull) break;
-        if (!active) continue;
-
-        const Hit h = BVH ? closest_hit_bvh<RULE>(a.scene, o, d, a.t_scale, s_stk + threadIdx.x)
-                          : closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
+        Hit h;
+        if constexpr (MF > 0) {
+            h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active,
+                                                s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats);
+            if (!active) continue;
+        } else {
+            if (!active) continue;
+            h = BVH ? closest_hit_bvh<RULE>(a.scene, o, d, a.t_scale, s_stk + threadIdx.x)
+                    : closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
+        }
         ++n_casts;
 
         bool terminal = false;
@@ -850,6 +865,9 @@ hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const fl
     return hipGetLastError();
 }
 
+#ifndef RT_MF_RENDER
+#define RT_MF_RENDER 1  // 0: the GPU preset's casts on the fp32 filter (A/B builds)
+#endif
 #ifndef RT_STEAL_MAX_LDS
 #define RT_STEAL_MAX_LDS (64 * 1024)  // sample stealing when its LDS fits (0: never)
 #endif
@@ -889,6 +907,26 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     const size_t lds = (size_t)(256 / a.split) * (size_t)a.spp * 3 * sizeof(float);
     const dim3 grid((unsigned)(a.n_blocks * a.split));
     const bool steal = PRESET == 1 && lds <= (size_t)RT_STEAL_MAX_LDS;
+    // the GPU preset's casts on the matrix-core filter: when the scene has the image and
+    // the camera is inside its origin bound (camera rays then get real masks)
+    const float cb = a.scene.mf_bound;
+    const bool mf = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
+                    a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale &&
+                    fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb;
+    if (mf) {
+        if (PRESET == 1) {  // (the CPU preset runs k_render_ps)
+            const bool one = a.scene.n_tri <= 64;
+            if (steal && one)
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 1>), grid, dim3(256), lds, stream, a);
+            else if (steal)
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 4>), grid, dim3(256), lds, stream, a);
+            else if (one)
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 1>), grid, dim3(256), 0, stream, a);
+            else
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 4>), grid, dim3(256), 0, stream, a);
+        }
+        return;
+    }
     if (a.scene.bvh_nodes != nullptr) {
         if (steal)
             hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, true>), grid, dim3(256), lds, stream, a);

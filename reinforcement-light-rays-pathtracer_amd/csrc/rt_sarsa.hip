@@ -283,7 +283,9 @@ __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, 
 }
 
 // path_trace_reinforcement_iterative (reinforcement_path_tracing.cu:50-120), GPU preset
-template <int RULE>
+// MF > 0: every cast on the matrix-core filter (closest_hit_mf, wave-level; the launcher
+// picks it as launch_render_t does for k_render: image present, camera inside its bound)
+template <int RULE, int MF = 0>
 __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, const SarsaMap m) {
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
@@ -300,6 +302,7 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     const int s_end = (chunk + 1) * a.per_chunk;
     __shared__ int kd_stack[kKdStack * 256];
     int* const st = kd_stack + threadIdx.x;
+    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
 
     int s = valid ? chunk * a.per_chunk : s_end;
     int depth = 0;
@@ -316,8 +319,15 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     for (;;) {
         const bool active = s < s_end;
         if (__ballot(active) == 0ull) break;
-        if (!active) continue;
-        const Hit h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
+        Hit h;
+        if constexpr (MF > 0) {
+            h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active,
+                                                s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats);
+            if (!active) continue;
+        } else {
+            if (!active) continue;
+            h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
+        }
         ++n_casts;
         const bool is_surf = (h.tri >= 0) && (h.tri < n_surf);
         f3 pos = o;
@@ -542,8 +552,29 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
     return hipGetLastError();
 }
 
+#ifndef RT_MF_SARSA
+#define RT_MF_SARSA 1  // 0: the casts on the fp32 filter (A/B builds)
+#endif
+
 hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
     if (a.n_blocks <= 0) return hipSuccess;
+    const float cb = a.scene.mf_bound;
+    const bool mf = RT_MF_SARSA && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
+                    a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
+                    fabsf(a.cam_z) <= cb;
+    if (mf) {
+        const dim3 grid((unsigned)(a.n_blocks * a.split));
+        const bool one = a.scene.n_tri <= 64;
+        if (a.hit_rule == 0 && one)
+            hipLaunchKernelGGL((k_sarsa_render<0, 1>), grid, dim3(256), 0, stream, a, m);
+        else if (a.hit_rule == 0)
+            hipLaunchKernelGGL((k_sarsa_render<0, 4>), grid, dim3(256), 0, stream, a, m);
+        else if (one)
+            hipLaunchKernelGGL((k_sarsa_render<1, 1>), grid, dim3(256), 0, stream, a, m);
+        else
+            hipLaunchKernelGGL((k_sarsa_render<1, 4>), grid, dim3(256), 0, stream, a, m);
+        return hipGetLastError();
+    }
     if (a.hit_rule == 0)
         hipLaunchKernelGGL(k_sarsa_render<0>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
     else
