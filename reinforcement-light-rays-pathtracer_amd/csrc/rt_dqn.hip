@@ -865,7 +865,7 @@ hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
 }
 
 #ifndef RT_MF_DQN
-#define RT_MF_DQN 1  // 0: the casts on the fp32 filter (A/B builds)
+#define RT_MF_DQN 0  // 1: the casts on the matrix-core filter (measured equal: DESIGN.md §4)
 #endif
 // 64-triangle blocks of the matrix-core filter for this launch (0: the fp32 filter): the
 // image present and the camera inside its origin bound (as launch_render_t)

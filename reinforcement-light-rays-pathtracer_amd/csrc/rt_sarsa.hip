@@ -553,7 +553,7 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 }
 
 #ifndef RT_MF_SARSA
-#define RT_MF_SARSA 1  // 0: the casts on the fp32 filter (A/B builds)
+#define RT_MF_SARSA 0  // 1: the casts on the matrix-core filter (measured slower: DESIGN.md §4)
 #endif
 
 hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
