@@ -84,8 +84,14 @@ def lib_sha256() -> str:
 
 
 def render_obj_sha256() -> str:
+    """sha256 of build/rt_kernels.o, or the hash the Makefile wrote beside it (the object
+    file itself is not shipped to the GPU box)."""
     path = os.path.join(os.path.dirname(rtmi.LIB_PATH), "rt_kernels.o")
-    return hashlib.sha256(open(path, "rb").read()).hexdigest() if os.path.exists(path) else ""
+    if os.path.exists(path):
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    if os.path.exists(path + ".sha256"):
+        return open(path + ".sha256").read().strip()
+    return ""
 
 
 def load_profile():

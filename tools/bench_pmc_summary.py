@@ -30,7 +30,9 @@ def main():
     d, tag = sys.argv[1], sys.argv[2]
     out = {"tag": tag, "workload": "bench.py --steps 10 --warmup 2 (Cornell 512x512, 256 spp, spp_split 64)",
            "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
-           "render_obj_sha256": hashlib.sha256(open(RENDER_OBJ, "rb").read()).hexdigest(), "kernels": {}}
+           "render_obj_sha256": (hashlib.sha256(open(RENDER_OBJ, "rb").read()).hexdigest()
+                                 if os.path.exists(RENDER_OBJ) else open(RENDER_OBJ + ".sha256").read().strip()),
+           "kernels": {}}
     stats = glob.glob(os.path.join(d, "kt", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(ROOT, "profiles", f"{tag}_bench_kernel_stats.csv"))
