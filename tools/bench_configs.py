@@ -78,7 +78,9 @@ def c1(ctx, stream):
 
 def c2(ctx, stream):
     g = rtmi.cornell_geometry(rtmi.RT_PRESET_CPU)
-    p = rtmi.default_params(rtmi.RT_PRESET_CPU, width=512, height=512, spp=256, spp_split=32)
+    # bench.py's split (64 lanes per pixel, 4 samples each): at 32 the sample slots of
+    # k_render_ps exceed its LDS budget and the frame falls back to k_render
+    p = rtmi.default_params(rtmi.RT_PRESET_CPU, width=512, height=512, spp=256, spp_split=64)
     with rtmi.Scene(ctx, g) as sc:
         tiles = rtmi.tiles.tile_origins(512, 512, TILE)
         ms, casts, _ = tile_render(ctx, sc, rtmi.camera(rtmi.CAMERAS["cornell"]), p, tiles, stream, 5)
