@@ -865,6 +865,9 @@ hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const fl
     return hipGetLastError();
 }
 
+#ifndef RT_MF_CAM_OUT_MAX_TRI
+#define RT_MF_CAM_OUT_MAX_TRI 0  // > 0: A/B builds (launch_render_t)
+#endif
 #ifndef RT_MF_RENDER
 #define RT_MF_RENDER 1  // 0: the GPU preset's casts on the fp32 filter (A/B builds)
 #endif
@@ -910,9 +913,18 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     // the GPU preset's casts on the matrix-core filter: when the scene has the image and
     // the camera is inside its origin bound (camera rays then get real masks)
     const float cb = a.scene.mf_bound;
+#if RT_MF_CAM_OUT_MAX_TRI > 0
+    // A/B builds: small scenes take the filter with the camera outside too (its camera
+    // rays keep every triangle: the shared exact phase tests them all)
+    const bool cam_ok = (fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb) ||
+                        a.scene.n_tri <= RT_MF_CAM_OUT_MAX_TRI;
+    const bool mf = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
+                    a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale && cam_ok;
+#else
     const bool mf = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
                     a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale &&
                     fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb;
+#endif
     if (mf) {
         if (PRESET == 1) {  // (the CPU preset runs k_render_ps)
             const bool one = a.scene.n_tri <= 64;
