@@ -1,5 +1,6 @@
 #!/bin/bash
-# k_dqn_mlp persistent (RT_MLP_PERSIST=1) vs one tile per workgroup (base): DQN tests on
+# k_dqn_mlp persistent (RT_MLP_PERSIST=1, a switch of the r2s experiment since removed from
+# the source: DESIGN.md §4) vs one tile per workgroup (base): DQN tests on
 # both builds, then the 1 M-ray forward and the archway 1024^2 x 4 spp render, interleaved.
 tag=${1:-r2s}
 mkdir -p gpurun_out/$tag
