@@ -157,7 +157,8 @@ int rt_intersect_device(rt_ctx* ctx, const rt_scene* scene, const float* d_orig,
 #define RT_ISECT_SCAN 0
 #define RT_ISECT_FILTER 1
 #define RT_ISECT_MFMA 2
-#define RT_ISECT_BVH 3 /* the exact BVH path (built on demand) */
+#define RT_ISECT_BVH 3 /* the exact BVH path: built on first use if the scene has none, and kept
+                          (this call may allocate); the scene's accel mode is not changed */
 int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, const float* dir, int n,
                         float t_scale, int hit_rule, int method, float* out_t, int32_t* out_hit,
                         int32_t* out_cand);
@@ -169,8 +170,10 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
  * scan's hit bit for bit (both hit rules): padded boxes that prove the exact test fails,
  * and a second BVH over the triangles' planes for the pairs a ray could graze (rt_bvh.cpp).  RT_ACCEL_AUTO (the
  * default) builds and uses it for scenes above RT_BVH_AUTO_MIN triangles; RT_ACCEL_SCAN
- * never uses it; RT_ACCEL_BVH builds it for any scene (A/B).  Renders and rt_intersect
- * follow the mode. */
+ * never uses it; RT_ACCEL_BVH builds it for any scene (A/B).  The default-sampler renders
+ * (rt_render, rt_render_tiles_device) and rt_intersect / rt_intersect_device follow the mode;
+ * the Expected-SARSA, DQN and Neural-Q kernels always run the (filtered) scan of every
+ * triangle, whatever the mode. */
 #define RT_ACCEL_AUTO 0
 #define RT_ACCEL_SCAN 1
 #define RT_ACCEL_BVH 2
@@ -439,6 +442,23 @@ int rt_rect_candidates(const float* filt, int n_tri, const rt_camera* cam, const
  * out on entry, words written on return. */
 int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
                          int x0, int y0, int w, int h, uint64_t* out, int64_t* n_words);
+
+/* Live kernel timing (no reference counterpart; bench.py's roofline): while enabled, every
+ * launch of the kernel families below is bracketed by a HIP event pair on its own launch
+ * stream.  rt_ktime_enable(1) clears the totals and starts, rt_ktime_enable(0) stops;
+ * rt_ktime_read waits for the recorded launches and returns the total milliseconds and the
+ * launch count of one family since the last enable. */
+#define RT_KT_RENDER_PS 0     /* k_render_ps: CPU preset (configs 1-2, the bench kernel) */
+#define RT_KT_RENDER 1        /* k_render: GPU preset (config 5) */
+#define RT_KT_SARSA_RENDER 2  /* k_sarsa_render (config 3) */
+#define RT_KT_SARSA_APPLY 3   /* k_sarsa_apply */
+#define RT_KT_DQN_MLP 4       /* k_dqn_mlp: the Q-network forward (config 4) */
+#define RT_KT_DQN_BOUNCE 5    /* k_dqn_bounce: Q.cos sampling + trace */
+#define RT_KT_DQN_CAMERA 6    /* k_dqn_camera */
+#define RT_KT_COUNT 7
+int rt_ktime_enable(int on);
+int rt_ktime_read(int kernel, double* total_ms, int64_t* launches);
+const char* rt_ktime_name(int kernel);
 
 /* SDLScreen::PutPixelSDL pack rule (CPU/sdl/sdl_screen.cpp:100-112). Host arrays. */
 int rt_pack_argb(const float* rgb, int n, uint32_t* out_argb);

@@ -79,8 +79,13 @@ struct rt_scene {
 
 namespace {
 // the BVH's device arrays, or nothing
+void scene_free_bvh(rt_scene* sc);
+
+// (on any failure every partial allocation is released: has_bvh stays false and the
+// pointers null, so a later call starts clean)
 int scene_build_bvh(rt_scene* sc) {
     if (sc->has_bvh) return RT_OK;
+    scene_free_bvh(sc);
     std::vector<float4> isect((size_t)sc->dev.n_tri * rt::kIsectF4);
     if (hipMemcpy(isect.data(), sc->dev.isect, sizeof(float4) * isect.size(), hipMemcpyDeviceToHost) != hipSuccess)
         return RT_E_HIP;
@@ -101,7 +106,10 @@ int scene_build_bvh(rt_scene* sc) {
     put(&sc->d_dir[0], starts);
     put(&sc->d_dir[1], b.dlist);
     put(&sc->d_dir[2], b.dlist_cam);
-    if (e != hipSuccess) return RT_E_HIP;
+    if (e != hipSuccess) {
+        scene_free_bvh(sc);
+        return RT_E_HIP;
+    }
     sc->has_bvh = true;
     return RT_OK;
 }
@@ -124,10 +132,11 @@ bool scene_uses_bvh(const rt_scene* sc) {
     return sc->accel == RT_ACCEL_AUTO && sc->dev.n_tri > RT_BVH_AUTO_MIN;
 }
 
-// the device view of the scene for a launch (BVH fields set when the BVH path is on)
-rt::DeviceScene launch_scene(const rt_scene* sc) {
+// the device view of the scene for a launch (BVH fields set when the BVH path is on, or
+// whenever the BVH exists with force_bvh: RT_ISECT_BVH, without touching the scene's mode)
+rt::DeviceScene launch_scene(const rt_scene* sc, bool force_bvh = false) {
     rt::DeviceScene d = sc->dev;
-    if (!scene_uses_bvh(sc)) return d;
+    if (force_bvh ? !sc->has_bvh : !scene_uses_bvh(sc)) return d;
     d.bvh_nodes = sc->d_bvh[0];
     d.bvh_tris = sc->d_bvh[1];
     d.bvh_graze = sc->d_bvh[2];
@@ -730,13 +739,11 @@ static int intersect_bvh_host(rt_ctx* ctx, const rt_scene* scene, const float* o
                               float t_scale, int hit_rule, float* out_t, int32_t* out_hit) {
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
+    // builds the BVH once if the scene has none yet (kept for later calls; rt_scene_set_accel
+    // builds it up front); the scene's accel mode is not touched
     rc = scene_build_bvh(const_cast<rt_scene*>(scene));
     if (rc != RT_OK) return fail(rc, "BVH build failed");
-    rt_scene* sc = const_cast<rt_scene*>(scene);
-    const int saved = sc->accel;
-    sc->accel = RT_ACCEL_BVH;
-    const rt::DeviceScene ds = launch_scene(sc);
-    sc->accel = saved;
+    const rt::DeviceScene ds = launch_scene(scene, /*force_bvh=*/true);
     float *d_o = nullptr, *d_d = nullptr, *d_t = nullptr;
     int32_t* d_h = nullptr;
     const size_t b3 = sizeof(float) * 3 * (size_t)n;
@@ -1024,6 +1031,12 @@ int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* ca
     std::vector<rt::BlockDesc> blocks;
     for (int by = 0; by < h; by += 16)
         for (int bx = 0; bx < w; bx += 16) blocks.push_back({x0 + bx, y0 + by, bx, by});
+    // k_cull_ps covers what k_render_ps's launch condition covers: the CPU preset, scenes of
+    // <= 64 * kRenderCullWords triangles (wider scenes would get truncated masks)
+    if (params->preset != RT_PRESET_CPU) return fail(RT_E_UNSUPPORTED, "the primary-ray cull is CPU-preset only");
+    if (scene->dev.n_tri > 64 * rt::kRenderCullWords)
+        return fail(RT_E_UNSUPPORTED, "the primary-ray cull covers scenes of <= %d triangles (this one has %d)",
+                    64 * rt::kRenderCullWords, scene->dev.n_tri);
     rt::RenderLaunch a = make_launch(scene, cam, params);
     if (!a.use_filter) return fail(RT_E_UNSUPPORTED, "no filter records for this scene and camera");
     a.n_blocks = (int)blocks.size();
@@ -1031,8 +1044,9 @@ int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* ca
     a.clip_y1 = y0 + h;
     const int64_t words = (int64_t)a.n_blocks * a.split * 4 * rt::kRenderCullWords;
     if (*n_words < words) {
+        const long long cap = (long long)*n_words;
         *n_words = words;
-        return fail(RT_E_INVALID, "out holds %lld words, %lld needed", (long long)*n_words, (long long)words);
+        return fail(RT_E_INVALID, "out holds %lld words, %lld needed", cap, (long long)words);
     }
     rt::BlockDesc* d_blocks = nullptr;
     hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());

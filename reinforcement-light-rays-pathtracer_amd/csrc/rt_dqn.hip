@@ -840,6 +840,7 @@ __global__ __launch_bounds__(256) void k_nq_image(const DqnLaunch a, const NqRay
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
                           int max_rows, float* q, int ldq, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
+    KernelTimer kt(KT_DQN_MLP, stream);
     // this file's weight-streaming kernel; the weight-stationary one (rt_dqn_ws.hip) when
     // asked (rt_dqn_set_mlp) and the network has the 200-300-200 shape
     if (net.mlp_mode == kMlpStationary && dqn_mlp_ws_fits(net)) {
@@ -878,6 +879,7 @@ static int dqn_mf(const DqnLaunch& a) {
 }
 
 hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
+    KernelTimer kt(KT_DQN_CAMERA, stream);
     switch (dqn_mf(a)) {
         case 1: hipLaunchKernelGGL(k_dqn_camera<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
         case 4: hipLaunchKernelGGL(k_dqn_camera<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
@@ -891,6 +893,7 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
     hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
                                   a.rays.q, a.rays.ldq, stream);
     if (e != hipSuccess) return e;
+    KernelTimer kt(KT_DQN_BOUNCE, stream);
     switch (dqn_mf(a)) {
         case 1: hipLaunchKernelGGL(k_dqn_bounce<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
         case 4: hipLaunchKernelGGL(k_dqn_bounce<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;

@@ -11,6 +11,28 @@
 
 namespace rt {
 
+// Kernel timing (rt_ktime.cpp; rt_ktime_enable / rt_ktime_read in rtmi.h): while enabled,
+// a KernelTimer scope records a HIP event pair on the launch stream around the launches
+// it encloses, per kernel family.  Off by default (one relaxed atomic load per launch).
+enum KtimeKernel {
+    KT_RENDER_PS = 0,   // k_render_ps (CPU preset, the bench kernel)
+    KT_RENDER = 1,      // k_render (GPU preset / no primary phase)
+    KT_SARSA_RENDER = 2,
+    KT_SARSA_APPLY = 3,
+    KT_DQN_MLP = 4,
+    KT_DQN_BOUNCE = 5,
+    KT_DQN_CAMERA = 6,
+    KT_COUNT = 7
+};
+struct KernelTimer {
+    int slot = -1;
+    hipStream_t stream = nullptr;
+    KernelTimer(int kernel, hipStream_t s);
+    ~KernelTimer();
+    KernelTimer(const KernelTimer&) = delete;
+    KernelTimer& operator=(const KernelTimer&) = delete;
+};
+
 // Device layout of one triangle for the hit test: 3 x float4 = 48 B
 //   [0] = {v0.x, v0.y, v0.z, c0}   c0 = e1.y*e2.z - e2.y*e1.z (the determinant
 //                                   minor that depends on the triangle only)

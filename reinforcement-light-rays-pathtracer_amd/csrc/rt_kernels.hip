@@ -898,6 +898,7 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                 if (RT_MF_LDS) mf_lds += (size_t)mf_groups(a.scene.n_tri) * (64 * sizeof(uint4) + 4 * sizeof(float4));
             }
             const dim3 grid((unsigned)(a.n_blocks * a.split));
+            KernelTimer kt(KT_RENDER_PS, stream);
             if (mf_lds > 0 && a.scene.n_tri <= 64)
                 hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 1>), grid, dim3(256), ps_lds + mf_lds, stream, a);
             else if (mf_lds > 0)
@@ -910,6 +911,7 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     const size_t lds = (size_t)(256 / a.split) * (size_t)a.spp * 3 * sizeof(float);
     const dim3 grid((unsigned)(a.n_blocks * a.split));
     const bool steal = PRESET == 1 && lds <= (size_t)RT_STEAL_MAX_LDS;
+    KernelTimer kt(KT_RENDER, stream);
     // the GPU preset's casts on the matrix-core filter: when the scene has the image and
     // the camera is inside its origin bound (camera rays then get real masks)
     const float cb = a.scene.mf_bound;

@@ -1,0 +1,113 @@
+// rt_ktime.cpp — per-kernel-family launch timing with HIP events on the launch stream
+// (bench.py's live kernel durations for the roofline of every workload; rt_ktime_* in
+// rtmi.h).  Disabled: a KernelTimer costs one atomic load.  Enabled: one event pair per
+// timed launch, recycled through a pool; rt_ktime_read waits for the recorded pairs and
+// folds them into per-family totals.
+#include <atomic>
+#include <mutex>
+#include <vector>
+
+#include "../../include/rtmi.h"
+#include "rt_internal.hpp"
+
+namespace rt {
+int set_error(int code, const char* msg);
+}
+
+namespace {
+
+struct Rec {
+    int kernel;
+    hipEvent_t a, b;
+};
+
+std::atomic<bool> g_on{false};
+std::mutex g_mu;
+std::vector<Rec> g_pending;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_pool;
+double g_ms[rt::KT_COUNT];
+int64_t g_n[rt::KT_COUNT];
+int g_errors = 0;
+
+const char* const kNames[rt::KT_COUNT] = {"k_render_ps", "k_render", "k_sarsa_render", "k_sarsa_apply",
+                                          "k_dqn_mlp", "k_dqn_bounce", "k_dqn_camera"};
+
+// fold every recorded pair into the totals (caller holds g_mu)
+void drain(bool keep) {
+    for (const Rec& r : g_pending) {
+        float ms = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            if (keep) {
+                g_ms[r.kernel] += ms;
+                g_n[r.kernel] += 1;
+            }
+        } else {
+            ++g_errors;
+        }
+        g_pool.emplace_back(r.a, r.b);
+    }
+    g_pending.clear();
+}
+
+}  // namespace
+
+namespace rt {
+
+KernelTimer::KernelTimer(int kernel, hipStream_t s) : stream(s) {
+    if (!g_on.load(std::memory_order_relaxed) || kernel < 0 || kernel >= KT_COUNT) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    hipEvent_t a = nullptr, b = nullptr;
+    if (!g_pool.empty()) {
+        a = g_pool.back().first;
+        b = g_pool.back().second;
+        g_pool.pop_back();
+    } else if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+        ++g_errors;
+        return;
+    }
+    if (hipEventRecord(a, s) != hipSuccess) {
+        g_pool.emplace_back(a, b);
+        ++g_errors;
+        return;
+    }
+    slot = (int)g_pending.size();
+    g_pending.push_back(Rec{kernel, a, b});
+}
+
+KernelTimer::~KernelTimer() {
+    if (slot < 0) return;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (slot < (int)g_pending.size() && hipEventRecord(g_pending[(size_t)slot].b, stream) != hipSuccess) ++g_errors;
+}
+
+}  // namespace rt
+
+extern "C" {
+
+int rt_ktime_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    drain(false);
+    for (int k = 0; k < rt::KT_COUNT; ++k) {
+        g_ms[k] = 0.0;
+        g_n[k] = 0;
+    }
+    g_errors = 0;
+    g_on.store(on != 0);
+    return RT_OK;
+}
+
+int rt_ktime_read(int kernel, double* total_ms, int64_t* launches) {
+    if (kernel < 0 || kernel >= rt::KT_COUNT) return rt::set_error(RT_E_INVALID, "bad kernel id");
+    std::lock_guard<std::mutex> lk(g_mu);
+    drain(true);
+    if (g_errors) return rt::set_error(RT_E_HIP, "kernel timing: a HIP event call failed");
+    if (total_ms) *total_ms = g_ms[kernel];
+    if (launches) *launches = g_n[kernel];
+    return RT_OK;
+}
+
+const char* rt_ktime_name(int kernel) {
+    return (kernel >= 0 && kernel < rt::KT_COUNT) ? kNames[kernel] : nullptr;
+}
+
+}  // extern "C"

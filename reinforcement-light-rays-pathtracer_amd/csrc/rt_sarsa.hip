@@ -558,6 +558,7 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 
 hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
     if (a.n_blocks <= 0) return hipSuccess;
+    KernelTimer kt(KT_SARSA_RENDER, stream);
     const float cb = a.scene.mf_bound;
     const bool mf = RT_MF_SARSA && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
@@ -590,6 +591,7 @@ hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream) {
 
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream) {
     if (m.n_vol <= 0) return hipSuccess;
+    KernelTimer kt(KT_SARSA_APPLY, stream);
     hipLaunchKernelGGL(k_sarsa_apply, dim3((unsigned)((m.n_vol + 255) / 256)), dim3(256), 0, stream, m);
     return hipGetLastError();
 }

@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
     const char* out = argc > a ? argv[a++] : "render.bmp";
     Scene scene;
     if (strcmp(argv[2], "cornell") == 0) scene.load_cornell_box_scene();
-    else if (!scene.load_custom_scene(argv[2], kind)) {
+    else if (!scene.load_custom_scene_kind(argv[2], kind)) {
         fprintf(stderr, "cannot load %s\n", argv[2]);
         return 1;
     }

@@ -2,7 +2,7 @@
 //   Material / Triangle / Surface / AreaLight / AreaLightPlane
 //     (CPU/objects/*.h, CPU/lights/*.h, GPU/objects/*.cuh, GPU/lights/*.cuh)
 //   get_cornell_shapes  (CPU/scenes/cornell_box_scene.h:15, GPU/scenes/cornell_box_scene.cu:4)
-//   load_scene          (GPU/objects/object_importer.cuh:15-16)
+//   load_scene          (GPU/objects/object_importer.cuh:15-16; bool lights_in_obj as at HEAD)
 //   Scene               (GPU/scenes/scene.cuh:27-47)
 // The geometry is produced by the C ABI (rt_cornell_geometry, rt_obj_geometry).
 #pragma once
@@ -156,11 +156,12 @@ inline bool get_cornell_shapes(std::vector<Surface>& surfaces, std::vector<AreaL
     return true;
 }
 
-// GPU/objects/object_importer.cu:8 load_scene; `kind` picks the reference's hard-coded
-// material/light block (0 generic, 1 door_room, 2 archway, 3 complex_light_room;
-// lights_in_obj of the reference == kind 3).
-inline bool load_scene(const char* path, std::vector<Surface>& surfaces, std::vector<AreaLight>& lights,
-                       std::vector<float>& vertices, int kind) {
+// The OBJ importer with an explicit scene kind (rt_obj_geometry): the reference's
+// hard-coded material/light blocks, 0 generic (white, no lights), 1 door_room, 2 archway,
+// 3 complex_light_room, plus RT_DOOR_* variant bits << 8 for the door room.  Not a
+// reference name: the reference's own signature is load_scene(..., bool) below.
+inline bool load_scene_kind(const char* path, std::vector<Surface>& surfaces, std::vector<AreaLight>& lights,
+                            std::vector<float>& vertices, int kind) {
     int ns = 0, nl = 0, nn = 0;
     if (rt_obj_geometry(path, kind, nullptr, nullptr, &ns, nullptr, nullptr, nullptr, &nl, nullptr, &nn) != RT_OK)
         return false;
@@ -180,6 +181,23 @@ inline bool load_scene(const char* path, std::vector<Surface>& surfaces, std::ve
     return true;
 }
 
+// GPU/objects/object_importer.cu:8-89 load_scene, the reference's signature and HEAD
+// semantics (:83-88):
+//   lights_in_obj == true  -> build_surfaces_and_lights (:318-412): the complex_light_room
+//                             blocks, the OBJ's own light triangles      == kind 3;
+//   lights_in_obj == false -> build_surfaces (:93-185, HEAD materials: red i > 80, blue
+//                             11 < i < 24) + build_area_lights (:210-314, HEAD: the archway
+//                             lights, emission 8)                         == kind 2.
+// (The reference's `main` calls scene.load_custom_scene("../Models/archway.obj", false),
+// GPU/main.cu:111.)  Returns false when the file cannot be opened or parsed.
+inline bool load_scene(const char* path, std::vector<Surface>& surfaces, std::vector<AreaLight>& lights,
+                       std::vector<float>& vertices, bool lights_in_obj) {
+    return load_scene_kind(path, surfaces, lights, vertices, lights_in_obj ? 3 : 2);
+}
+// Only bool selects the reference's blocks: an int (a scene kind) does not convert silently.
+template <class T>
+bool load_scene(const char*, std::vector<Surface>&, std::vector<AreaLight>&, std::vector<float>&, T) = delete;
+
 // GPU/scenes/scene.cuh:27-47 (owning flat arrays; no new[]/delete[] by the caller)
 struct Scene {
     std::vector<Surface> surfaces;
@@ -191,8 +209,17 @@ struct Scene {
         get_cornell_shapes(surfaces, area_lights, vertices);
         counts();
     }
-    bool load_custom_scene(const char* filename, int kind) {
-        const bool ok = load_scene(filename, surfaces, area_lights, vertices, kind);
+    // GPU/scenes/scene.cu:33-39 (lights_in_obj as in load_scene above)
+    bool load_custom_scene(const char* filename, bool lights_in_obj) {
+        const bool ok = load_scene(filename, surfaces, area_lights, vertices, lights_in_obj);
+        counts();
+        return ok;
+    }
+    template <class T>
+    bool load_custom_scene(const char*, T) = delete;
+    // explicit scene kind (load_scene_kind)
+    bool load_custom_scene_kind(const char* filename, int kind) {
+        const bool ok = load_scene_kind(filename, surfaces, area_lights, vertices, kind);
         counts();
         return ok;
     }

@@ -31,6 +31,16 @@ RT_HIT_NONE = -1
 RT_HIT_TYPE_LIGHT = 1
 RT_HIT_TYPE_SURFACE = 2
 
+# kernel families of rt_ktime_read
+RT_KT_RENDER_PS = 0
+RT_KT_RENDER = 1
+RT_KT_SARSA_RENDER = 2
+RT_KT_SARSA_APPLY = 3
+RT_KT_DQN_MLP = 4
+RT_KT_DQN_BOUNCE = 5
+RT_KT_DQN_CAMERA = 6
+RT_KT_COUNT = 7
+
 # every symbol include/rtmi.h declares (checked by tests/test_abi.py)
 EXPORTS = (
     "rt_params_default", "rt_ctx_create", "rt_ctx_destroy", "rt_last_error",
@@ -50,6 +60,7 @@ EXPORTS = (
     "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
     "rt_dqn_td_targets_device",
     "rt_scene_set_accel", "rt_scene_accel_info", "rt_bvh_check",
+    "rt_ktime_enable", "rt_ktime_read", "rt_ktime_name",
 )
 
 
@@ -161,6 +172,9 @@ def _declare(lib):
                                              _IP, i, i, _P, _P, i, _P]),
         "rt_sarsa_td_device": (i, [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_int64)]),
         "rt_sarsa_apply": (i, [_P, _P]),
+        "rt_ktime_enable": (i, [i]),
+        "rt_ktime_read": (i, [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)]),
+        "rt_ktime_name": (ctypes.c_char_p, [i]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name):  # an older A/B variant build; EXPORTS is checked by tests

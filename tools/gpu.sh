@@ -1,0 +1,82 @@
+#!/bin/bash
+# One parametrised GPU-box runner for every measurement of this repo (replaces the
+# round-2 single-use tools/gpu_*.sh wrappers).  Each step runs under its own time limit;
+# the first failing step ends the call (no GPU work after a fault, abort or timeout).
+#
+#   bash tools/gpu.sh <tag> <step> [<step> ...]
+#
+# steps (one shell word each; quote a step that takes arguments):
+#   smoke                    __graft_entry__.smoke()
+#   tests[:<pytest args>]    pytest -m gpu (default: the whole GPU suite)
+#   bench[:<bench args>]     python bench.py --steps 20 --warmup 3 <args>
+#   kt:<workload>            counter-free rocprofv3 --kernel-trace --stats of the bench
+#                            workload (profiles/<tag>_<workload>_kernel_stats.csv)
+#   pmc:<workload>           PMC passes of the bench workload, summarised into
+#                            profiles/<tag>_<workload>_bench_pmc.json (bench.py's roofline)
+#   ab:<variant,variant,..>  tools/ab_render.py over build/variants/<v> (same image check)
+#   run:<name>:<limit>:<cmd> any command, output in gpurun_out/<tag>/<name>.log
+# Outputs: gpurun_out/<tag>/.
+set -o pipefail
+tag=$1; shift
+cd "$(dirname "$0")/.." || exit 1
+out=gpurun_out/$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$out/$name.log" 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc $(tail -1 "$out/$name.log" | cut -c1-1500)"
+  if [ $rc -ne 0 ]; then tail -25 "$out/$name.log"; echo "[$name] fatal rc=$rc, stopping"; exit $rc; fi
+}
+
+bench_cmd() {  # workload -> the bench command the profiles are taken of
+  local w=$1 steps=${2:-10}
+  case $w in
+    cornell) echo "python3 bench.py --steps $steps --warmup 3 --cpu-seconds 0 --no-parity" ;;
+    door_room_sarsa) echo "python3 bench.py --workload door_room_sarsa --steps 2 --warmup 1 --cpu-seconds 0" ;;
+    archway_dqn) echo "python3 bench.py --workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0" ;;
+    complex_light) echo "python3 bench.py --workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0" ;;
+    *) echo "unknown workload $w" >&2; exit 2 ;;
+  esac
+}
+
+pmc_pass() {  # workload name counters...
+  local w=$1 name=$2; shift 2
+  local d=$out/pmc_$w
+  mkdir -p "$d"
+  timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace -d "$d/$name" -o "$name" --output-format csv \
+      -- $(bench_cmd "$w" 4) > "$d/$name.log" 2>&1
+  local rc=$?
+  echo "[pmc $w $name] rc=$rc"
+  if [ $rc -ne 0 ]; then tail -8 "$d/$name.log"; echo "[pmc $w $name] fatal rc=$rc, stopping"; exit $rc; fi
+}
+
+for step in "$@"; do
+  kind=${step%%:*}; arg=""
+  [ "$kind" != "$step" ] && arg=${step#*:}
+  case $kind in
+    smoke) run smoke 240 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run "tests" 900 python3 -u -m pytest ${arg:-tests} -m gpu -x -q --timeout 240 --timeout-method thread ;;
+    bench) run "bench${arg:+_$(echo "$arg" | tr -c 'a-z0-9' '_')}" 400 python3 -u bench.py --steps 20 --warmup 3 $arg ;;
+    kt)
+      w=${arg:-cornell}
+      run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" 40)
+      cp "$out/kt_$w/kt_kernel_stats.csv" "profiles/${tag}_${w}_kernel_stats.csv" ;;
+    pmc)
+      w=${arg:-cornell}
+      pmc_pass "$w" fetch FETCH_SIZE
+      pmc_pass "$w" write WRITE_SIZE
+      pmc_pass "$w" sq1 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU
+      pmc_pass "$w" sq2 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_BRANCH
+      pmc_pass "$w" sq3 SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_F32 GRBM_GUI_ACTIVE
+      run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" ;;
+    ab) run "ab" 400 python3 -u tools/ab_render.py $(echo "$arg" | tr ',' '\n' | sed 's#^#build/variants/#') --split 64 --rounds 7 ;;
+    run)
+      name=${arg%%:*}; rest=${arg#*:}; lim=${rest%%:*}; cmd=${rest#*:}
+      run "$name" "$lim" bash -c "$cmd" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "[gpu.sh $tag] done"
