@@ -51,8 +51,7 @@ TILE = 32
 VALU_ISSUE_PEAK_G = 1024 * 2.4 / 2.0  # G wave-instructions / s
 VALU_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
-# the committed rocprofv3 profile of the default workload (tools/gpu_bench_pmc.sh)
-PMC_GLOB = os.path.join(ROOT, "profiles", "*_bench_pmc.json")
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 
 WORKLOADS = {
     # name: (scene, preset, sampler, width, height, spp, spp_split, BASELINE config)
@@ -61,6 +60,16 @@ WORKLOADS = {
     "archway_dqn": ("archway", rtmi.RT_PRESET_GPU, "dqn", 1024, 1024, 512, 1, 4),
     "complex_light": ("complex_light_room", rtmi.RT_PRESET_GPU, "uniform", 2048, 2048, 1024, 8, 5),
 }
+# the roofline's dominant kernel per workload: (rt_ktime family timed live, its name in the
+# profiles, bound, object file holding it -- the profile must come from the same object)
+ROOF = {
+    "cornell": (rtmi.RT_KT_RENDER_PS, "k_render_ps<", "valu", "rt_kernels.o"),
+    "complex_light": (rtmi.RT_KT_RENDER, "k_render<", "valu", "rt_kernels.o"),
+    "door_room_sarsa": (rtmi.RT_KT_SARSA_RENDER, "k_sarsa_render<", "valu", "rt_sarsa.o"),
+    "archway_dqn": (rtmi.RT_KT_DQN_MLP, "k_dqn_mlp<", "mfma", "rt_dqn.o"),
+}
+# committed rocprofv3 PMC profiles (tools/gpu.sh pmc:<workload> -> tools/bench_pmc_summary.py)
+PMC_GLOB = os.path.join(ROOT, "profiles", "*_bench_pmc.json")
 
 
 def parse():
@@ -83,10 +92,10 @@ def lib_sha256() -> str:
     return hashlib.sha256(open(rtmi.LIB_PATH, "rb").read()).hexdigest()
 
 
-def render_obj_sha256() -> str:
-    """sha256 of build/rt_kernels.o, or the hash the Makefile wrote beside it (the object
-    file itself is not shipped to the GPU box)."""
-    path = os.path.join(os.path.dirname(rtmi.LIB_PATH), "rt_kernels.o")
+def obj_sha256(name: str) -> str:
+    """sha256 of build/<name>, or the hash the Makefile wrote beside it (object files do not
+    travel to the GPU box)."""
+    path = os.path.join(os.path.dirname(rtmi.LIB_PATH), name)
     if os.path.exists(path):
         return hashlib.sha256(open(path, "rb").read()).hexdigest()
     if os.path.exists(path + ".sha256"):
@@ -94,69 +103,140 @@ def render_obj_sha256() -> str:
     return ""
 
 
-def load_profile():
-    """The newest bench PMC profile of this build: its library hash equals the loaded
-    librtmi.so, or its render-kernel object (build/rt_kernels.o, which holds k_render_ps and
-    nothing the other sources contribute) equals the one this library was linked from."""
-    sha, osha = lib_sha256(), render_obj_sha256()
-    newest = None
-    for path in sorted(glob.glob(PMC_GLOB), key=os.path.getmtime):
+def load_profile(workload: str):
+    """The committed PMC profile of this workload and build: its library hash equals the
+    loaded librtmi.so, or the hash of the object holding the workload's kernels equals the one
+    this library was linked from (a change elsewhere leaves those kernels' code, and so their
+    counters, unchanged).  Among several, the newest by the profile's own creation stamp
+    (then its file name); without a match, the newest of the workload, flagged."""
+    sha, osha = lib_sha256(), obj_sha256(ROOF[workload][3])
+    best = None
+    for path in glob.glob(PMC_GLOB):
         try:
             prof = json.load(open(path))
         except (OSError, ValueError):
             continue
-        newest = (os.path.relpath(path, ROOT), prof)
-        if prof.get("lib_sha256") == sha or (osha and prof.get("render_obj_sha256") == osha):
-            return newest[0], prof, True
-    return (newest[0], newest[1], False) if newest else (None, None, False)
+        if prof.get("workload_name", "cornell") != workload:
+            continue
+        psha = prof.get("obj_sha256") or prof.get("render_obj_sha256")
+        match = prof.get("lib_sha256") == sha or bool(osha and psha == osha)
+        key = (match, prof.get("created", ""), os.path.basename(path))
+        if best is None or key > best[0]:
+            best = (key, os.path.relpath(path, ROOT), prof)
+    return (best[1], best[2], best[0][0]) if best else (None, None, False)
 
 
-def roofline(geom, casts_per_launch: float, kernel_ms: float, default_workload: bool, kernel: str):
-    """VALU-issue roofline of the render kernel (k_render_ps on the default workload).
+def frame_counters(prof, kernel: str, warmup: int, steps: int):
+    """Counters of the kernel per frame: the profiled frames [warmup, warmup + steps) when the
+    profile ran the bench's own frames (learning workloads differ frame to frame), else the
+    mean over its frames; old profiles: the per-dispatch means (one launch per frame)."""
+    ks = [k for k in prof["kernels"] if k.startswith(kernel) or ("::" + kernel) in k]
+    per = {}
+    matched = False
+    for k in ks:
+        e = prof["kernels"][k]
+        fr = e.get("per_frame")
+        if fr:
+            if prof.get("warmup") == warmup and prof.get("steps") == steps and len(fr) >= warmup + steps:
+                sel, matched = fr[warmup:warmup + steps], True
+            else:
+                sel = fr
+            for f in sel:
+                for c, v in f.items():
+                    per[c] = per.get(c, 0.0) + v / len(sel)
+        else:
+            for c, v in e.get("per_dispatch", {}).items():
+                per[c] = per.get(c, 0.0) + v
+            if "hbm_bytes_per_dispatch" in e:
+                per["hbm_bytes"] = per.get("hbm_bytes", 0.0) + e["hbm_bytes_per_dispatch"]
+            if "avg_ns" in e:
+                per["duration_ns"] = per.get("duration_ns", 0.0) + e["avg_ns"]
+    return per, matched
 
-    frac = VALU wave-instructions per launch (SQ_INSTS_VALU of the committed profile of the
-    same build and workload) / (kernel time from this run's HIP events x the chip's issue
-    peak: 1024 SIMDs x one wave-instruction per 2 cycles at 2.4 GHz).  The kernel is bound by
-    VALU issue: its HBM traffic is the 3 MB frame (profile), the triangle records are
-    scalar-cache resident.  Informational: the reference's brute-force flops (71 per
-    ray-triangle test) per second, and the HBM-algorithmic ratio the north
-    star names (36 B per triangle per cast as if streamed: not a bound on this kernel)."""
-    t = kernel_ms * 1e-3
-    n_tri = geom.n_tri
-    path, prof, match = load_profile() if default_workload else (None, None, False)
-    line = {"bound": "valu", "achieved": None, "peak": VALU_ISSUE_PEAK_G, "unit": "G VALU wave-instr/s",
-            "frac": None, "traffic": None, "kernel": kernel,
-            "kernel_ms": round(kernel_ms, 4), "profile": path, "profile_matches_build": match}
-    if prof is not None and match:
-        ks = [k for k in prof["kernels"] if "k_render_ps" in k]
-        valu = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_INSTS_VALU", 0.0) for k in ks)
-        hbm = sum(prof["kernels"][k].get("hbm_bytes_per_dispatch", 0.0) for k in ks)
-        ren = [prof["kernels"][k] for k in ks if "k_render_ps" in k]
-        achieved = valu / t / 1e9
-        line.update({
-            "achieved": round(achieved, 1), "frac": round(achieved / VALU_ISSUE_PEAK_G, 4),
-            "traffic": int(hbm) if hbm else None,
-            "valu_insts_per_launch": valu,
-            "valu_insts_per_cast": round(valu / casts_per_launch, 1),
-            "pmc_clock_ghz": round(ren[0]["clock_ghz"], 3) if ren and "clock_ghz" in ren[0] else None,
-            "pmc_kernel_ms": round(sum(prof["kernels"][k].get("avg_ns", 0.0) for k in ks) * 1e-6, 4),
-        })
-        if line["pmc_clock_ghz"]:
-            line["frac_at_pmc_clock"] = round(valu / (1024 * line["pmc_clock_ghz"] * 1e9 * t / 2.0), 4)
-        # the bounce casts' filter on the matrix cores (v_mfma_f32_16x16x32_bf16): instructions
-        # and the matrix pipe's busy cycles (summed over the 1024 SIMDs) per launch
-        mf = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_INSTS_MFMA", 0.0) for k in ks)
-        mfb = sum(prof["kernels"][k].get("per_dispatch", {}).get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for k in ks)
+
+def roofline(args, geom, params, casts_per_frame: float, kt: dict):
+    """Roofline of the workload's dominant kernel.
+
+    Time: that kernel's launches in the timed steps, HIP events on its own launch stream
+    (rt_ktime_*), per frame.  Work: the committed rocprofv3 profile of the same build and
+    workload (tools/gpu.sh pmc:<workload>), per frame.
+    * VALU-bound kernels (k_render_ps, k_render, k_sarsa_render): frac = VALU
+      wave-instructions / (time x 1024 SIMDs x one wave-instruction per 2 cycles at 2.4 GHz).
+      Their triangle records are scalar-cache resident; HBM traffic is the frame (profile).
+    * The DQN forward k_dqn_mlp (a dense contraction): frac = the reference's algorithmic
+      flops (2 sum(in x out) per ray per NN bounce; rays = the frame's
+      bounce casts, one forward each) / time / the 2.5 PF dense bf16 peak; the executed bf16
+      MFMA flops and the matrix pipe's busy fraction beside it.
+    Informational for the scan kernels: the reference's brute-force flops (71 per
+    ray-triangle test) per second and the north star's HBM-algorithmic ratio (36 B per
+    triangle per cast as if streamed: not a bound on these kernels)."""
+    fam, kname, bound, _ = ROOF[args.workload]
+    steps = args.steps
+    t = kt[fam][0] / steps * 1e-3  # s per frame in the dominant kernel
+    path, prof, match = load_profile(args.workload)
+    line = {"bound": bound, "achieved": None, "frac": None, "traffic": None, "kernel": kname.rstrip("<"),
+            "kernel_ms": round(t * 1e3, 4), "kernel_launches_per_step": kt[fam][1] / steps,
+            "profile": path, "profile_matches_build": match}
+    if bound == "valu":
+        line.update({"peak": VALU_ISSUE_PEAK_G, "unit": "G VALU wave-instr/s"})
+    else:
+        line.update({"peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s"})
+    # every timed kernel family's share of the frame's kernel time
+    tot = sum(v[0] for v in kt.values())
+    line["kernel_ms_per_step"] = {rtmi.ktime_name(k): round(v[0] / steps, 4)
+                                  for k, v in kt.items() if v[1]}
+    line["kernel_share"] = round(kt[fam][0] / tot, 4) if tot else None
+    per, frames_matched = (frame_counters(prof, kname, args.warmup, steps) if prof is not None and match
+                           else ({}, False))
+    if per:
+        line["profile_frames_matched"] = frames_matched
+        hbm = per.get("hbm_bytes")
+        line["traffic"] = int(hbm) if hbm else None
+        if per.get("GRBM_GUI_ACTIVE") and per.get("duration_ns"):
+            line["pmc_clock_ghz"] = round(per["GRBM_GUI_ACTIVE"] / 8.0 / per["duration_ns"], 3)
+            line["pmc_kernel_ms"] = round(per["duration_ns"] * 1e-6, 4)
+        valu = per.get("SQ_INSTS_VALU", 0.0)
+        mf = per.get("SQ_INSTS_MFMA", 0.0)
+        mfb = per.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0)
+        if valu:
+            line["valu_insts_per_step"] = valu
+            line["valu_insts_per_cast"] = round(valu / casts_per_frame, 2)
+            line["valu_issue_frac"] = round(valu / t / 1e9 / VALU_ISSUE_PEAK_G, 4)
         if mf:
-            line["mfma_insts_per_launch"] = mf
-            line["mfma_insts_per_cast"] = round(mf / casts_per_launch, 3)
+            line["mfma_insts_per_step"] = mf
+            line["mfma_insts_per_cast"] = round(mf / casts_per_frame, 3)
+        if mfb:
             line["mfma_busy_frac"] = round(mfb / (1024 * 2.4e9 * t), 4)
-    useful = casts_per_launch * 71.0 * n_tri / t / 1e12
-    line["brute_force_tflops"] = round(useful, 2)
-    line["brute_force_frac_of_fp32"] = round(useful / VALU_PEAK_TFLOPS, 4)
-    b_cast = 36 * n_tri + 32
-    line["hbm_algorithmic_bytes_per_cast"] = b_cast
-    line["hbm_algorithmic_ratio"] = round(casts_per_launch * b_cast / t / 1e9 / HBM_PEAK_GBS, 3)
+        if per.get("SQ_WAVE_CYCLES") and per.get("SQ_WAIT_ANY") is not None:
+            line["wave_cycles_waiting_frac"] = round(per["SQ_WAIT_ANY"] / per["SQ_WAVE_CYCLES"], 4)
+            if per.get("SQ_ACTIVE_INST_ANY"):
+                line["wave_cycles_issuing_frac"] = round(per["SQ_ACTIVE_INST_ANY"] / per["SQ_WAVE_CYCLES"], 4)
+        if bound == "valu" and valu:
+            line["achieved"] = round(valu / t / 1e9, 1)
+            line["frac"] = round(line["achieved"] / VALU_ISSUE_PEAK_G, 4)
+            if line.get("pmc_clock_ghz"):
+                line["frac_at_pmc_clock"] = round(valu / (1024 * line["pmc_clock_ghz"] * 1e9 * t / 2.0), 4)
+        bf16 = per.get("SQ_INSTS_VALU_MFMA_BF16", 0.0)
+        if bound == "mfma" and bf16:
+            line["executed_bf16_tflops"] = round(bf16 * 16384 / t / 1e12, 1)  # 16x16x32 bf16
+            line["executed_frac"] = round(line["executed_bf16_tflops"] / MFMA_BF16_PEAK_TFLOPS, 4)
+    if bound == "mfma":
+        n_in = geom.nn_vertices.size
+        dims = [n_in, 200, 300, 200, 144]
+        flop_ray = 2 * sum(dims[i] * dims[i + 1] for i in range(4))
+        rows = casts_per_frame - params.width * params.height * params.spp  # bounce casts = forwards
+        line["algorithmic_flops_per_ray"] = flop_ray
+        line["forwards_per_step"] = int(rows)
+        line["achieved"] = round(rows * flop_ray / t / 1e12, 1)
+        line["frac"] = round(line["achieved"] / MFMA_BF16_PEAK_TFLOPS, 4)
+    else:
+        n_tri = geom.n_tri
+        useful = casts_per_frame * 71.0 * n_tri / t / 1e12
+        line["brute_force_tflops"] = round(useful, 2)
+        line["brute_force_frac_of_fp32"] = round(useful / VALU_PEAK_TFLOPS, 4)
+        b_cast = 36 * n_tri + 32
+        line["hbm_algorithmic_bytes_per_cast"] = b_cast
+        line["hbm_algorithmic_ratio"] = round(casts_per_frame * b_cast / t / 1e9 / HBM_PEAK_GBS, 3)
     return line
 
 
@@ -314,6 +394,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    rtmi.ktime_enable(True)  # the kernels' own launches, HIP events on their launch stream
     t0 = time.perf_counter()
     for i in range(args.steps):
         pipe.wait(i % 2)  # outside the kernel's event window
@@ -326,8 +407,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kt = rtmi.ktime_read()
+    rtmi.ktime_enable(False)
 
-    kernel_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    frame_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     rank_casts = int(casts.item())
     if world > 1:
         t_max = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -341,8 +424,6 @@ def main():
     frame = pipe.frame(args.steps - 1)
     if rank == 0:
         image = rtmi.tiles.assemble(frame.cpu().numpy(), params.width, params.height, TILE, world)
-        default = args.workload == "cornell" and (params.width, params.height, params.spp, params.spp_split) == (
-            512, 512, 256, 64)
         line = {
             "metric": f"Mrays/sec ({WORKLOADS[args.workload][0]} {params.width}^2 {params.spp}spp ray casts)"
             if params.width == params.height else f"Mrays/sec ({args.workload} ray casts)",
@@ -370,9 +451,8 @@ def main():
                 "triangles": geom.n_tri,
             },
             "ray_casts_per_step": total_casts // args.steps,
-            "roofline": roofline(geom, rank_casts / args.steps, kernel_ms, default, {
-                "uniform": "k_render_ps<0,0,MF>" if params.preset == rtmi.RT_PRESET_CPU else "k_render<1,0,1,steal,MF>",
-                "sarsa": "k_sarsa_render<1,MF> + k_sarsa_apply", "dqn": "k_dqn_mlp + k_dqn_bounce<MF> (wavefront)"}[sampler]),
+            "frame_ms": round(frame_ms, 4),
+            "roofline": roofline(args, geom, params, rank_casts / args.steps, kt),
         }
         if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
             line["parity"] = parity_tiles(ctx, scene, geom, params, cam, cam_pos, image)

@@ -293,3 +293,25 @@ def save_png(path: str, argb: np.ndarray) -> None:
     a = np.ascontiguousarray(argb, np.uint32)
     h, w = a.shape
     check(lib().rt_save_png(path.encode(), a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), w, h))
+
+
+def ktime_enable(on: bool = True) -> None:
+    """Start (clearing the totals) or stop the library's per-kernel launch timing: HIP events
+    on each launch's own stream around k_render_ps, k_render, k_sarsa_render, k_sarsa_apply,
+    k_dqn_mlp, k_dqn_bounce and k_dqn_camera (rt_ktime_enable)."""
+    check(lib().rt_ktime_enable(int(bool(on))))
+
+
+def ktime_read() -> dict:
+    """{family id: (total ms, launches)} since the last ktime_enable(True) (rt_ktime_read;
+    waits for the recorded launches)."""
+    out = {}
+    for fam in range(_lib.RT_KT_COUNT):
+        ms, n = ctypes.c_double(0.0), ctypes.c_int64(0)
+        check(lib().rt_ktime_read(fam, ctypes.byref(ms), ctypes.byref(n)))
+        out[fam] = (ms.value, n.value)
+    return out
+
+
+def ktime_name(fam: int) -> str:
+    return lib().rt_ktime_name(fam).decode()

@@ -1,95 +1,151 @@
 #!/usr/bin/env python3
-"""Summarise tools/gpu_bench_pmc.sh into profiles/<tag>_bench_pmc.json: per kernel of the
-bench workload, the average duration (rocprofv3 --kernel-trace --stats) and every PMC
-counter per dispatch (mean over the dispatches of each pass), plus the sha256 of the
-librtmi.so that was profiled and of its render-kernel object build/rt_kernels.o (bench.py
-accepts the profile when either equals the build it loads: a change elsewhere in the
-library leaves the render kernel's code, and so its counters, unchanged).
+"""Summarise the rocprofv3 PMC passes of one bench workload (tools/gpu.sh pmc:<workload>)
+into the profile bench.py reads for that workload's roofline.
 
-    python tools/bench_pmc_summary.py gpurun_out/<tag>/pmc_<workload> <tag> [<workload>]
+    python tools/bench_pmc_summary.py gpurun_out/<tag>/pmc_<workload> <tag> <workload>
 
-The default workload (cornell) writes profiles/<tag>_bench_pmc.json, the others
-profiles/<tag>_<workload>_bench_pmc.json; bench.py picks the profile whose "workload_name"
-and object hash match the run.
+Output: profiles/<tag>_bench_pmc.json (cornell, the driver's workload) or
+profiles/<tag>_<workload>_bench_pmc.json, holding
+  * the profiled command (tools/gpu.sh bench_cmd: the bench's own command, so its frames are
+    the bench's frames) with its --warmup / --steps,
+  * the sha256 of librtmi.so and of the object file that holds the workload's kernels
+    (bench.py accepts the profile when either equals the build it loads),
+  * per kernel: every counter as the mean per dispatch and as the total per frame (frames
+    split at the workload's marker kernel, in dispatch order), the PMC-pass durations
+    (sq1's kernel trace: the counters slow the clock, so these are not the timing evidence --
+    that is the counter-free kt summary, tools/gpu.sh kt:<workload>), and the clock the pass
+    ran at (GRBM_GUI_ACTIVE / 8 / duration).
 
 HBM bytes (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB per
-dispatch; FETCH_SIZE counts half the bytes of wide streaming reads on gfx950, so
-fetch bytes = 2 x FETCH_SIZE x 1024; write bytes = WRITE_SIZE x 1024.
+dispatch, in separate passes; FETCH_SIZE counts half the bytes of wide streaming reads on
+gfx950, so fetch bytes = 2 x FETCH_SIZE x 1024; write bytes = WRITE_SIZE x 1024.
 """
 import csv
+import datetime
 import glob
 import hashlib
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", "build", "librtmi.so")
 BUILD = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", "build")
-# workload -> (kernel-name substrings kept, the object file that holds those kernels, bench command)
+LIB = os.path.join(BUILD, "librtmi.so")
+
+# workload -> (kernel-name pattern kept, frame-marker pattern, object file of those kernels,
+#              bench arguments: must equal tools/gpu.sh bench_cmd)
 WORKLOADS = {
-    "cornell": (("k_render", "k_cull"), "rt_kernels.o",
-                "bench.py --steps 4 --warmup 3 --cpu-seconds 0 --no-parity (Cornell 512x512, 256 spp, spp_split 64)"),
-    "complex_light": (("k_render",), "rt_kernels.o",
-                      "bench.py --workload complex_light --spp 64 --steps 4 --warmup 1 (2048x2048, 64 spp)"),
-    "door_room_sarsa": (("k_sarsa",), "rt_sarsa.o",
-                        "bench.py --workload door_room_sarsa --steps 4 --warmup 1 (512x512, 256 spp; frames 1-5)"),
-    "archway_dqn": (("k_dqn",), "rt_dqn.o",
-                    "bench.py --workload archway_dqn --spp 16 --steps 4 --warmup 1 (1024x1024, 16 spp)"),
+    "cornell": (r"::k_render_ps<|::k_cull", r"::k_render_ps<", "rt_kernels.o",
+                "--steps 4 --warmup 3 --cpu-seconds 0 --no-parity"),
+    "complex_light": (r"::k_render<", r"::k_render<", "rt_kernels.o",
+                      "--workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity"),
+    "door_room_sarsa": (r"::k_sarsa_", r"::k_sarsa_render<", "rt_sarsa.o",
+                        "--workload door_room_sarsa --steps 4 --warmup 1 --cpu-seconds 0"),
+    "archway_dqn": (r"::k_dqn_", r"::k_dqn_frame_begin", "rt_dqn.o",
+                    "--workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0"),
 }
 
 
-def obj_sha(name):
-    path = os.path.join(BUILD, name)
+def sha(path):
     if os.path.exists(path):
         return hashlib.sha256(open(path, "rb").read()).hexdigest()
     return open(path + ".sha256").read().strip() if os.path.exists(path + ".sha256") else ""
 
 
+def family(name):
+    """'void rt::(anonymous namespace)::k_dqn_bounce<0>(rt::DqnLaunch, int)' -> 'k_dqn_bounce<0>'"""
+    m = re.search(r"::(k_[a-z0-9_]+(<[^>]*>)?)\(", name)
+    return m.group(1) if m else name
+
+
+def frames_of(rows, keep, marker):
+    """rows of one pass in dispatch order -> list of frames, each a list of kept rows"""
+    frames = []
+    for r in rows:
+        if re.search(marker, r["Kernel_Name"]):
+            frames.append([])
+        if frames and re.search(keep, r["Kernel_Name"]):
+            frames[-1].append(r)
+    return frames
+
+
 def main():
+    if sys.argv[1] == "--args":  # the profiled bench arguments of a workload (tools/gpu.sh)
+        print(WORKLOADS[sys.argv[2]][3])
+        return
     d, tag = sys.argv[1], sys.argv[2]
     wl = sys.argv[3] if len(sys.argv) > 3 else "cornell"
-    keys, obj, cmd = WORKLOADS[wl]
-    out = {"tag": tag, "workload_name": wl, "workload": cmd,
-           "lib_sha256": hashlib.sha256(open(LIB, "rb").read()).hexdigest(),
-           "obj": obj, "obj_sha256": obj_sha(obj),
-           "kernels": {}}
-    if wl == "cornell":  # the name earlier bench.py versions match on
+    keep, marker, obj, args = WORKLOADS[wl]
+    w = re.search(r"--warmup (\d+)", args)
+    s = re.search(r"--steps (\d+)", args)
+    out = {"tag": tag, "workload_name": wl, "command": "python3 bench.py " + args,
+           "warmup": int(w.group(1)), "steps": int(s.group(1)),
+           "created": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds"),
+           "lib_sha256": sha(LIB), "obj": obj, "obj_sha256": sha(os.path.join(BUILD, obj)), "kernels": {}}
+    if wl == "cornell":  # the key earlier bench.py versions matched on
         out["render_obj_sha256"] = out["obj_sha256"]
-    # PMC-pass kernel durations (the counters slow the clock: not the timing evidence --
-    # that is the counter-free kt_<workload> summary, tools/gpu.sh kt:<workload>)
+    n_frames = None
+    owner = {}  # counter -> the pass it is taken from (GRBM_GUI_ACTIVE is in two passes)
     for f in sorted(glob.glob(os.path.join(d, "*", "*counter_collection.csv"))):
-        acc, disp = {}, {}
-        for row in csv.DictReader(open(f)):
-            if not any(k in row["Kernel_Name"] for k in keys):
-                continue
-            acc.setdefault((row["Kernel_Name"], row["Counter_Name"]), []).append(float(row["Counter_Value"]))
-        for (k, c), v in acc.items():
-            e = out["kernels"].setdefault(k, {}).setdefault("per_dispatch", {})
-            e[c] = sum(v) / len(v)
-    for f in sorted(glob.glob(os.path.join(d, "*", "*kernel_trace.csv"))):
-        if not f.endswith("sq1_kernel_trace.csv"):
-            continue
-        dur = {}
-        for row in csv.DictReader(open(f)):
-            if any(k in row["Kernel_Name"] for k in keys):
-                dur.setdefault(row["Kernel_Name"], []).append(
-                    float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
-        for k, v in dur.items():
-            out["kernels"].setdefault(k, {}).update({"avg_ns": sum(v) / len(v), "calls": len(v)})
-    for k, e in out["kernels"].items():
-        c = e.get("per_dispatch", {})
+        rows = list(csv.DictReader(open(f)))
+        # one row per (dispatch, counter): group into dispatches
+        disp = {}
+        for r in rows:
+            e = disp.setdefault(int(r["Dispatch_Id"]), {"Kernel_Name": r["Kernel_Name"], "c": {}})
+            e["c"][r["Counter_Name"]] = e["c"].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        ordered = [disp[k] for k in sorted(disp)]
+        frames = frames_of(ordered, keep, marker)
+        n_frames = len(frames) if n_frames is None else min(n_frames, len(frames))
+        for fi, fr in enumerate(frames):
+            for r in fr:
+                k = out["kernels"].setdefault(family(r["Kernel_Name"]), {"per_dispatch": {}, "per_frame": [], "_n": {}})
+                while len(k["per_frame"]) <= fi:
+                    k["per_frame"].append({})
+                for c, v in r["c"].items():
+                    if owner.setdefault(c, f) != f:
+                        continue
+                    k["per_frame"][fi][c] = k["per_frame"][fi].get(c, 0.0) + v
+                    k["per_dispatch"][c] = k["per_dispatch"].get(c, 0.0) + v
+                    k["_n"][c] = k["_n"].get(c, 0) + 1
+    for k in out["kernels"].values():
+        for c in k["per_dispatch"]:
+            k["per_dispatch"][c] /= k["_n"][c]
+        del k["_n"]
+    # durations of the sq1 pass (the one with GRBM_GUI_ACTIVE), per frame
+    for f in glob.glob(os.path.join(d, "sq1", "*kernel_trace.csv")):
+        rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Dispatch_Id"]))
+        for fi, fr in enumerate(frames_of(rows, keep, marker)):
+            for r in fr:
+                k = out["kernels"].get(family(r["Kernel_Name"]))
+                if k is None or fi >= len(k["per_frame"]):
+                    continue
+                ns = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+                k["per_frame"][fi]["duration_ns"] = k["per_frame"][fi].get("duration_ns", 0.0) + ns
+                k.setdefault("_dur", []).append(ns)
+    for k in out["kernels"].values():
+        dur = k.pop("_dur", [])
+        if dur:
+            k["avg_ns"] = sum(dur) / len(dur)
+            k["calls"] = len(dur)
+        c = k["per_dispatch"]
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            e["hbm_bytes_per_dispatch"] = 2.0 * c["FETCH_SIZE"] * 1024.0 + c["WRITE_SIZE"] * 1024.0
-        if "GRBM_GUI_ACTIVE" in c and "avg_ns" in e:
-            e["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8.0 / e["avg_ns"]
+            k["hbm_bytes_per_dispatch"] = 2.0 * c["FETCH_SIZE"] * 1024.0 + c["WRITE_SIZE"] * 1024.0
+        for fr in k["per_frame"]:
+            if "FETCH_SIZE" in fr and "WRITE_SIZE" in fr:
+                fr["hbm_bytes"] = 2.0 * fr["FETCH_SIZE"] * 1024.0 + fr["WRITE_SIZE"] * 1024.0
+            if "GRBM_GUI_ACTIVE" in fr and fr.get("duration_ns"):
+                fr["clock_ghz"] = fr["GRBM_GUI_ACTIVE"] / 8.0 / fr["duration_ns"]
+        if "GRBM_GUI_ACTIVE" in c and "avg_ns" in k:
+            k["clock_ghz"] = c["GRBM_GUI_ACTIVE"] / 8.0 / k["avg_ns"]
         if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
-            e["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0 / 2.0)
+            k["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0 / 2.0)
+    out["frames"] = n_frames or 0
     path = os.path.join(ROOT, "profiles", f"{tag}_bench_pmc.json" if wl == "cornell"
                         else f"{tag}_{wl}_bench_pmc.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
-    print(json.dumps(out, indent=1))
+    print(json.dumps({k: (v if k != "kernels" else sorted(v)) for k, v in out.items()}))
 
 
 if __name__ == "__main__":

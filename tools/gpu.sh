@@ -31,15 +31,12 @@ run() {  # name limit cmd...
   if [ $rc -ne 0 ]; then tail -25 "$out/$name.log"; echo "[$name] fatal rc=$rc, stopping"; exit $rc; fi
 }
 
-bench_cmd() {  # workload -> the bench command the profiles are taken of
-  local w=$1 steps=${2:-10}
-  case $w in
-    cornell) echo "python3 bench.py --steps $steps --warmup 3 --cpu-seconds 0 --no-parity" ;;
-    door_room_sarsa) echo "python3 bench.py --workload door_room_sarsa --steps 2 --warmup 1 --cpu-seconds 0" ;;
-    archway_dqn) echo "python3 bench.py --workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0" ;;
-    complex_light) echo "python3 bench.py --workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0" ;;
-    *) echo "unknown workload $w" >&2; exit 2 ;;
-  esac
+bench_cmd() {  # workload [steps] -> the bench command the profiles are taken of (one source:
+               # tools/bench_pmc_summary.py WORKLOADS); kt runs it with more steps
+  local a
+  a=$(python3 tools/bench_pmc_summary.py --args "$1") || exit 2
+  [ -n "$2" ] && a=$(echo "$a" | sed "s/--steps [0-9]*/--steps $2/")
+  echo "python3 bench.py $a"
 }
 
 pmc_pass() {  # workload name counters...
@@ -47,7 +44,7 @@ pmc_pass() {  # workload name counters...
   local d=$out/pmc_$w
   mkdir -p "$d"
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-trace -d "$d/$name" -o "$name" --output-format csv \
-      -- $(bench_cmd "$w" 4) > "$d/$name.log" 2>&1
+      -- $(bench_cmd "$w") > "$d/$name.log" 2>&1
   local rc=$?
   echo "[pmc $w $name] rc=$rc"
   if [ $rc -ne 0 ]; then tail -8 "$d/$name.log"; echo "[pmc $w $name] fatal rc=$rc, stopping"; exit $rc; fi
@@ -62,7 +59,8 @@ for step in "$@"; do
     bench) run "bench${arg:+_$(echo "$arg" | tr -c 'a-z0-9' '_')}" 400 python3 -u bench.py --steps 20 --warmup 3 $arg ;;
     kt)
       w=${arg:-cornell}
-      run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" 40)
+      steps=20; [ "$w" = cornell ] && steps=40
+      run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" $steps)
       cp "$out/kt_$w/kt_kernel_stats.csv" "profiles/${tag}_${w}_kernel_stats.csv" ;;
     pmc)
       w=${arg:-cornell}
