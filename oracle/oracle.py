@@ -289,6 +289,41 @@ def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False):
     return out, int(casts.value)
 
 
+ORC_Q_FN = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_float),
+                            ctypes.c_void_p)
+
+
+def render_dqn_wave(geom, cam, params, q_fn, rect=None):
+    """orc_render_dqn_wave: the DQN render with every bounce's Q from q_fn(loc (n, 3) float32)
+    -> (n, 144) float32 (e.g. the GPU forward), in wavefront order."""
+    L = lib()
+    L.orc_render_dqn_wave.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.POINTER(OrcCamera),
+                                      ctypes.POINTER(OrcParams), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_int, ORC_Q_FN, ctypes.c_void_p, _FP, ctypes.POINTER(ctypes.c_uint64)]
+    get = (lambda k: geom[k]) if isinstance(geom, dict) else (lambda k: getattr(geom, k))
+    tri = np.ascontiguousarray(np.concatenate([get("tri"), get("light")], 0), np.float32)
+    alb = np.ascontiguousarray(get("albedo"), np.float32)
+    em = np.ascontiguousarray(get("emission"), np.float32)
+    grp = np.ascontiguousarray(get("light_group"), np.int32)
+    x0, y0, w, h = rect if rect is not None else (0, 0, params.width, params.height)
+    out = np.zeros((h, w, 3), np.float32)
+    casts = ctypes.c_uint64(0)
+    calls = []
+
+    def cb(loc_p, n, q_p, _user):
+        loc = np.ctypeslib.as_array(loc_p, shape=(n, 3)).copy()
+        q = np.ascontiguousarray(q_fn(loc), np.float32)
+        assert q.shape == (n, 144)
+        ctypes.memmove(q_p, q.ctypes.data, q.nbytes)
+        calls.append(n)
+
+    fn = ORC_Q_FN(cb)
+    L.orc_render_dqn_wave(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp), get("light").shape[0],
+                          ctypes.byref(cam), ctypes.byref(params), x0, y0, w, h, fn, None, _f(out),
+                          ctypes.byref(casts))
+    return out, int(casts.value), calls
+
+
 KD_DTYPE = np.dtype([("dim", "<i4"), ("leaf", "<i4"), ("left", "<i4"), ("right", "<i4"), ("data", "<f4"),
                      ("px", "<f4"), ("py", "<f4"), ("pz", "<f4"), ("nx", "<f4"), ("ny", "<f4"), ("nz", "<f4"),
                      ("vol", "<i4")])

@@ -1015,6 +1015,88 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
     return 0;
 }
 
+/* The same render in wavefront order with the Q values supplied by the caller: per bounce,
+ * every live path's position goes out in one batch (path order: sample-major, then the
+ * rect's pixels row-major) and q_fn returns their 144 Q values; the sampling, the traces
+ * and the per-pixel sums are orc_render_dqn's (each path's arithmetic does not depend on the
+ * batch, so with the network's own Q this equals orc_render_dqn).  The tests pass the GPU
+ * forward (k_dqn_mlp through rt_dqn_forward) as q_fn: everything downstream of the bf16
+ * GEMM is then checked bit for bit against the device render
+ * (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491). */
+typedef void (*orc_q_fn)(const float *loc, int n, float *q, void *user);
+
+ORC_API int orc_render_dqn_wave(const float *tri, const float *albedo, int n_surf, const float *emission,
+                                const int32_t *light_group, int n_light, const orc_camera *cam,
+                                const orc_params *p, int x0, int y0, int w, int h, orc_q_fn q_fn, void *user,
+                                float *out_rgb, uint64_t *out_casts) {
+    orc_scene sc;
+    scene_init(&sc, tri, albedo, n_surf, emission, light_group, n_light);
+    const float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
+    const float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
+    const int n_pix = w * h, n = n_pix * p->spp;
+    v3 *tp = (v3 *)malloc(sizeof(v3) * (size_t)n), *loc = (v3 *)malloc(sizeof(v3) * (size_t)n);
+    int *tri_i = (int *)malloc(sizeof(int) * (size_t)n), *live = (int *)malloc(sizeof(int) * (size_t)n);
+    float *bl = (float *)malloc(sizeof(float) * 3 * (size_t)n), *bq = (float *)malloc(sizeof(float) * 144 * (size_t)n);
+    uint64_t total_casts = 0;
+    int n_live = 0;
+    for (int r = 0; r < n; r++) {
+        const int s = r / n_pix, pi = r % n_pix;
+        const int px = x0 + pi % w, py = y0 + pi / w;
+        const uint32_t pix = (uint32_t)py * (uint32_t)p->width + (uint32_t)px;
+        float r1, r2;
+        draw2(p->seed, pix, (uint32_t)s, 0u, &r1, &r2);
+        v3 o, d;
+        orc_params pg = *p;
+        pg.preset = 1;
+        camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+        tp[r] = mk(1.0f, 1.0f, 1.0f);
+        loc[r] = o;
+        tri_i[r] = 0;
+        if (dqn_trace(&sc, p, o, d, &loc[r], &tri_i[r], &tp[r], &total_casts)) live[n_live++] = r;
+    }
+    for (int bnc = 1; n_live > 0 && bnc < p->max_bounces; bnc++) {
+        for (int k = 0; k < n_live; k++) {
+            bl[3 * (size_t)k] = loc[live[k]].x;
+            bl[3 * (size_t)k + 1] = loc[live[k]].y;
+            bl[3 * (size_t)k + 2] = loc[live[k]].z;
+        }
+        q_fn(bl, n_live, bq, user);
+        int m = 0;
+        for (int k = 0; k < n_live; k++) {
+            const int r = live[k], s = r / n_pix, pi = r % n_pix;
+            const uint32_t pix = (uint32_t)(y0 + pi / w) * (uint32_t)p->width + (uint32_t)(x0 + pi % w);
+            const float *nn = sc.normal + (size_t)tri_i[r] * 3;
+            v3 dir;
+            const int act = dqn_sample(bq + (size_t)k * 144, mk(nn[0], nn[1], nn[2]), loc[r], p->seed, pix,
+                                       (uint32_t)s, 1u + (uint32_t)bnc, &tp[r], &dir);
+            int alive;
+            if (act < 0) {
+                total_casts++;
+                tp[r] = mk(tp[r].x * p->env_light, tp[r].y * p->env_light, tp[r].z * p->env_light);
+                alive = 0;
+            } else {
+                alive = dqn_trace(&sc, p, loc[r], dir, &loc[r], &tri_i[r], &tp[r], &total_casts);
+            }
+            if (alive) live[m++] = r;
+        }
+        n_live = m;
+    }
+    for (int pi = 0; pi < n_pix; pi++) {
+        v3 acc = mk(0.0f, 0.0f, 0.0f);
+        for (int s = 0; s < p->spp; s++) {
+            const v3 t = tp[(size_t)s * n_pix + pi];
+            acc.x = acc.x + t.x; acc.y = acc.y + t.y; acc.z = acc.z + t.z;
+        }
+        const float fs = (float)p->spp;
+        float *dst = out_rgb + (size_t)pi * 3;
+        dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+    }
+    free(tp); free(loc); free(tri_i); free(live); free(bl); free(bq);
+    free(sc.normal);
+    if (out_casts) *out_casts = total_casts;
+    return 0;
+}
+
 /* ================================================================== */
 /* Expected-SARSA path (BASELINE config 3)                             */
 /* ================================================================== */

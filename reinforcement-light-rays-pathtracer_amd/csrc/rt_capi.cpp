@@ -392,19 +392,24 @@ void bf16_split(double x, uint16_t* hi, uint16_t* lo) {
     *lo = bf16_rne((float)(x - bf16_value(*hi)));
 }
 
-// The four rows of one triangle over the features (d, o', R, 1) and its margins.
-// Error of the matrix-core evaluation of a row against its real value: the split
-// drops at most 3.1 * 2^-16 of sum |f_i b_i| (hi*lo, lo*hi kept; lo*lo and the split
+// The four rows of one triangle over the features (d, o', R, 1), each scaled so that its
+// margin is 1.  Error of the matrix-core evaluation of a row against its real value: the
+// split drops at most 3.1 * 2^-16 of sum |f_i b_i| (hi*lo, lo*hi kept; lo*lo and the split
 // remainders dropped), the fp32 accumulation of the 30 products adds <= 2^-18 of it
-// (measured 5.3 * 2^-24, profiles/probe/r2_mfma_split_probe.log), the rounding of
-// R and o' a few u: under 3.5 * 2^-16 S.  The exact float test is within 16u S = 2^-20 S
+// (measured 5.3 * 2^-24, profiles/probe/r2_mfma_split_probe.log), the rounding of R and o'
+// a few u: under 3.5 * 2^-16 S.  The exact float test is within 16u S = 2^-20 S
 // (build_filter).  The margins are build_filter's at c = 2^-12 >= 4.5x their sum, with
 // |d_i| <= dinf = kMfDirBound, B = mf_bound + max |v0_i| and the t test folded into
 // T' = T - ets A (|o'_i| <= mf_bound + dinf ets_max, ets_max = eps kFiltMaxTScale):
 //   S_A = dinf M,  S_U = 2 dinf B |e2|_1,  S_V = 2 dinf B |e1|_1,  S_T' <= (B + dinf ets_max) M
 //   eA = c S_A + F,  EW = 2 (c S_U + c S_V + eA) + F,  ET = c S_T' + 2 ets_max eA + F
-bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double mf_bound, double rows[4][10],
-                   float4* marg) {
+// Every error bound is relative to the row's own sum of |products|, so it scales with the
+// row: A, U, V are scaled by alpha < 1/EW (W = A - U - V then too) and T' by beta < 1/ET,
+// which puts the barycentric and t margins at (below) 1.  The sign test of A keeps its
+// meaning at the constant 1/2: alpha eA <= 1/2 since EW >= 2 eA, so |A'| > 1/2 implies
+// |A| > eA (a looser test than eA itself: a few more grazing pairs go to the exact phase).
+// The kernel's keep test then needs no per-triangle data (closest_hit_mf, mf_drop).
+bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double mf_bound, double rows[4][10]) {
     const double v0[3] = {P0.x, P0.y, P0.z};
     const double a[3] = {P1.x, P1.y, P1.z};  // e1
     const double b[3] = {P2.x, P2.y, P2.z};  // e2
@@ -438,18 +443,24 @@ bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double 
     const double EW = 2.0 * (c * 2.0 * dinf * B * n2 + c * 2.0 * dinf * B * n1 + eA) + F;
     const double ET = c * (B + dinf * ets_max) * M + 2.0 * ets_max * eA + F;
     if (!(M < ldexp(1.0, 36)) || !(B < ldexp(1.0, 20)) || !std::isfinite(EW) || !std::isfinite(ET)) return false;
-    *marg = make_float4(round_up(eA), round_up(EW), round_up(ET), 0.0f);
+    // (1 - 2^-20: the double rounding of the scale and the products stays below 1)
+    const double alpha = (1.0 / EW) * (1.0 - ldexp(1.0, -20)), beta = (1.0 / ET) * (1.0 - ldexp(1.0, -20));
+    if (!(alpha * eA <= 0.5) || !(alpha * EW < 1.0) || !(beta * ET < 1.0)) return false;
+    for (int k = 0; k < 10; ++k) {
+        rows[0][k] *= alpha;
+        rows[1][k] *= beta;
+        rows[2][k] *= alpha;
+        rows[3][k] *= alpha;
+    }
     return true;
 }
 
-// Device image of the matrix-core filter: frag (8 * rounds groups x 64 lanes x 8 bf16)
-// and marg (8 * rounds groups x 4 slots); layout in rt_internal.hpp.
-bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, std::vector<uint16_t>* frag,
-                    std::vector<float4>* marg) {
+// Device image of the matrix-core filter: frag (8 * rounds groups x 64 lanes x 8 bf16);
+// layout in rt_internal.hpp.
+bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, std::vector<uint16_t>* frag) {
     const int rounds = (n + rt::kMfRound - 1) / rt::kMfRound;
     const size_t groups = (size_t)rounds * rt::kMfGroupsPerRound;
     frag->assign(groups * 64 * 8, 0);
-    marg->assign(groups * 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
     for (int r = 0; r < rounds; ++r) {
         const int base = r * rt::kMfRound;
         const int cnt = std::min(rt::kMfRound, n - base);
@@ -458,11 +469,11 @@ bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, st
             const size_t gi = (size_t)r * rt::kMfGroupsPerRound + g;
             for (int s = 0; s < 4; ++s) {
                 const int tl = s * G + (G - 1 - g);
-                if (tl >= cnt) continue;  // pad slot: zero rows and margins (masked off)
+                if (tl >= cnt) continue;  // pad slot: zero rows (masked off)
                 const int t = base + tl;
                 double rows[4][10];
                 if (!build_mf_rows(isect[(size_t)t * 3], isect[(size_t)t * 3 + 1], isect[(size_t)t * 3 + 2],
-                                   mf_bound, rows, &(*marg)[gi * 4 + s]))
+                                   mf_bound, rows))
                     return false;
                 for (int i = 0; i < 4; ++i) {
                     uint16_t bh[10], bl[10];
@@ -627,8 +638,7 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     // the kernel compares with this float; the margins are built for it
     const double mf_bound = (double)round_up(vmax_scene * (1.0 + ldexp(1.0, -10)) + ldexp(1.0, -10));
     std::vector<uint16_t> mf_frag;
-    std::vector<float4> mf_marg;
-    const bool mf_ok = filt_ok && build_mf_image(isect, n, mf_bound, &mf_frag, &mf_marg);
+    const bool mf_ok = filt_ok && build_mf_image(isect, n, mf_bound, &mf_frag);
     sc->dev.n_surf = n_surf;
     sc->dev.n_tri = n;
     sc->dev.origin_bound = (float)obound;
@@ -638,7 +648,6 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
         if (sc->dev.shade) (void)hipFree(sc->dev.shade);
         if (sc->dev.filt) (void)hipFree(sc->dev.filt);
         if (sc->dev.mf_frag) (void)hipFree(sc->dev.mf_frag);
-        if (sc->dev.mf_marg) (void)hipFree(sc->dev.mf_marg);
         if (sc->dev.code_cpu) (void)hipFree(sc->dev.code_cpu);
         if (sc->dev.code_gpu) (void)hipFree(sc->dev.code_gpu);
         delete sc;
@@ -658,11 +667,8 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     }
     if (e == hipSuccess && mf_ok) {
         e = hipMalloc(&sc->dev.mf_frag, sizeof(uint16_t) * mf_frag.size());
-        if (e == hipSuccess) e = hipMalloc(&sc->dev.mf_marg, sizeof(float4) * mf_marg.size());
         if (e == hipSuccess)
             e = hipMemcpy(sc->dev.mf_frag, mf_frag.data(), sizeof(uint16_t) * mf_frag.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(sc->dev.mf_marg, mf_marg.data(), sizeof(float4) * mf_marg.size(), hipMemcpyHostToDevice);
     }
     if (e != hipSuccess) {
         cleanup();
@@ -683,7 +689,6 @@ int rt_scene_destroy(rt_scene* scene) {
     (void)hipFree(scene->dev.code_gpu);
     if (scene->dev.filt) (void)hipFree(scene->dev.filt);
     if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
-    if (scene->dev.mf_marg) (void)hipFree(scene->dev.mf_marg);
     scene_free_bvh(scene);
     delete scene;
     return RT_OK;

@@ -76,10 +76,11 @@ constexpr float kFiltMaxTScale = 16384.0f;
 // group g of a round holds triangle s G + (G - 1 - g) in slot s = 0..3 (rows 4 s + i,
 // i = A, T', U, V).  Device image per group (index 8 r + g):
 //   frag: 64 lanes x 8 bf16 (lane l: row l & 15, k = 8 (l >> 4) ..), the A operand
-//   marg: 4 slots x {eA, EW, ET, 0}: the margins of the filter at c = 2^-12
-// The margins hold for |d_i| <= kMfDirBound (unit directions), |o_i| <= mf_bound (the
-// scene's box, widened by 2^-10 relative + 2^-10: surface points and the bounce loop's
-// 1e-5 offset) and t_scale <= kFiltMaxTScale; a lane outside keeps every triangle.
+// Each row is scaled so that the filter's margins at c = 2^-12 become the constants 1
+// (U, V, W = A - U - V, T') and 1/2 (|A|, the sign test): build_mf_rows.  The margins hold
+// for |d_i| <= kMfDirBound (unit directions), |o_i| <= mf_bound (the scene's box, widened
+// by 2^-10 relative + 2^-10: surface points and the bounce loop's 1e-5 offset) and
+// t_scale <= kFiltMaxTScale; a lane outside keeps every triangle.
 constexpr int kMfRound = 32;
 constexpr int kMfGroupsPerRound = 8;
 constexpr float kMfDirBound = 1.0009765625f;  // 1 + 2^-10
@@ -122,7 +123,6 @@ struct DeviceScene {
     float4* shade = nullptr;   // n_tri * kShadeF4
     float4* filt = nullptr;    // n_tri * kFiltF4 (nullptr: no filter records for this scene)
     uint4* mf_frag = nullptr;  // matrix-core filter image (above; nullptr: none)
-    float4* mf_marg = nullptr;
     float mf_bound = 0.0f;     // |o_i| bound of the matrix-core margins
     float origin_bound = 0.0f; // |o_i| bound the filter records were built for
     int32_t* code_cpu = nullptr;  // n_tri packed hit codes under hit rule CPU
@@ -164,6 +164,10 @@ struct RenderLaunch {
     unsigned long long* casts;
     uint32_t sample_base;  // first RNG sample index (SARSA: frame * spp); 0 elsewhere
     int use_filter;        // 1: two-phase closest hit (filter records valid for this launch)
+    // k_render<MF> (GPU preset): 1 = camera rays take the wave's primary-ray candidate set
+    // (rt_cull.hpp) instead of the matrix-core filter -- set by the launcher when the camera
+    // lies outside the image's origin bound (every camera ray would keep every triangle)
+    int cam_cull;
     // k_cull_ps (diagnostic): kRenderCullWords 64-bit candidate masks per wave
     // (n_blocks * split * 4 waves); unused by the renders
     unsigned long long* cull;

@@ -109,6 +109,50 @@ __global__ __launch_bounds__(256) void k_intersect_bvh(const DeviceScene s, cons
 // (closest_hit_mf, wave-level: lanes without a live sample take part with no
 // candidates), as the bounce casts of k_render_ps; the launcher picks it when the camera
 // lies inside the image's origin bound (else every camera ray would keep every triangle).
+// the bits of 64-triangle group g that are triangles of an n-triangle scene
+__device__ __forceinline__ uint64_t tri_mask(int n, int g) {
+    const int k = n - 64 * g;
+    return k >= 64 ? ~0ull : (k <= 0 ? 0ull : ((1ull << k) - 1ull));
+}
+
+// The candidate triangles of the wave's camera rays: bit i of cm[i / 64] = triangle i may
+// be the hit of a camera ray through one of the wave's pixels (the pixel rectangle's cull,
+// rect_cull in rt_cull.hpp; wave-uniform).  k_render_ps phase P, k_render<MF> camera rays.
+template <int RULE>
+__device__ __forceinline__ void wave_candidates(const RenderLaunch& a, bool valid, int px, int py, int lane,
+                                                uint64_t* cm) {
+    int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
+    int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        x0 = min(x0, __shfl_xor(x0, off, 64));
+        x1 = max(x1, __shfl_xor(x1, off, 64));
+        y0 = min(y0, __shfl_xor(y0, off, 64));
+        y1 = max(y1, __shfl_xor(y1, off, 64));
+    }
+    const CamRect c = make_cam_rect(a.cam_x, a.cam_y, a.cam_z, a.cos_y, a.sin_y, a.width, a.height, a.t_scale,
+                                    __builtin_amdgcn_readfirstlane(x0), __builtin_amdgcn_readfirstlane(x1),
+                                    __builtin_amdgcn_readfirstlane(y0), __builtin_amdgcn_readfirstlane(y1));
+    const int n_tri = a.scene.n_tri;
+#pragma unroll
+    for (int g = 0; g < kRenderCullWords; ++g) {
+        if (g * 64 >= n_tri) {  // (wave-uniform) no triangle in this word
+            cm[g] = 0ull;
+            continue;
+        }
+        const int i = g * 64 + lane;
+        const bool in_range = i < n_tri;
+#ifdef RT_TIMING_NO_CULL
+        const bool keep = in_range;
+#else
+        // every lane tests a real record (triangle 0 past the end), the range masks after
+        const bool cull = rect_cull<RULE>(a.scene.filt + (size_t)(in_range ? i : 0) * kFiltF4, c);
+        const bool keep = in_range && !cull;
+#endif
+        cm[g] = __ballot(keep) & tri_mask(n_tri, g);
+    }
+}
+
 template <int PRESET, int SAMPLER, int RULE, bool STEAL, bool BVH, int MF = 0>
 #ifndef RT_MIN_WAVES
 #define RT_MIN_WAVES 1
@@ -156,6 +200,9 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
         draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
         camera_ray<PRESET>(a, px, py, r1, r2, &d);
     }
+    // MF with the camera outside the image's bound: camera rays take the wave's cull
+    uint64_t cm[kRenderCullWords] = {0ull, 0ull, 0ull, 0ull};
+    if (MF > 0 && a.cam_cull && __ballot(valid) != 0ull) wave_candidates<RULE>(a, valid, px, py, lane, cm);
 
     for (;;) {
         const bool active = s < s_end;
@@ -163,7 +210,8 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
         Hit h;
         if constexpr (MF > 0) {
             h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active,
-                                                s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats);
+                                                s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats, nullptr, nullptr,
+                                                a.cam_cull ? cm : nullptr, depth == 0);
             if (!active) continue;
         } else {
             if (!active) continue;
@@ -331,9 +379,9 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
 // k_render<0, ...> (oracle/ parity); PRESET 0 paths are 1-3 casts, so about 37% of the
 // casts of the frame move from the full-scene scan to a few exact tests.
 //
-// LDS: per wave and sample slot k, five 64-lane rows (lane-contiguous: conflict-free):
-//   continuing: d.x, d.y, d.z, t, triangle;  ended: L.x, L.y, L.z, -, -1.
-constexpr int kPsFields = 5;
+// LDS: per wave and sample slot k, four 64-lane rows (lane-contiguous: conflict-free):
+//   continuing: the hit point x, y, z, triangle;  ended: L.x, L.y, L.z, -1.
+constexpr int kPsFields = 4;
 
 #ifndef RT_PS_STEAL
 #define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
@@ -344,11 +392,6 @@ __host__ __device__ constexpr int ps_wave_floats(int pc) {
     return pc * kPsFields * 64 + (RT_PS_STEAL ? pc * 32 : 0);
 }
 
-// the bits of 64-triangle group g that are triangles of an n-triangle scene
-__device__ __forceinline__ uint64_t tri_mask(int n, int g) {
-    const int k = n - 64 * g;
-    return k >= 64 ? ~0ull : (k <= 0 ? 0ull : ((1ull << k) - 1ull));
-}
 
 // Candidate masks of the primary-ray phase: wave w of workgroup b writes
 // cull[(b * 4 + w) * kRenderCullWords + g], bit j = triangle 64 g + j may be the hit of a
@@ -357,37 +400,6 @@ __device__ __forceinline__ uint64_t tri_mask(int n, int g) {
 // Candidate masks of the wave's pixel rectangle (the valid lanes' pixels): bit j of
 // cm[g] = triangle 64 g + j may be the hit of a camera ray through the rectangle
 // (rect_cull); never a bit past the scene.  All lanes of the wave take part.
-template <int RULE>
-__device__ __forceinline__ void wave_candidates(const RenderLaunch& a, bool valid, int px, int py, int lane,
-                                                uint64_t* cm) {
-    int x0 = valid ? px : 0x7fffffff, x1 = valid ? px : -1;
-    int y0 = valid ? py : 0x7fffffff, y1 = valid ? py : -1;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        x0 = min(x0, __shfl_xor(x0, off, 64));
-        x1 = max(x1, __shfl_xor(x1, off, 64));
-        y0 = min(y0, __shfl_xor(y0, off, 64));
-        y1 = max(y1, __shfl_xor(y1, off, 64));
-    }
-    const CamRect c = make_cam_rect(a.cam_x, a.cam_y, a.cam_z, a.cos_y, a.sin_y, a.width, a.height, a.t_scale,
-                                    __builtin_amdgcn_readfirstlane(x0), __builtin_amdgcn_readfirstlane(x1),
-                                    __builtin_amdgcn_readfirstlane(y0), __builtin_amdgcn_readfirstlane(y1));
-    const int n_tri = a.scene.n_tri;
-#pragma unroll
-    for (int g = 0; g < kRenderCullWords; ++g) {
-        const int i = g * 64 + lane;
-        const bool in_range = i < n_tri;
-#ifdef RT_TIMING_NO_CULL
-        const bool keep = in_range;
-#else
-        // every lane tests a real record (triangle 0 past the end), the range masks after
-        const bool cull = rect_cull<RULE>(a.scene.filt + (size_t)(in_range ? i : 0) * kFiltF4, c);
-        const bool keep = in_range && !cull;
-#endif
-        cm[g] = __ballot(keep) & tri_mask(n_tri, g);
-    }
-}
-
 // The masks alone, as k_render_ps computes them, into a.cull (wave w of workgroup b at
 // words (b * 4 + w) * kRenderCullWords ..): the diagnostic rt_cull_masks_device.
 template <int RULE>
@@ -461,7 +473,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             }
         }
         n_casts += valid ? 1u : 0u;
-        float v0 = d.x, v1 = d.y, v2 = d.z, v3 = h.t;
+        // a continuing path parks its hit point (the same operations the bounce loop's
+        // shading used to apply to (cam, t, d): D = d t_scale, pos = cam + t D)
+        float v0 = cam.x + h.t * (d.x * a.t_scale), v1 = cam.y + h.t * (d.y * a.t_scale),
+              v2 = cam.z + h.t * (d.z * a.t_scale);
         int code = h.tri;
         if (h.tri < 0) {
             v0 = v1 = v2 = 0.0f;  // PRESET 0: a miss contributes 0
@@ -478,8 +493,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         sl[0 * 64] = v0;
         sl[1 * 64] = v1;
         sl[2 * 64] = v2;
-        sl[3 * 64] = v3;
-        sl[4 * 64] = __int_as_float(code);
+        sl[3 * 64] = __int_as_float(code);
     }
 
     // ---- phase S: bounces ----
@@ -492,9 +506,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     int cur = 0;        // sample of the live path
     int depth = 0;      // surface bounces of the live path so far
     f3 o = cam, d = make3(0.0f, 0.0f, 1.0f);
-    Hit h;
-    h.t = 0.0f;
-    h.tri = 0;
+    f3 pos = cam;       // the live path's surface hit to shade next, and its triangle
+    int hit_tri = 0;
     int f_tri0 = 0;
     float f_cos0 = 0.0f;
 #if RT_PS_STEAL
@@ -506,7 +519,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     uint16_t* const queue = reinterpret_cast<uint16_t*>(wslots + pc * kPsFields * 64);
     int q_total = 0;
     for (int kk = 0; kk < pc; ++kk) {
-        const bool cont = valid && __float_as_int(slots[kk * kPsFields * 64 + 4 * 64]) >= 0;
+        const bool cont = valid && __float_as_int(slots[kk * kPsFields * 64 + 3 * 64]) >= 0;
         const uint64_t m = __ballot(cont);
         if (cont) queue[q_total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)((kk << 6) | lane);
@@ -525,10 +538,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             const uint32_t e = queue[j];
             const int ol = (int)(e & 63u), kk = (int)(e >> 6);
             own = wslots + kk * kPsFields * 64 + ol;
-            d = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
-            h.t = own[3 * 64];
-            h.tri = __float_as_int(own[4 * 64]);
-            o = cam;
+            pos = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
+            hit_tri = __float_as_int(own[3 * 64]);
             depth = 0;
             const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the lane's pixel
             lpix = (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
@@ -542,7 +553,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     auto fetch = [&]() -> bool {
         while (k < pc) {
             const float* sl = slots + k * kPsFields * 64;
-            const int code = __float_as_int(sl[4 * 64]);
+            const int code = __float_as_int(sl[3 * 64]);
             if (code < 0) {
                 acc.x = acc.x + sl[0 * 64];
                 acc.y = acc.y + sl[1 * 64];
@@ -550,10 +561,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
                 ++k;
                 continue;
             }
-            d = make3(sl[0 * 64], sl[1 * 64], sl[2 * 64]);
-            h.t = sl[3 * 64];
-            h.tri = code;
-            o = cam;
+            pos = make3(sl[0 * 64], sl[1 * 64], sl[2 * 64]);
+            hit_tri = code;
             depth = 0;
             cur = chunk * pc + k;
             ++k;
@@ -581,12 +590,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         int s_tri = 0;
         float s_cos = 0.0f;
         if (live) {
-            // shade the live path's surface hit h (depth < max_bounces by construction)
-            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
-            const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
-            const float4 N = shade[h.tri * kShadeF4 + 0];
-            const float4 T = shade[h.tri * kShadeF4 + 1];
-            const float4 B = shade[h.tri * kShadeF4 + 2];
+            // shade the live path's surface hit (depth < max_bounces by construction)
+            const float4 N = shade[hit_tri * kShadeF4 + 0];
+            const float4 T = shade[hit_tri * kShadeF4 + 1];
+            const float4 B = shade[hit_tri * kShadeF4 + 2];
             float r1, r2;
 #if RT_PS_STEAL
             draw2(lpix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
@@ -607,7 +614,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
                                 (sx * B.y + cos_theta * N.y) + sz * T.y,
                                 (sx * B.z + cos_theta * N.z) + sz * T.z);
-            s_tri = h.tri;
+            s_tri = hit_tri;
             s_cos = cos_theta;
             if (depth == 0) {
                 f_tri0 = s_tri;
@@ -623,6 +630,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         const uint64_t tb = __builtin_amdgcn_s_memtime();
         uint64_t tm = tb;
 #endif
+        Hit h;
         if (use_mf)
 #if RT_PROF
             h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl, nullptr, &tm);
@@ -671,7 +679,9 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         } else if (depth == a.max_bounces) {
             // bounces == MAX_RAY_BOUNCES -> vec3(0)
         } else {
-            terminal = false;  // shade h on the next trip
+            terminal = false;  // shade the hit on the next trip
+            pos = make3(o.x + h.t * (d.x * a.t_scale), o.y + h.t * (d.y * a.t_scale), o.z + h.t * (d.z * a.t_scale));
+            hit_tri = h.tri;
         }
         if (terminal) {
 #if RT_PS_STEAL
@@ -764,20 +774,19 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
             float4* li = reinterpret_cast<float4*>(next);
             float4* ls = li + (size_t)n * kIsectF4;
             for (int i = threadIdx.x; i < n * kIsectF4; i += 256) li[i] = a.scene.isect[i];
-            for (int i = threadIdx.x; i < n * kShadeF4; i += 256) ls[i] = a.scene.shade[i];
             ms.isect = li;
-            ms.shade = ls;
-            next = reinterpret_cast<float*>(ls + (size_t)n * kShadeF4);
+            if (RT_PS_SHADE_LDS) {
+                for (int i = threadIdx.x; i < n * kShadeF4; i += 256) ls[i] = a.scene.shade[i];
+                ms.shade = ls;
+            }
+            next = reinterpret_cast<float*>(ls + (RT_PS_SHADE_LDS ? (size_t)n * kShadeF4 : 0));
         }
 #endif
 #if RT_MF_LDS
         const int ng = mf_groups(a.scene.n_tri);
         uint4* lf = reinterpret_cast<uint4*>(next);
-        float4* lm = reinterpret_cast<float4*>(lf + (size_t)ng * 64);
         for (int i = threadIdx.x; i < ng * 64; i += 256) lf[i] = a.scene.mf_frag[i];
-        for (int i = threadIdx.x; i < ng * 4; i += 256) lm[i] = a.scene.mf_marg[i];
         ms.mf_frag = lf;
-        ms.mf_marg = lm;
 #endif
         if (RT_PS_SCENE_LDS || RT_MF_LDS) __syncthreads();
     }
@@ -852,7 +861,7 @@ hipError_t launch_intersect_bvh(const DeviceScene& s, const float* orig, const f
 hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const float* dir, int n, float t_scale,
                                int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
-    if (s.mf_frag == nullptr || s.mf_marg == nullptr || !(t_scale > 0.0f && t_scale <= kFiltMaxTScale))
+    if (s.mf_frag == nullptr || !(t_scale > 0.0f && t_scale <= kFiltMaxTScale))
         return hipErrorInvalidValue;
     const dim3 block(256);
     const dim3 grid((unsigned)((n + 255) / 256));
@@ -865,11 +874,11 @@ hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const fl
     return hipGetLastError();
 }
 
-#ifndef RT_MF_CAM_OUT_MAX_TRI
-#define RT_MF_CAM_OUT_MAX_TRI 0  // > 0: A/B builds (launch_render_t)
-#endif
 #ifndef RT_MF_RENDER
 #define RT_MF_RENDER 1  // 0: the GPU preset's casts on the fp32 filter (A/B builds)
+#endif
+#ifndef RT_CAM_CULL
+#define RT_CAM_CULL 1  // 0: a camera outside the image's bound keeps the fp32 filter (A/B builds)
 #endif
 #ifndef RT_STEAL_MAX_LDS
 #define RT_STEAL_MAX_LDS (64 * 1024)  // sample stealing when its LDS fits (0: never)
@@ -894,8 +903,9 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
             size_t mf_lds = 0;
             if (RT_MF && a.scene.mf_frag != nullptr) {
                 mf_lds = (size_t)4 * kMfWaveFloats * sizeof(float);
-                if (RT_PS_SCENE_LDS) mf_lds += (size_t)a.scene.n_tri * (kIsectF4 + kShadeF4) * sizeof(float4);
-                if (RT_MF_LDS) mf_lds += (size_t)mf_groups(a.scene.n_tri) * (64 * sizeof(uint4) + 4 * sizeof(float4));
+                if (RT_PS_SCENE_LDS)
+                    mf_lds += (size_t)a.scene.n_tri * (kIsectF4 + (RT_PS_SHADE_LDS ? kShadeF4 : 0)) * sizeof(float4);
+                if (RT_MF_LDS) mf_lds += (size_t)mf_groups(a.scene.n_tri) * 64 * sizeof(uint4);
             }
             const dim3 grid((unsigned)(a.n_blocks * a.split));
             KernelTimer kt(KT_RENDER_PS, stream);
@@ -915,29 +925,28 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
     // the GPU preset's casts on the matrix-core filter: when the scene has the image and
     // the camera is inside its origin bound (camera rays then get real masks)
     const float cb = a.scene.mf_bound;
-#if RT_MF_CAM_OUT_MAX_TRI > 0
-    // A/B builds: small scenes take the filter with the camera outside too (its camera
-    // rays keep every triangle: the shared exact phase tests them all)
-    const bool cam_ok = (fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb) ||
-                        a.scene.n_tri <= RT_MF_CAM_OUT_MAX_TRI;
-    const bool mf = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
-                    a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale && cam_ok;
-#else
-    const bool mf = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
-                    a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale &&
-                    fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb;
-#endif
+    const bool mf_base = PRESET == 1 && RT_MF_RENDER && a.use_filter && a.scene.mf_frag != nullptr &&
+                         a.scene.bvh_nodes == nullptr && a.t_scale > 0.0f && a.t_scale <= kFiltMaxTScale;
+    const bool cam_in = fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb && fabsf(a.cam_z) <= cb;
+    // a camera outside the bound: its rays take the wave's primary-ray cull (rt_cull.hpp),
+    // which models the CPU preset's camera -- the GPU preset's is the same ray when the
+    // pitch is 0 (camera_ray: the second rotation is the identity, exactly)
+    const bool cam_cull = !cam_in && RT_CAM_CULL && a.scene.n_tri <= 64 * kRenderCullWords &&
+                          a.cos_x == 1.0f && a.sin_x == 0.0f;
+    const bool mf = mf_base && (cam_in || cam_cull);
     if (mf) {
         if (PRESET == 1) {  // (the CPU preset runs k_render_ps)
+            RenderLaunch b = a;
+            b.cam_cull = cam_in ? 0 : 1;
             const bool one = a.scene.n_tri <= 64;
             if (steal && one)
-                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 1>), grid, dim3(256), lds, stream, a);
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 1>), grid, dim3(256), lds, stream, b);
             else if (steal)
-                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 4>), grid, dim3(256), lds, stream, a);
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 4>), grid, dim3(256), lds, stream, b);
             else if (one)
-                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 1>), grid, dim3(256), 0, stream, a);
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 1>), grid, dim3(256), 0, stream, b);
             else
-                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 4>), grid, dim3(256), 0, stream, a);
+                hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, false, false, 4>), grid, dim3(256), 0, stream, b);
         }
         return;
     }

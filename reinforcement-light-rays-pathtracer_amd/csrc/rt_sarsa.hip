@@ -55,7 +55,14 @@ __device__ __forceinline__ float len3(float x, float y, float z) { return sqrtf(
 // KD descent; a far child is visited when delta^2 < MAX_DIST; leaves need an
 // identical normal; the search starts from volume 0 at the distance of element 0's
 // position (the origin for an internal root).  The stack lives in LDS, one column per
-// lane (st[k * 256]); its depth is bounded by the tree depth (host-checked).
+// lane of the wave's own block (st[k * 64], kd_stack_of); its depth is bounded by the
+// tree depth (host-checked).
+// the k-d stack column of this lane: each wave owns a contiguous kKdStack x 64 block (the
+// exact phase of the matrix-core filter reuses it between searches: k_sarsa_render<MF>)
+__device__ __forceinline__ int* kd_stack_of(int* kd_stack) {
+    return kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64) + ((int)threadIdx.x & 63);
+}
+
 __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
     if (RT_SARSA_NO_KD) return 0;
     const uint4* __restrict__ kd = m.kd4;
@@ -65,7 +72,7 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
     int sp = 1;
     while (sp > 0) {
         --sp;
-        const uint4 nd = kd[st[sp * 256]];
+        const uint4 nd = kd[st[sp * 64]];
         if (nd.w != 0xFFFFFFFFu) {  // leaf
             const float d = len3(__uint_as_float(nd.x) - pos.x, __uint_as_float(nd.y) - pos.y,
                                  __uint_as_float(nd.z) - pos.z);
@@ -82,8 +89,8 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
             const bool near_split = (delta * delta) < m.max_dist;
             const int left = (int)nd.y;
             const int nearc = delta < 0.0f ? left : left + 1;
-            if (near_split) st[(sp++) * 256] = (left + left + 1) - nearc;
-            st[(sp++) * 256] = nearc;
+            if (near_split) st[(sp++) * 64] = (left + left + 1) - nearc;
+            st[(sp++) * 64] = nearc;
         }
     }
     return best;
@@ -285,8 +292,16 @@ __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, 
 // path_trace_reinforcement_iterative (reinforcement_path_tracing.cu:50-120), GPU preset
 // MF > 0: every cast on the matrix-core filter (closest_hit_mf, wave-level; the launcher
 // picks it as launch_render_t does for k_render: image present, camera inside its bound)
+// MF: the exact phase's LDS is the wave's own block of the k-d stack (free between searches;
+// wave_lds_sync orders the two uses), so the workgroup needs the stack's 32 KB only; scenes
+// of <= 64 triangles held to 4 waves per SIMD (<= 128 VGPRs without spills; the 4-block
+// variant would spill there and keeps the compiler's 3 waves).
+#ifndef RT_MF_SARSA_WAVES
+#define RT_MF_SARSA_WAVES 4
+#endif
 template <int RULE, int MF = 0>
-__global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, const SarsaMap m) {
+__global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_render(const RenderLaunch a,
+                                                                                     const SarsaMap m) {
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
     const int part = blockIdx.x & (a.split - 1);
@@ -301,8 +316,9 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
     const int n_surf = a.scene.n_surf;
     const int s_end = (chunk + 1) * a.per_chunk;
     __shared__ int kd_stack[kKdStack * 256];
-    int* const st = kd_stack + threadIdx.x;
-    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
+    int* const st = kd_stack_of(kd_stack);
+    static_assert(kKdStack * 64 >= kMfWaveFloats, "the exact phase's LDS fits a wave's stack block");
+    float* const wl = reinterpret_cast<float*>(kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64));
 
     int s = valid ? chunk * a.per_chunk : s_end;
     int depth = 0;
@@ -321,8 +337,9 @@ __global__ __launch_bounds__(256) void k_sarsa_render(const RenderLaunch a, cons
         if (__ballot(active) == 0ull) break;
         Hit h;
         if constexpr (MF > 0) {
-            h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active,
-                                                s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats);
+            wave_lds_sync();  // the previous search's stack accesses stay before the exact phase
+            h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+            wave_lds_sync();  // and its LDS traffic before the next search
             if (!active) continue;
         } else {
             if (!active) continue;
@@ -540,7 +557,7 @@ __global__ __launch_bounds__(256) void k_sarsa_nearest(const SarsaMap m, const f
     if (i >= n) return;
     const f3 p = make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
     const f3 nr = make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]);
-    out[i] = sarsa_nearest_fast(m, m.use_grid ? sarsa_class_of(m, nr) : -1, p, nr, kd_stack + threadIdx.x);
+    out[i] = sarsa_nearest_fast(m, m.use_grid ? sarsa_class_of(m, nr) : -1, p, nr, kd_stack_of(kd_stack));
 }
 
 }  // namespace

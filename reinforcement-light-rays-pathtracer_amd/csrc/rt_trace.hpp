@@ -384,9 +384,9 @@ __device__ __forceinline__ Hit closest_hit_filtered(const float4* __restrict__ f
 // closest_hit_filtered spends 31 VALU instructions per (ray, triangle) pair, 18 of them
 // the four dot products A, T, U, V.  closest_hit_mf evaluates those on
 // v_mfma_f32_16x16x32_bf16 (features and rows split into bf16 hi + lo, three products
-// per term: rt_internal.hpp, kMfRound) and keeps 11 VALU instructions per pair for
-// the sign fold and the three tests, at margins 16x wider (c = 2^-12, build_mf_rows in
-// rt_capi.cpp) than the fp32 filter's.  Wave-level: every lane of the wave calls it
+// per term: rt_internal.hpp, kMfRound) and keeps 10 VALU instructions per pair for
+// the tests, at margins 16x wider (c = 2^-12) than the fp32 filter's, folded into the
+// rows' scale (build_mf_rows in rt_capi.cpp): no per-triangle margin loads.  Wave-level: every lane of the wave calls it
 // (`active` false: a lane whose result is not used; it gets no candidates).
 typedef __bf16 mf_bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 mf_bf16x2 __attribute__((ext_vector_type(2)));
@@ -414,22 +414,43 @@ __device__ __forceinline__ void mf_transpose(uint32_t& x0, uint32_t& x1, uint32_
     x3 = d[1];
 }
 
+typedef uint32_t mf_u32x4 __attribute__((ext_vector_type(4)));
+
+// A 16-B global load the compiler cannot move or merge (closest_hit_mf's prefetch), and
+// the waits that make its result usable: vmcnt(1) = every load but the newest landed
+// (the other fragment may still be in flight; extra loads of the compiler's only make it
+// stricter), vmcnt(0) = all landed.  The fragments pass through the waits' asm as
+// in/out operands, so no use of them can be scheduled above the wait.  No memory clobber:
+// the image is read-only, and the compiler's own loads need no ordering against these
+// (its waits count only its loads, so ours can only make them wait longer).
+__device__ __forceinline__ mf_u32x4 mf_load(const uint4* p) {
+    mf_u32x4 v;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p));
+    return v;
+}
+__device__ __forceinline__ void mf_wait1(mf_u32x4& v) { asm volatile("s_waitcnt vmcnt(1)" : "+v"(v)); }
+__device__ __forceinline__ void mf_wait0(mf_u32x4& a, mf_u32x4& b) {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b));
+}
+
 __device__ __forceinline__ mf_bf16x8 mf_frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = {a, b, c, d};
     return __builtin_bit_cast(mf_bf16x8, v);
 }
 
-// keep bit (bit 31) of one pair from the row values A, T', U, V and the margins
-__device__ __forceinline__ uint32_t mf_keep(mf_f32x4 q, float4 m) {
-    const uint32_t sg = __float_as_uint(q[0]) & 0x80000000u;
-    const float su = __uint_as_float(__float_as_uint(q[2]) ^ sg);
-    const float sv = __uint_as_float(__float_as_uint(q[3]) ^ sg);
-    const float st = __uint_as_float(__float_as_uint(q[1]) ^ sg);
-    const float aa = fabsf(q[0]);
-    const float w = (aa - su) - sv;
-    const float mn = fminf(fminf(su, sv), w);
-    return keep_bit(m.x - aa, mn + m.y, st + m.z);
+// drop bit (bit 31) of one pair from the scaled row values A, T', U, V (build_mf_rows:
+// margins 1, sign test at 1/2): set iff the exact test must fail, i.e. |A| > 1/2 and one
+// of s U, s V, s W (W = A - U - V), s T' is below -1, s = sign A.  s X + 1 < 0 is tested
+// as the sign of fma(X, A, |A|) = |A| (s X + 1), which one rounding cannot flip (an exact
+// 0 gives +0: keep); W's two subtractions round as the fp32 filter's (aa - su) - sv do.
+__device__ __forceinline__ uint32_t mf_drop(mf_f32x4 q) {
+    const float A = q[0], aa = fabsf(q[0]);
+    const float w = (A - q[2]) - q[3];
+    const float xu = fmaf(q[2], A, aa), xv = fmaf(q[3], A, aa);
+    const float xw = fmaf(w, A, aa), xt = fmaf(q[1], A, aa);
+    const float mn = fminf(fminf(xu, xv), fminf(xw, xt));
+    return __float_as_uint(0.5f - aa) & __float_as_uint(mn);
 }
 
 // groups of the image that hold triangles (all rounds but the last are full)
@@ -565,12 +586,16 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
     }
 }
 
-// s.mf_frag / s.mf_marg may point to a workgroup's LDS copy of the image (k_render_ps);
+// s.mf_frag may point to a workgroup's LDS copy of the image (k_render_ps);
 // wl: the wave's LDS for the shared exact phase (kMfWaveFloats floats)
 // NB: 64-triangle blocks per super-block (1: scenes of <= 64 triangles, fewer registers)
+// ovr (wave-uniform, kRenderCullWords 64-triangle masks) with use_ovr: the lane's candidates
+// are ovr's instead of the filter's (k_render's camera rays: the wave's primary-ray cull,
+// rt_cull.hpp, when the camera lies outside mf_bound); they join the shared exact phase.
 template <int RULE, bool COUNT = false, int NB = 4>
 __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, float t_scale, bool active,
-                                              float* wl, int* n_cand = nullptr, uint64_t* t_mask_end = nullptr) {
+                                              float* wl, int* n_cand = nullptr, uint64_t* t_mask_end = nullptr,
+                                              const uint64_t* ovr = nullptr, bool use_ovr = false) {
     const float nDx = -(d.x * t_scale);
     const float nDy = -(d.y * t_scale);
     const float nDz = -(d.z * t_scale);
@@ -580,9 +605,7 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
     const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     const bool keep_all = !(finite && om <= s.mf_bound && dm <= kMfDirBound);
     const int lane = threadIdx.x & 63;
-    const int slot = lane >> 4;
     const uint4* __restrict__ frag = s.mf_frag;
-    const float4* __restrict__ marg = s.mf_marg;
     const mf_f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
 
     Hit h;
@@ -625,57 +648,58 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
                 const int G = (cnt + 3) >> 2;
                 uint32_t m0 = 0u, m1 = 0u, m2 = 0u, m3 = 0u;
                 const int gi0 = r * kMfGroupsPerRound;
-                // one 4-triangle group: 4 MFMAs (ray blocks 0..3), keep bits shifted in
-                auto group = [&](const uint4 af, const float4 mg) {
-                    const mf_bf16x8 A = mf_frag(af.x, af.y, af.z, af.w);
+                // one 4-triangle group: 4 MFMAs (ray blocks 0..3), drop bits shifted in
+                auto group = [&](const mf_u32x4 af) {
+                    const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
                     const mf_f32x4 q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B0, zero, 0, 0, 0);
                     const mf_f32x4 q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B1, zero, 0, 0, 0);
                     const mf_f32x4 q2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B2, zero, 0, 0, 0);
                     const mf_f32x4 q3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B3, zero, 0, 0, 0);
-                    m0 = __builtin_amdgcn_alignbit(m0, mf_keep(q0, mg), 31);
-                    m1 = __builtin_amdgcn_alignbit(m1, mf_keep(q1, mg), 31);
-                    m2 = __builtin_amdgcn_alignbit(m2, mf_keep(q2, mg), 31);
-                    m3 = __builtin_amdgcn_alignbit(m3, mf_keep(q3, mg), 31);
+                    m0 = __builtin_amdgcn_alignbit(m0, mf_drop(q0), 31);
+                    m1 = __builtin_amdgcn_alignbit(m1, mf_drop(q1), 31);
+                    m2 = __builtin_amdgcn_alignbit(m2, mf_drop(q2), 31);
+                    m3 = __builtin_amdgcn_alignbit(m3, mf_drop(q3), 31);
                 };
 #if RT_MF_PINGPONG
-                // two operand sets in flight, no register copies: group g + 1's loads are
-                // issued before group g's MFMAs (32-bit offsets from the round's base)
+                // two operand sets in flight: group g + 2's fragment is loaded right after
+                // group g's MFMAs have read theirs, a whole group of work before its use.
+                // The loads are inline asm with explicit waits: written as plain loads, the
+                // optimizer proves the prefetched value equals a load at the top of the
+                // next trip and moves it there, waiting on it at once.  mf_wait1 returns
+                // the fragment (tied through the asm), so its MFMAs cannot move above it.
+                // An odd G starts with a pad group (index G < 8: zero rows, so its drop bit
+                // is 0 and lands at bit G of the slot mask, where the next slot's bit 0 is
+                // or-ed in).  The prefetches past the end reload group G - 1 (in range).
                 const uint4* __restrict__ fr = frag + (size_t)gi0 * 64 + lane;
-                const float4* __restrict__ mr = marg + (size_t)gi0 * 4 + slot;
-                // (loads unconditional, clamped to the last group: a redundant reload of it)
-                uint4 fa = fr[0];
-                float4 ma = mr[0];
-                for (int g = 0; g < G; g += 2) {
-                    const int g1 = min(g + 1, G - 1);
-                    const uint4 fb = fr[g1 * 64];
-                    const float4 mb = mr[g1 * 4];
-                    group(fa, ma);
-                    if (g + 1 >= G) break;
-                    const int g2 = min(g + 2, G - 1);
-                    fa = fr[g2 * 64];
-                    ma = mr[g2 * 4];
-                    group(fb, mb);
+                const int gs = -(G & 1);
+                mf_u32x4 fa = mf_load(fr + (gs < 0 ? G : 0) * 64);
+                mf_u32x4 fb = mf_load(fr + (gs + 1) * 64);
+                for (int g = gs; g < G; g += 2) {
+                    const int n2 = min(g + 2, G - 1), n3 = min(g + 3, G - 1);
+                    mf_wait1(fa);
+                    group(fa);
+                    fa = mf_load(fr + n2 * 64);
+                    mf_wait1(fb);
+                    group(fb);
+                    fb = mf_load(fr + n3 * 64);
                 }
+                mf_wait0(fa, fb);  // the last (unused) loads land before their registers are reused
 #else
                 uint4 afn = frag[gi0 * 64 + lane];
-                float4 mgn = marg[gi0 * 4 + slot];
                 for (int g = 0; g < G; ++g) {
                     const uint4 af = afn;
-                    const float4 mg = mgn;
-                    if (g + 1 < G) {  // the next group's operand and margins ahead of this group's work
-                        afn = frag[(gi0 + g + 1) * 64 + lane];
-                        mgn = marg[(gi0 + g + 1) * 4 + slot];
-                    }
-                    group(af, mg);
+                    if (g + 1 < G) afn = frag[(gi0 + g + 1) * 64 + lane];  // the next group's operand ahead
+                    const mf_u32x4 v = {af.x, af.y, af.z, af.w};
+                    group(v);
                 }
 #endif
                 // lane (slot s, ray q) holds m_c for ray 16 c + q; after the transpose lane
                 // (c, q) holds the masks of slots 0..3 of its own ray: bit j of slot s's mask
                 // is triangle s G + j of the round
                 mf_transpose(m0, m1, m2, m3);
-                uint32_t Fr = m0 | (m1 << G) | (m2 << (2 * G)) | (m3 << (3 * G));
+                const uint32_t Dr = m0 | (m1 << G) | (m2 << (2 * G)) | (m3 << (3 * G));  // drop bits
                 const uint32_t all = (cnt >= 32) ? 0xffffffffu : ((1u << cnt) - 1u);
-                Fr = keep_all ? all : (Fr & all);
+                const uint32_t Fr = keep_all ? all : (~Dr & all);
                 const uint64_t Fs = (uint64_t)Fr << (32 * (rr & 1));  // wave-uniform word select
                 const int w = rr >> 1;
                 F0 |= (w == 0) ? Fs : 0ull;
@@ -693,7 +717,11 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
         for (int w = 0; w < NB; ++w) {
             const int tri0 = sb + 64 * w;
             if (tri0 >= n_tri) break;
-            const uint64_t Fw = active ? (w == 0 ? F0 : w == 1 ? F1 : w == 2 ? F2 : F3) : 0ull;
+            uint64_t Fw = active ? (w == 0 ? F0 : w == 1 ? F1 : w == 2 ? F2 : F3) : 0ull;
+            if (ovr != nullptr) {
+                const int g = (sb >> 6) + w;
+                Fw = use_ovr ? ((active && g < 4) ? ovr[g < 4 ? g : 0] : 0ull) : Fw;
+            }
             if (COUNT) *n_cand += __builtin_popcountll(Fw);
 #if RT_MF_COOP
             mf_exact_wave<RULE>(s.isect, tri0, Fw, o, nDx, nDy, nDz, wl, lane, h);
@@ -718,6 +746,9 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
 #endif
 #ifndef RT_PS_SCENE_LDS
 #define RT_PS_SCENE_LDS 1  // k_render_ps<MF>: the scene's isect/shade records in LDS (0: global)
+#endif
+#ifndef RT_PS_SHADE_LDS
+#define RT_PS_SHADE_LDS 1  // 0: with RT_PS_SCENE_LDS, only the isect records in LDS (shading from L1/L2)
 #endif
 #ifndef RT_MF_LDS
 #define RT_MF_LDS 0  // 1: k_render_ps reads the image from a workgroup copy in LDS (0: global)

@@ -1,11 +1,14 @@
 """Multi-GPU frame assembly: one process per GPU, image tiles dealt to the
-ranks by diagonals (rtmi.tiles: tile (tx, ty) -> rank (tx + ty) mod P), one all-gather of the equal-sized per-rank tile
-buffers over RCCL (backend "nccl" on ROCm; "gloo" for CPU tests).
+ranks by diagonals (rtmi.tiles: tile (tx, ty) -> rank (tx + ty) mod P), one gather of the
+equal-sized per-rank tile buffers to rank 0 over RCCL (backend "nccl" on ROCm: ncclSend /
+ncclRecv pairs; "gloo" for CPU tests).  Only rank 0 consumes the frame (the SDL frame
+buffer of the reference's loop), so the other ranks receive nothing: an all-gather would
+move P times the bytes (2048^2 on 8 GPUs: 44 MB into every rank instead of 6.3 MB per
+rank into one).
 
 Data path per frame: rank r renders its tiles
-into out[k_r, T, T, 3] -> all_gather_into_tensor -> gathered[P, k_r, T, T, 3]
--> rtmi.tiles.assemble on the consumer.  Message per rank = k_r*T*T*12 B
-(512^2 frame on 8 GPUs: 393 KB per rank).
+into out[k, T, T, 3] -> gather(dst=0) -> gathered[P, k, T, T, 3] on rank 0
+-> rtmi.tiles.assemble.  Message per rank = k*T*T*12 B (512^2 frame on 8 GPUs: 393 KB).
 """
 from __future__ import annotations
 
@@ -13,24 +16,25 @@ import torch
 import torch.distributed as dist
 
 
-def gather_tiles(out: torch.Tensor, gathered: torch.Tensor, async_op: bool = False):
-    """All-gather the per-rank tile buffers (out: [k, T, T, 3]) into
-    gathered: [world, k, T, T, 3].  async_op: return the collective's work handle
-    (RCCL runs on its own stream after the work already queued on the current one;
-    work.wait() makes the current stream wait for it) so the next frame's render
-    overlaps the exchange; None when there is nothing to wait for."""
+def gather_tiles(out: torch.Tensor, gathered, async_op: bool = False, dst: int = 0):
+    """Gather the per-rank tile buffers (out: [k, T, T, 3]) into gathered: [world, k, T, T, 3]
+    on rank `dst` (other ranks pass gathered = None and receive nothing).  async_op: return
+    the collective's work handle (RCCL runs on its own stream after the work already queued
+    on the current one; work.wait() makes the current stream wait for it) so the next
+    frame's render overlaps the exchange; None when there is nothing to wait for."""
     world = dist.get_world_size() if dist.is_initialized() else 1
     if world == 1:
         gathered[0].copy_(out)
         return None if async_op else gathered
-    work = dist.all_gather_into_tensor(gathered.view(world * out.shape[0], *out.shape[1:]), out,
-                                       async_op=async_op)
+    root = dist.get_rank() == dst
+    glist = list(gathered.unbind(0)) if root else None
+    work = dist.gather(out, gather_list=glist, dst=dst, async_op=async_op)
     return work if async_op else gathered
 
 
 class FramePipeline:
     """Two frame buffers per rank: frame i renders into buffer i % 2 while frame i-1
-    is all-gathered from the other one (bench.py).  `render(out)` queues one frame's
+    is gathered to rank 0 from the other one (bench.py).  `render(out)` queues one frame's
     render into `out` ([k, T, T, 3]) on the current stream; a buffer is rendered into
     again only after its previous gather completed (work.wait() orders the current
     stream after the collective -- a host wait on gloo)."""
@@ -39,8 +43,10 @@ class FramePipeline:
         self.render = render
         self.world = world
         self.outs = [torch.zeros(shape, dtype=torch.float32, device=device) for _ in range(2)]
+        self.root = world == 1 or dist.get_rank() == 0
+        # the assembled frames live on rank 0 only
         self.gathered = [torch.empty((world,) + tuple(shape), dtype=torch.float32, device=device)
-                         for _ in range(2)]
+                         if self.root and world > 1 else None for _ in range(2)]
         self.pending = [None, None]
 
     def wait(self, b: int) -> None:
@@ -63,7 +69,8 @@ class FramePipeline:
             self.wait(b)
 
     def frame(self, i: int) -> torch.Tensor:
-        """[world, k, T, T, 3] tiles of frame i (after drain(), for the last two frames)."""
+        """[world, k, T, T, 3] tiles of frame i on rank 0 (after drain(), for the last two
+        frames); None on the other ranks."""
         b = i % 2
         return self.outs[b][None] if self.world == 1 else self.gathered[b]
 

@@ -180,6 +180,46 @@ def test_config4_archway_dqn_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx):
     assert rtmi_mod.metrics.mape_f(ref, img) <= noise, (rtmi_mod.metrics.mape_f(ref, img), noise)
 
 
+def test_oracle_wavefront_render_equals_per_path(rtmi_mod, oracle_mod):
+    """orc_render_dqn_wave fed by the restatement's own bf16 forward is orc_render_dqn bit for
+    bit: the wavefront order and the batched Q change nothing (CPU, no GPU)."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=2)
+    rect = (480, 480, 12, 10)
+    ocam = oracle_mod.camera(rtmi_mod.CAMERAS["archway"])
+    op = oracle_mod.params_from(p)
+    ref, rc = oracle_mod.render_dqn(g, W, b, g.nn_vertices, ocam, op, rect, bf16=True)
+    got, gc, calls = oracle_mod.render_dqn_wave(
+        g, ocam, op, lambda loc: oracle_mod.dqn_forward(W, b, g.nn_vertices, loc, bf16=True), rect)
+    assert gc == rc and np.array_equal(got.view(np.uint32), ref.view(np.uint32))
+    assert len(calls) > 10 and calls[0] <= 12 * 10 * 2
+
+
+@pytest.mark.gpu
+def test_config4_bit_exact_downstream_of_forward(rtmi_mod, oracle_mod, gpu_ctx):
+    """BASELINE config 4 (archway, 918 inputs, 80 bounces, a 64x64 window of the 1024x1024
+    frame, 4 spp) bit for bit in image and ray casts: the restatement's trace, Q.cos sampler
+    and sums (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491;
+    importance_sample_direction, nn_rendering_helpers.cu:391-489) run on the Q values of the
+    device forward itself (k_dqn_mlp via rt_dqn_forward, the same kernel the render uses).
+    The only stage left out is the bf16 GEMM, gated on its own by test_forward_matches_oracle."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=4)
+    assert p.max_bounces == 80
+    rect = (448, 448, 64, 64)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["archway"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        img, casts = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+        ref, rc, calls = oracle_mod.render_dqn_wave(g, oracle_mod.camera(rtmi_mod.CAMERAS["archway"]),
+                                                    oracle_mod.params_from(p), net.forward, rect)
+    assert len(calls) > 20
+    assert casts == rc, (casts, rc)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), \
+        int((img.view(np.uint32) != ref.view(np.uint32)).sum())
+
+
 @pytest.mark.gpu
 def test_config4_full_frame_properties(rtmi_mod, gpu_ctx):
     """The whole 1024x1024 config-4 frame (2 spp): deterministic, the tile-list render equals

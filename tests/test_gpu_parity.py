@@ -207,6 +207,51 @@ def test_full_size_properties(rtmi_mod, oracle_mod, gpu_ctx):
     assert np.array_equal(win, ref)
 
 
+def test_config5_rank_tile_sets_assemble_to_single_gpu_frame(rtmi_mod, oracle_mod, gpu_ctx):
+    """BASELINE config 5 at its full size on one GPU: complex_light_room 2048x2048, GPU-engine
+    preset (80 bounces), 8 spp at the bench's spp_split 8, rendered through
+    render_tiles_device once per rank tile set of the P = 8 partition (rtmi.tiles: 32x32
+    tiles dealt by diagonals) and assembled: bit-identical to the single-rank frame, the
+    ranks' ray casts sum to its casts, and two tiles bit-exact against the CPU
+    restatement.  This is the multi-GPU data path minus the RCCL gather (which moves the
+    bytes unchanged: tests/test_tiles_dist.py)."""
+    torch = pytest.importorskip("torch")
+    geom = rtmi_mod.obj_geometry(os.path.join(MODELS, "complex_light_room.obj"), "complex_light_room")
+    W = H = 2048
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=W, height=H, spp=8, spp_split=8)
+    assert p.max_bounces == 80
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["complex_light_room"])
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def render_set(sc, tiles):
+        out = torch.zeros((len(tiles), 32, 32, 3), dtype=torch.float32, device="cuda")
+        casts = torch.zeros(1, dtype=torch.int64, device="cuda")
+        rtmi_mod.render_tiles_device(gpu_ctx, sc, cam, p, tiles, 32, out.data_ptr(), casts.data_ptr(), stream)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), int(casts.item())
+
+    with rtmi_mod.Scene(gpu_ctx, geom) as sc:
+        one, casts1 = render_set(sc, rtmi_mod.tiles.rank_tiles(W, H, 32, 0, 1))
+        k = rtmi_mod.tiles.tiles_per_rank(W, H, 32, 8)
+        gathered = np.zeros((8, k, 32, 32, 3), np.float32)
+        total = 0
+        for r in range(8):
+            n_real = rtmi_mod.tiles.rank_tile_count(W, H, 32, r, 8)
+            tiles = rtmi_mod.tiles.rank_tiles(W, H, 32, r, 8)[:n_real]  # real tiles only: casts add up
+            gathered[r, :n_real], c = render_set(sc, tiles)
+            total += c
+    img1 = rtmi_mod.tiles.assemble(one[None], W, H, 32, 1)
+    img8 = rtmi_mod.tiles.assemble(gathered, W, H, 32, 8)
+    assert np.array_equal(img1.view(np.uint32), img8.view(np.uint32))
+    assert total == casts1
+    assert np.isfinite(img1).all() and img1.mean() > 0
+    assert 20.0 < casts1 / (W * H * 8) < 60.0
+    ocam = oracle_mod.camera(rtmi_mod.CAMERAS["complex_light_room"])
+    for (x, y) in [(1024, 1024), (320, 1600)]:
+        ref, _ = oracle_mod.render(geom, ocam, oracle_mod.params_from(p), (x, y, 32, 32))
+        assert np.array_equal(img8[y:y + 32, x:x + 32].view(np.uint32), ref.view(np.uint32)), (x, y)
+
+
 def test_config1_gpu_vs_reference_sequential(rtmi_mod, oracle_mod, gpu_ctx):
     """SURVEY.md §8(c) gate 3 on BASELINE config 1 (Cornell 256^2, 4 spp, CPU preset):
     the GPU frame (Philox stream) against the CPU engine's own sampling order and glibc

@@ -105,7 +105,7 @@ def _pipe_worker(rank, world, port, q):
     def render(out):
         f = state["frame"]
         b = f % 2
-        if f >= 2:  # the gather of frame f-2 from this buffer completed before the re-render
+        if f >= 2 and rank == 0:  # the gather of frame f-2 from this buffer completed before the re-render
             for r in range(world):
                 state["ok"] &= bool(torch.all(pipe.gathered[b][r] == val(r, f - 2)))
         out.fill_(val(rank, f))
@@ -117,8 +117,11 @@ def _pipe_worker(rank, world, port, q):
         pipe.gather_frame(pipe.render_frame(f))
     pipe.drain()
     for f in (frames - 2, frames - 1):
-        for r in range(world):
-            state["ok"] &= bool(torch.all(pipe.frame(f)[r] == val(r, f)))
+        if rank == 0:
+            for r in range(world):
+                state["ok"] &= bool(torch.all(pipe.frame(f)[r] == val(r, f)))
+        else:  # a gather to rank 0: nothing is received elsewhere
+            state["ok"] &= pipe.frame(f) is None
     q.put(state["ok"])
     dist.barrier()
     dist.destroy_process_group()

@@ -2,7 +2,7 @@
 """Summarise the rocprofv3 PMC passes of one bench workload (tools/gpu.sh pmc:<workload>)
 into the profile bench.py reads for that workload's roofline.
 
-    python tools/bench_pmc_summary.py gpurun_out/<tag>/pmc_<workload> <tag> <workload>
+    python tools/bench_pmc_summary.py gpurun_out/<tag>/pmc_<workload> <tag> <workload> [out_dir]
 
 Output: profiles/<tag>_bench_pmc.json (cornell, the driver's workload) or
 profiles/<tag>_<workload>_bench_pmc.json, holding
@@ -141,8 +141,11 @@ def main():
         if "SQ_INSTS_VALU" in c and "GRBM_GUI_ACTIVE" in c:
             k["valu_issue_frac"] = c["SQ_INSTS_VALU"] / (1024.0 * c["GRBM_GUI_ACTIVE"] / 8.0 / 2.0)
     out["frames"] = n_frames or 0
-    path = os.path.join(ROOT, "profiles", f"{tag}_bench_pmc.json" if wl == "cornell"
-                        else f"{tag}_{wl}_bench_pmc.json")
+    # (on the GPU box: into gpurun_out/<tag>/profiles/, which gpurun copies back; tools/gpu.sh
+    # collect:<tag> moves it to profiles/ here)
+    odir = sys.argv[4] if len(sys.argv) > 4 else os.path.join(ROOT, "profiles")
+    os.makedirs(odir, exist_ok=True)
+    path = os.path.join(odir, f"{tag}_bench_pmc.json" if wl == "cornell" else f"{tag}_{wl}_bench_pmc.json")
     with open(path, "w") as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps({k: (v if k != "kernels" else sorted(v)) for k, v in out.items()}))

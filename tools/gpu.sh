@@ -15,7 +15,9 @@
 #                            profiles/<tag>_<workload>_bench_pmc.json (bench.py's roofline)
 #   ab:<variant,variant,..>  tools/ab_render.py over build/variants/<v> (same image check)
 #   run:<name>:<limit>:<cmd> any command, output in gpurun_out/<tag>/<name>.log
-# Outputs: gpurun_out/<tag>/.
+# Outputs: gpurun_out/<tag>/ (gpurun copies only gpurun_out/ back); the summaries meant for
+# profiles/ go to gpurun_out/<tag>/profiles/.  Here, without a GPU:
+#   bash tools/gpu.sh <tag> collect      copies them into profiles/
 set -o pipefail
 tag=$1; shift
 cd "$(dirname "$0")/.." || exit 1
@@ -61,7 +63,8 @@ for step in "$@"; do
       w=${arg:-cornell}
       steps=20; [ "$w" = cornell ] && steps=40
       run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" $steps)
-      cp "$out/kt_$w/kt_kernel_stats.csv" "profiles/${tag}_${w}_kernel_stats.csv" ;;
+      mkdir -p "$out/profiles"
+      cp "$out/kt_$w/kt_kernel_stats.csv" "$out/profiles/${tag}_${w}_kernel_stats.csv" ;;
     pmc)
       w=${arg:-cornell}
       pmc_pass "$w" fetch FETCH_SIZE
@@ -69,7 +72,11 @@ for step in "$@"; do
       pmc_pass "$w" sq1 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU
       pmc_pass "$w" sq2 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_BRANCH
       pmc_pass "$w" sq3 SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_F32 GRBM_GUI_ACTIVE
-      run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" ;;
+      run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" "$out/profiles" ;;
+    collect)
+      mkdir -p profiles
+      for f in "$out"/profiles/*; do [ -e "$f" ] && cp -v "$f" profiles/; done
+      for f in "$out"/smoke.log "$out"/tests.log "$out"/bench*.log; do [ -e "$f" ] && cp "$f" "profiles/${tag}_$(basename "$f")"; done ;;
     ab) run "ab" 400 python3 -u tools/ab_render.py $(echo "$arg" | tr ',' '\n' | sed 's#^#build/variants/#') --split 64 --rounds 7 ;;
     run)
       name=${arg%%:*}; rest=${arg#*:}; lim=${rest%%:*}; cmd=${rest#*:}
