@@ -405,11 +405,12 @@ void bf16_split(double x, uint16_t* hi, uint16_t* lo) {
 //   eA = c S_A + F,  EW = 2 (c S_U + c S_V + eA) + F,  ET = c S_T' + 2 ets_max eA + F
 // Every error bound is relative to the row's own sum of |products|, so it scales with the
 // row: A, U, V are scaled by alpha < 1/EW (W = A - U - V then too) and T' by beta < 1/ET,
-// which puts the barycentric and t margins at (below) 1.  The sign test of A keeps its
-// meaning at the constant 1/2: alpha eA <= 1/2 since EW >= 2 eA, so |A'| > 1/2 implies
-// |A| > eA (a looser test than eA itself: a few more grazing pairs go to the exact phase).
-// The kernel's keep test then needs no per-triangle data (closest_hit_mf, mf_drop).
-bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double mf_bound, double rows[4][10]) {
+// which puts the barycentric and t margins at (below) 1.  The sign test of A keeps its own
+// threshold *rho >= alpha eA (<= 1/2, since EW >= 2 eA): one float per triangle, carried in
+// the fragment's unused K entries (build_mf_image; closest_hit_mf, mf_drop).  A constant 1/2 in its place doubled
+// the exact tests on complex_light_room, whose small triangles have eA << EW.
+bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double mf_bound, double rows[4][10],
+                   float* rho) {
     const double v0[3] = {P0.x, P0.y, P0.z};
     const double a[3] = {P1.x, P1.y, P1.z};  // e1
     const double b[3] = {P2.x, P2.y, P2.z};  // e2
@@ -446,6 +447,7 @@ bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double 
     // (1 - 2^-20: the double rounding of the scale and the products stays below 1)
     const double alpha = (1.0 / EW) * (1.0 - ldexp(1.0, -20)), beta = (1.0 / ET) * (1.0 - ldexp(1.0, -20));
     if (!(alpha * eA <= 0.5) || !(alpha * EW < 1.0) || !(beta * ET < 1.0)) return false;
+    *rho = round_up(alpha * eA * (1.0 + ldexp(1.0, -20)));
     for (int k = 0; k < 10; ++k) {
         rows[0][k] *= alpha;
         rows[1][k] *= beta;
@@ -455,12 +457,14 @@ bool build_mf_rows(const float4& P0, const float4& P1, const float4& P2, double 
     return true;
 }
 
-// Device image of the matrix-core filter: frag (8 * rounds groups x 64 lanes x 8 bf16);
-// layout in rt_internal.hpp.
-bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, std::vector<uint16_t>* frag) {
+// Device image of the matrix-core filter: frag (8 * rounds groups x 64 lanes x 8 bf16) and
+// rho (8 * rounds groups x 4 slots); layout in rt_internal.hpp.
+bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, std::vector<uint16_t>* frag,
+                    std::vector<float>* rho) {
     const int rounds = (n + rt::kMfRound - 1) / rt::kMfRound;
     const size_t groups = (size_t)rounds * rt::kMfGroupsPerRound;
     frag->assign(groups * 64 * 8, 0);
+    rho->assign(groups * 4, 0.0f);
     for (int r = 0; r < rounds; ++r) {
         const int base = r * rt::kMfRound;
         const int cnt = std::min(rt::kMfRound, n - base);
@@ -473,7 +477,7 @@ bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, st
                 const int t = base + tl;
                 double rows[4][10];
                 if (!build_mf_rows(isect[(size_t)t * 3], isect[(size_t)t * 3 + 1], isect[(size_t)t * 3 + 2],
-                                   mf_bound, rows))
+                                   mf_bound, rows, &(*rho)[gi * 4 + s]))
                     return false;
                 for (int i = 0; i < 4; ++i) {
                     uint16_t bh[10], bl[10];
@@ -489,7 +493,21 @@ bool build_mf_image(const std::vector<float4>& isect, int n, double mf_bound, st
                         for (int j = 0; j < 8; ++j) (*frag)[(gi * 64 + lane) * 8 + j] = kv[8 * p + j];
                     }
                 }
+                // the slot's sign-test threshold rides in the fragment's unused k = 30, 31 of
+                // row 4 s (lane 48 + 4 s, its 4th dword; the ray operand is 0 there, so the
+                // MFMA ignores it): closest_hit_mf reads it with v_readlane
+                uint32_t rb;
+                memcpy(&rb, &(*rho)[gi * 4 + s], 4);
+                (*frag)[(gi * 64 + 48 + 4 * s) * 8 + 6] = (uint16_t)(rb & 0xffffu);
+                (*frag)[(gi * 64 + 48 + 4 * s) * 8 + 7] = (uint16_t)(rb >> 16);
             }
+            // and the group's largest threshold (lane 49: RT_MF_RHO_GROUP builds)
+            float gmax = 0.0f;
+            for (int s = 0; s < 4; ++s) gmax = std::max(gmax, (*rho)[gi * 4 + s]);
+            uint32_t gb;
+            memcpy(&gb, &gmax, 4);
+            (*frag)[(gi * 64 + 49) * 8 + 6] = (uint16_t)(gb & 0xffffu);
+            (*frag)[(gi * 64 + 49) * 8 + 7] = (uint16_t)(gb >> 16);
         }
     }
     return true;
@@ -638,7 +656,8 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
     // the kernel compares with this float; the margins are built for it
     const double mf_bound = (double)round_up(vmax_scene * (1.0 + ldexp(1.0, -10)) + ldexp(1.0, -10));
     std::vector<uint16_t> mf_frag;
-    const bool mf_ok = filt_ok && build_mf_image(isect, n, mf_bound, &mf_frag);
+    std::vector<float> mf_rho;
+    const bool mf_ok = filt_ok && build_mf_image(isect, n, mf_bound, &mf_frag, &mf_rho);
     sc->dev.n_surf = n_surf;
     sc->dev.n_tri = n;
     sc->dev.origin_bound = (float)obound;
@@ -669,6 +688,7 @@ int rt_scene_create(rt_ctx* ctx, const float* tri_v, const float* albedo, int n_
         e = hipMalloc(&sc->dev.mf_frag, sizeof(uint16_t) * mf_frag.size());
         if (e == hipSuccess)
             e = hipMemcpy(sc->dev.mf_frag, mf_frag.data(), sizeof(uint16_t) * mf_frag.size(), hipMemcpyHostToDevice);
+
     }
     if (e != hipSuccess) {
         cleanup();

@@ -284,12 +284,33 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
 }
 
+// The fused Q.cos sampler's per-ray inputs (k_dqn_mlp<MT, true>): the rays' pixel keys and
+// sample (ray id = slot * n_pix + pixel slot, as k_dqn_bounce), the Philox event and key.
+struct MlpSample {
+    const uint32_t* pix = nullptr;
+    int n_pix = 0, s0 = 0;
+    uint32_t ev = 0, k0 = 0, k1 = 0;
+};
+
+__device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
+    const int gxi = a / kDqnGrid;
+    const int gyi = a - gxi * kDqnGrid;
+    return chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
+}
+
 // One workgroup = MT*16 rays (LDS: MT=4 -> 77 KB, two workgroups per CU).
-template <int MT>
+// FUSED: instead of writing Q out, the workgroup runs importance_sample_direction's
+// selection (nn_rendering_helpers.cu:391-489) on its LDS tile -- Q*cos of every cell, the
+// total and the CDF walk in sample_from_q's two-level order, 256 threads over the
+// (ray, 4-cell quad) pairs and one lane per ray for the two sequential 36-step scans -- and
+// writes the chosen cell and its normalised Q*cos per ray (q[i] = action bits,
+// q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
+// direction.  Q never leaves the chip.
+template <int MT, bool FUSED = false>
 __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
-                                                 float* __restrict__ q, int ldq) {
+                                                 float* __restrict__ q, int ldq, const MlpSample smp) {
     constexpr int kRows = MT * 16;
     __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrideA];
     __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrideB];
@@ -330,6 +351,103 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
         mlp_layer<slots(9), true, MT>(net, 3, bufB, kStrideB, bufA, 0);           // N = 144
     }
     __syncthreads();
+    if constexpr (FUSED) {
+        static_assert(kRows == 64 && kMlpThreads == 256, "the fused sampler maps 4 threads to a ray");
+        constexpr int kQuads = kDqnActions / 4;  // 36
+        constexpr int kPart = kQuads + 1;        // odd row stride: conflict-free
+        float* const stage = reinterpret_cast<float*>(bufA);  // [row][kStageStride]: Q -> Q*cos -> qd
+        float* const part = reinterpret_cast<float*>(bufB);   // [row][kPart]: quad sums (free after layer 3)
+        float* const tot = part + kRows * kPart;
+        const int r = threadIdx.x & 63, w = threadIdx.x >> 6;
+        const bool live = r < rows_valid;
+        uint32_t pixid = 0, sample = 0;
+        if (live) {
+            const int rid = list[row0 + r];
+            const int slot = rid / smp.n_pix;
+            pixid = smp.pix[rid - slot * smp.n_pix];
+            sample = (uint32_t)(smp.s0 + slot);
+        }
+        float* const srow = stage + r * kStageStride;
+        float* const prow = part + r * kPart;
+        // (1) Q*cos per cell (one Philox draw per two cells, counter 1 + a/2) and the quad sums
+        if (live) {
+#pragma unroll 3
+            for (int j = w; j < kQuads; j += 4) {
+                const int a0 = 4 * j;
+                uint32_t o0[4], o1[4];
+                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o0);
+                philox4x32_10(pixid, sample, smp.ev, 2u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o1);
+                const float c0 = srow[a0 + 0] * chiu_cos_cell(a0 + 0, u01(o0[0]), u01(o0[1]));
+                const float c1 = srow[a0 + 1] * chiu_cos_cell(a0 + 1, u01(o0[2]), u01(o0[3]));
+                const float c2 = srow[a0 + 2] * chiu_cos_cell(a0 + 2, u01(o1[0]), u01(o1[1]));
+                const float c3 = srow[a0 + 3] * chiu_cos_cell(a0 + 3, u01(o1[2]), u01(o1[3]));
+                srow[a0 + 0] = c0;
+                srow[a0 + 1] = c1;
+                srow[a0 + 2] = c2;
+                srow[a0 + 3] = c3;
+                prow[j] = ((c0 + c1) + c2) + c3;
+            }
+        }
+        __syncthreads();
+        // (2) the total, quads in order (one lane per ray)
+        if (w == 0 && live) {
+            float v[kQuads];
+#pragma unroll
+            for (int j = 0; j < kQuads; ++j) v[j] = prow[j];
+            float t = 0.0f;
+#pragma unroll
+            for (int j = 0; j < kQuads; ++j) t = t + v[j];
+            tot[r] = t;
+        }
+        __syncthreads();
+        // (3) qd = Q*cos / total per cell, and the quads' sums of qd
+        if (live) {
+            const float t = tot[r];
+#pragma unroll 3
+            for (int j = w; j < kQuads; j += 4) {
+                const int a0 = 4 * j;
+                const float d0 = srow[a0 + 0] / t, d1 = srow[a0 + 1] / t;
+                const float d2 = srow[a0 + 2] / t, d3 = srow[a0 + 3] / t;
+                srow[a0 + 0] = d0;
+                srow[a0 + 1] = d1;
+                srow[a0 + 2] = d2;
+                srow[a0 + 3] = d3;
+                prow[j] = ((d0 + d1) + d2) + d3;
+            }
+        }
+        __syncthreads();
+        // (4) the CDF walk over the quads, then the cells of the first quad past rv
+        if (w == 0 && live) {
+            uint32_t o[4];
+            philox4x32_10(pixid, sample, smp.ev, 0u, smp.k0, smp.k1, o);
+            const float rv = u01(o[0]);
+            float v[kQuads];
+#pragma unroll
+            for (int j = 0; j < kQuads; ++j) v[j] = prow[j];
+            int act = -1, jsel = -1;
+            float P = 0.0f, qsel = 0.0f;
+#pragma unroll
+            for (int j = 0; j < kQuads; ++j) {
+                const float Pn = P + v[j];
+                if (jsel < 0 && Pn > rv) {
+                    // the cells of quad j from P (rarely, rounding leaves rv unreached: go on)
+                    float cum = P;
+                    for (int u = 0; u < 4 && act < 0; ++u) {
+                        cum = cum + srow[4 * j + u];
+                        if (cum > rv) act = 4 * j + u;
+                    }
+                    if (act >= 0) {
+                        jsel = j;
+                        qsel = srow[act];
+                    }
+                }
+                P = Pn;
+            }
+            q[row0 + r] = __int_as_float(act);
+            q[(size_t)ldq + row0 + r] = qsel;
+        }
+        return;
+    }
     // Q tile [kRows][144] from LDS (odd row stride: conflict-free column reads) in
     // 16-B stores: row-major rows are one contiguous run, action-major columns runs
     // of kRows rows (ldq covers every launched row, so padding rows may be written).
@@ -356,8 +474,37 @@ struct SampleOut {
     f3 dir;
 };
 
+// the chosen cell's jittered direction (Philox counter 1 + 72) and the throughput update
+// cos / pdf, pdf = RHO * (qd / GRID_RHO) -- the end of importance_sample_direction
+__device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 N, f3 T, f3 B, f3 pos, uint32_t pix,
+                                                   uint32_t smp, uint32_t ev, uint32_t k0, uint32_t k1, f3* tp,
+                                                   bool update_tp) {
+    SampleOut res;
+    res.action = action;
+    res.dir = make3(0.0f, 0.0f, 0.0f);
+    if (action >= 0) {
+        uint32_t o[4];
+        philox4x32_10(pix, smp, ev, 1u + kDqnActions / 2, k0, k1, o);
+        const int gxi = action / kDqnGrid;
+        const int gyi = action - gxi * kDqnGrid;
+        res.dir = grid_direction((float)gxi + u01(o[0]), (float)gyi + u01(o[1]), N, T, B, pos);
+        if (update_tp) {
+            const float c = dot(N, res.dir);
+            const float pdf = kRho * (qd_sel / kGridRho);
+            tp->x = (tp->x * c) / pdf;
+            tp->y = (tp->y * c) / pdf;
+            tp->z = (tp->z * c) / pdf;
+        }
+    }
+    return res;
+}
+
 // importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray;
-// q: its 144 Q values, overwritten with Q*cos (as the reference does in place).
+// q: its 144 Q values, overwritten with Q*cos (as the reference does in place).  The
+// total and the CDF walk add in a fixed two-level order (quads of 4 consecutive cells,
+// ((x0 + x1) + x2) + x3, the quads in order; the walk steps over quad sums and then over
+// the cells of the first quad whose end exceeds rv): the fused forward + sampler computes
+// the quads in parallel (k_dqn_mlp<FUSED>), and the oracle's dqn_sample adds the same way.
 // q[a * qs]: qs = 1 for a [row][144] buffer, ldq for the action-major one.
 __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t qs, f3 N, f3 T, f3 B, f3 pos,
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
@@ -368,6 +515,7 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     // Q is read in groups of kQGroup cells (all loads of a group in flight at once:
     // one-at-a-time loads put an HBM round trip on every cell)
     constexpr int kQGroup = 16;  // 8 and 24 measure the same, 48 and 72 slower
+    // the sums in the fixed two-level order of dqn_cdf (quads of 4 cells; oracle dqn_sample)
     float total = 0.0f;
     for (int g = 0; g < kDqnActions; g += kQGroup) {
         float qv[kQGroup];
@@ -385,45 +533,42 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
                 const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
                 const float qc = qv[u2 + h] * c;
                 q[(size_t)a * qs] = qc;
-                total = total + qc;
+                qv[u2 + h] = qc;
             }
         }
+#pragma unroll
+        for (int k = 0; k < kQGroup; k += 4) total = total + (((qv[k] + qv[k + 1]) + qv[k + 2]) + qv[k + 3]);
     }
     SampleOut res;
     res.action = -1;
     res.dir = make3(0.0f, 0.0f, 0.0f);
-    float q_sum = 0.0f;
+    float P = 0.0f;
     float qd_sel = 0.0f;
     for (int g = 0; g < kDqnActions && res.action < 0; g += kQGroup) {
         float qv[kQGroup];
 #pragma unroll
         for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
 #pragma unroll
-        for (int u = 0; u < kQGroup; ++u) {
-            if (res.action < 0) {
-                const float qd = qv[u] / total;
-                q_sum = q_sum + qd;
-                if (q_sum > rv) {
-                    res.action = g + u;
-                    qd_sel = qd;
+        for (int k = 0; k < kQGroup; k += 4) {
+            float qd[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) qd[u] = qv[k + u] / total;
+            const float Pn = P + (((qd[0] + qd[1]) + qd[2]) + qd[3]);
+            if (res.action < 0 && Pn > rv) {
+                float cum = P;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    cum = cum + qd[u];
+                    if (res.action < 0 && cum > rv) {
+                        res.action = g + k + u;
+                        qd_sel = qd[u];
+                    }
                 }
             }
+            P = Pn;
         }
     }
-    if (res.action >= 0) {
-        philox4x32_10(pix, smp, ev, 1u + kDqnActions / 2, k0, k1, o);
-        const int gxi = res.action / kDqnGrid;
-        const int gyi = res.action - gxi * kDqnGrid;
-        res.dir = grid_direction((float)gxi + u01(o[0]), (float)gyi + u01(o[1]), N, T, B, pos);
-        if (update_tp) {
-            const float c = dot(N, res.dir);
-            const float pdf = kRho * (qd_sel / kGridRho);
-            tp->x = (tp->x * c) / pdf;
-            tp->y = (tp->y * c) / pdf;
-            tp->z = (tp->z * c) / pdf;
-        }
-    }
-    return res;
+    return sample_finish(res.action, qd_sel, N, T, B, pos, pix, smp, ev, k0, k1, tp, update_tp);
 }
 
 // trace_ray (pre_trained_pathtracer.cu:413-491): Ray(pos + dir*1e-5, dir), GPU hit rule.
@@ -545,7 +690,8 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camer
 }
 
 // one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
-template <int MF>
+// FUSED: the cell was chosen by k_dqn_mlp<MT, true> (q[i] = its index bits, q[ldq + i] = qd)
+template <int MF, bool FUSED = false>
 __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounce(const DqnLaunch a, int bounce) {
     __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
@@ -571,9 +717,12 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
         const float4 T4 = a.scene.shade[tri * kShadeF4 + 1];
         const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
         const SampleOut so =
-            sample_from_q(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
-                          make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
-                          1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
+            FUSED ? sample_finish(__float_as_int(a.rays.q[i]), a.rays.q[(size_t)a.rays.ldq + i], make3(N4.x, N4.y, N4.z),
+                                  make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
+                                  1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true)
+                  : sample_from_q(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                                  make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
+                                  1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
         loc = pos;
         ntri = tri;
@@ -837,8 +986,18 @@ __global__ __launch_bounds__(256) void k_nq_image(const DqnLaunch a, const NqRay
 
 }  // namespace
 
+static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, const int32_t* list,
+                                       const int32_t* count, int max_rows, float* q, int ldq, const MlpSample* smp,
+                                       hipStream_t stream);
+
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
                           int max_rows, float* q, int ldq, hipStream_t stream) {
+    return launch_dqn_mlp_fused(net, loc, list, count, max_rows, q, ldq, nullptr, stream);
+}
+
+// fused (smp != nullptr): the sampler runs in the forward kernel (k_dqn_mlp<MT, true>)
+static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
+                                int max_rows, float* q, int ldq, const MlpSample* smp, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
     KernelTimer kt(KT_DQN_MLP, stream);
     // this file's weight-streaming kernel; the weight-stationary one (rt_dqn_ws.hip) when
@@ -852,8 +1011,12 @@ hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* li
     }
     const int blocks = (max_rows + kTileM - 1) / kTileM;
     if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_dqn_mlp<RT_MLP_MT>, dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc, list, count,
-                       max_rows, q, ldq);
+    if (smp != nullptr)
+        hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc,
+                           list, count, max_rows, q, ldq, *smp);
+    else
+        hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, false>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc,
+                           list, count, max_rows, q, ldq, MlpSample());
     return hipGetLastError();
 }
 
@@ -888,16 +1051,34 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#ifndef RT_DQN_FUSED
+#define RT_DQN_FUSED 1  // 0: Q written out by k_dqn_mlp, sampled by k_dqn_bounce (A/B builds)
+#endif
+
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream) {
     const int cur = (bounce - 1) & 1;
-    hipError_t e = launch_dqn_mlp(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
-                                  a.rays.q, a.rays.ldq, stream);
+    // the fused sampler: the streaming forward (the weight-stationary A/B kernel writes Q)
+    const bool fused = RT_DQN_FUSED && !(a.net.mlp_mode == kMlpStationary && dqn_mlp_ws_fits(a.net)) &&
+                       a.net.N[3] == kDqnActions && a.rays.ldq >= 2;
+    MlpSample smp;
+    smp.pix = a.rays.pix;
+    smp.n_pix = a.rays.n_pix;
+    smp.s0 = a.rays.s0;
+    smp.ev = 1u + (uint32_t)bounce;
+    smp.k0 = a.seed_lo;
+    smp.k1 = a.seed_hi;
+    hipError_t e = launch_dqn_mlp_fused(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
+                                        a.rays.q, a.rays.ldq, fused ? &smp : nullptr, stream);
     if (e != hipSuccess) return e;
     KernelTimer kt(KT_DQN_BOUNCE, stream);
-    switch (dqn_mf(a)) {
-        case 1: hipLaunchKernelGGL(k_dqn_bounce<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
-        case 4: hipLaunchKernelGGL(k_dqn_bounce<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
-        default: hipLaunchKernelGGL(k_dqn_bounce<0>, dim3(ray_blocks(a)), dim3(256), 0, stream, a, bounce); break;
+    const dim3 grid(ray_blocks(a));
+    switch (dqn_mf(a) * 2 + (fused ? 1 : 0)) {
+        case 2: hipLaunchKernelGGL((k_dqn_bounce<1, false>), grid, dim3(256), 0, stream, a, bounce); break;
+        case 3: hipLaunchKernelGGL((k_dqn_bounce<1, true>), grid, dim3(256), 0, stream, a, bounce); break;
+        case 8: hipLaunchKernelGGL((k_dqn_bounce<4, false>), grid, dim3(256), 0, stream, a, bounce); break;
+        case 9: hipLaunchKernelGGL((k_dqn_bounce<4, true>), grid, dim3(256), 0, stream, a, bounce); break;
+        case 1: hipLaunchKernelGGL((k_dqn_bounce<0, true>), grid, dim3(256), 0, stream, a, bounce); break;
+        default: hipLaunchKernelGGL((k_dqn_bounce<0, false>), grid, dim3(256), 0, stream, a, bounce); break;
     }
     return hipGetLastError();
 }

@@ -76,8 +76,10 @@ constexpr float kFiltMaxTScale = 16384.0f;
 // group g of a round holds triangle s G + (G - 1 - g) in slot s = 0..3 (rows 4 s + i,
 // i = A, T', U, V).  Device image per group (index 8 r + g):
 //   frag: 64 lanes x 8 bf16 (lane l: row l & 15, k = 8 (l >> 4) ..), the A operand
-// Each row is scaled so that the filter's margins at c = 2^-12 become the constants 1
-// (U, V, W = A - U - V, T') and 1/2 (|A|, the sign test): build_mf_rows.  The margins hold
+//   (lane 48 + 4 s, dword 3 = k 30, 31 of row 4 s, where the ray operand is 0: slot s's
+//    threshold of the sign test |A| > rho, fp32 bits; 0 for a pad slot)
+// Each row is scaled so that the filter's barycentric and t margins at c = 2^-12 become
+// the constant 1 (U, V, W = A - U - V, T'): build_mf_rows.  The margins hold
 // for |d_i| <= kMfDirBound (unit directions), |o_i| <= mf_bound (the scene's box, widened
 // by 2^-10 relative + 2^-10: surface points and the bounce loop's 1e-5 offset) and
 // t_scale <= kFiltMaxTScale; a lane outside keeps every triangle.

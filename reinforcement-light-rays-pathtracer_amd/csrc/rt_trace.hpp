@@ -440,17 +440,17 @@ __device__ __forceinline__ mf_bf16x8 mf_frag(uint32_t a, uint32_t b, uint32_t c,
 }
 
 // drop bit (bit 31) of one pair from the scaled row values A, T', U, V (build_mf_rows:
-// margins 1, sign test at 1/2): set iff the exact test must fail, i.e. |A| > 1/2 and one
-// of s U, s V, s W (W = A - U - V), s T' is below -1, s = sign A.  s X + 1 < 0 is tested
+// margins 1, sign-test threshold rho): set iff the exact test must fail, i.e. |A| > rho and
+// one of s U, s V, s W (W = A - U - V), s T' is below -1, s = sign A.  s X + 1 < 0 is tested
 // as the sign of fma(X, A, |A|) = |A| (s X + 1), which one rounding cannot flip (an exact
 // 0 gives +0: keep); W's two subtractions round as the fp32 filter's (aa - su) - sv do.
-__device__ __forceinline__ uint32_t mf_drop(mf_f32x4 q) {
+__device__ __forceinline__ uint32_t mf_drop(mf_f32x4 q, float rho) {
     const float A = q[0], aa = fabsf(q[0]);
     const float w = (A - q[2]) - q[3];
     const float xu = fmaf(q[2], A, aa), xv = fmaf(q[3], A, aa);
     const float xw = fmaf(w, A, aa), xt = fmaf(q[1], A, aa);
     const float mn = fminf(fminf(xu, xv), fminf(xw, xt));
-    return __float_as_uint(0.5f - aa) & __float_as_uint(mn);
+    return __float_as_uint(rho - aa) & __float_as_uint(mn);
 }
 
 // groups of the image that hold triangles (all rounds but the last are full)
@@ -505,17 +505,20 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #ifndef RT_MF_PINGPONG
 #define RT_MF_PINGPONG 1  // 0: one operand set prefetched a group ahead (copied each group)
 #endif
+#ifndef RT_MF_RHO_GROUP
+#define RT_MF_RHO_GROUP 0  // 1: one sign-test threshold per 4-triangle group (the largest); 2: 1/2
+#endif
 #ifndef RT_MF_COOP
 #define RT_MF_COOP 1  // 0: each lane runs its own candidates' exact tests (A/B builds)
 #endif
 
 // LDS of one wave for the shared exact phase: rays [6][64] (o, -D), pairs [cap] u16
-// (lane << 6 | triangle of the block), t [cap]
+// (lane << 6 | triangle of the block); the tests' t values stay in registers
 #ifndef RT_MF_PAIR_CAP
 #define RT_MF_PAIR_CAP 256
 #endif
 constexpr int kMfPairCap = RT_MF_PAIR_CAP;
-constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2 + kMfPairCap;
+constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2;
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -526,25 +529,19 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 template <int RULE>
 __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, int tri0, uint64_t F, f3 o,
                                               float nDx, float nDy, float nDz, float* wl, int lane, Hit& h) {
-    const int cnt = __builtin_popcountll(F);
-    int incl = cnt;
+    const int cnt = __builtin_popcountll(F);  // 0..64: 7 bits
+    // exclusive prefix sum over the lanes, bit-sliced through ballots (no LDS round trips,
+    // unlike a shuffle scan: the cross-lane permutes were a dependent chain of 6)
+    int excl = 0, total = 0;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += y;
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t bm = __ballot((cnt >> b) & 1);
+        excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << b;
+        total += __builtin_popcountll(bm) << b;
     }
-    const int total = __builtin_amdgcn_readlane(incl, 63);
     if (total == 0) return;
-    const int excl = incl - cnt;
-    float* ray = wl;
+    const float* ray = wl;  // (o, -D) of every lane: written by closest_hit_mf before its masks
     uint16_t* pr = reinterpret_cast<uint16_t*>(wl + 6 * 64);
-    float* tv = wl + 6 * 64 + kMfPairCap / 2;
-    ray[0 * 64 + lane] = o.x;
-    ray[1 * 64 + lane] = o.y;
-    ray[2 * 64 + lane] = o.z;
-    ray[3 * 64 + lane] = nDx;
-    ray[4 * 64 + lane] = nDy;
-    ray[5 * 64 + lane] = nDz;
     for (int cb = 0; cb < total; cb += kMfPairCap) {
         {
             uint64_t G = F;
@@ -558,22 +555,25 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
         }
         wave_lds_sync();
         const int nb = min(kMfPairCap, total - cb);
-        for (int k = lane; k < nb; k += 64) {
-            const uint32_t q = pr[k];
-            const int rl = (int)(q >> 6);
-            const f3 ro = make3(ray[0 * 64 + rl], ray[1 * 64 + rl], ray[2 * 64 + rl]);
-            tv[k] = exact_tv<RULE>(isect, tri0 + (int)(q & 63u), ro, ray[3 * 64 + rl], ray[4 * 64 + rl],
-                                   ray[5 * 64 + rl]);
-        }
-        wave_lds_sync();
-        {
+        for (int sb = 0; sb < nb; sb += 64) {
+            // 64 pairs at a time: lane k tests pair sb + k; each lane then takes its own pairs'
+            // results from the testing lanes' registers (ds_bpermute: no LDS array for them)
+            float tr = __builtin_inff();
+            const int k = sb + lane;
+            if (k < nb) {
+                const uint32_t q = pr[k];
+                const int rl = (int)(q >> 6);
+                const f3 ro = make3(ray[0 * 64 + rl], ray[1 * 64 + rl], ray[2 * 64 + rl]);
+                tr = exact_tv<RULE>(isect, tri0 + (int)(q & 63u), ro, ray[3 * 64 + rl], ray[4 * 64 + rl],
+                                    ray[5 * 64 + rl]);
+            }
             uint64_t G = F;
-            int p = excl - cb;
+            int p = excl - cb - sb;
             while (G != 0ull) {
                 const int b = __builtin_ctzll(G);
                 G &= G - 1ull;
-                if (p >= 0 && p < kMfPairCap) {
-                    const float t = tv[p];
+                if (p >= 0 && p < 64) {
+                    const float t = __shfl(tr, p, 64);
                     if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
                         h.t = t;
                         h.tri = tri0 + b;
@@ -582,7 +582,7 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
                 ++p;
             }
         }
-        wave_lds_sync();
+        wave_lds_sync();  // the pair list is read before the next window overwrites it
     }
 }
 
@@ -605,7 +605,16 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
     const float dm = fmaxf(fmaxf(fabsf(d.x), fabsf(d.y)), fabsf(d.z));
     const bool keep_all = !(finite && om <= s.mf_bound && dm <= kMfDirBound);
     const int lane = threadIdx.x & 63;
+    // the lane's ray for the shared exact phase, parked in LDS now: o and -D are not held in
+    // registers through the masks (the caller may read them back: wl rows 0-5)
+    wl[0 * 64 + lane] = o.x;
+    wl[1 * 64 + lane] = o.y;
+    wl[2 * 64 + lane] = o.z;
+    wl[3 * 64 + lane] = nDx;
+    wl[4 * 64 + lane] = nDy;
+    wl[5 * 64 + lane] = nDz;
     const uint4* __restrict__ frag = s.mf_frag;
+    const int slot = lane >> 4;  // the lane's slot of the MFMA output
     const mf_f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
 
     Hit h;
@@ -650,15 +659,29 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
                 const int gi0 = r * kMfGroupsPerRound;
                 // one 4-triangle group: 4 MFMAs (ray blocks 0..3), drop bits shifted in
                 auto group = [&](const mf_u32x4 af) {
+                    // the slots' sign-test thresholds, stored in the fragment's unused K entries
+                    // (build_mf_image: lane 48 + 4 s, dword 3)
+#if RT_MF_RHO_GROUP == 2
+                    const float rho = 0.5f;  // the bound of every threshold (loosest)
+#elif RT_MF_RHO_GROUP == 1
+                    // the group's largest (one scalar per group: a looser test for its smaller triangles)
+                    const float rho = __int_as_float(__builtin_amdgcn_readlane((int)af[3], 49));
+#else
+                    const float t0 = __int_as_float(__builtin_amdgcn_readlane((int)af[3], 48));
+                    const float t1 = __int_as_float(__builtin_amdgcn_readlane((int)af[3], 52));
+                    const float t2 = __int_as_float(__builtin_amdgcn_readlane((int)af[3], 56));
+                    const float t3 = __int_as_float(__builtin_amdgcn_readlane((int)af[3], 60));
+                    const float rho = (slot & 2) ? ((slot & 1) ? t3 : t2) : ((slot & 1) ? t1 : t0);
+#endif
                     const mf_bf16x8 A = __builtin_bit_cast(mf_bf16x8, af);
                     const mf_f32x4 q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B0, zero, 0, 0, 0);
                     const mf_f32x4 q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B1, zero, 0, 0, 0);
                     const mf_f32x4 q2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B2, zero, 0, 0, 0);
                     const mf_f32x4 q3 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B3, zero, 0, 0, 0);
-                    m0 = __builtin_amdgcn_alignbit(m0, mf_drop(q0), 31);
-                    m1 = __builtin_amdgcn_alignbit(m1, mf_drop(q1), 31);
-                    m2 = __builtin_amdgcn_alignbit(m2, mf_drop(q2), 31);
-                    m3 = __builtin_amdgcn_alignbit(m3, mf_drop(q3), 31);
+                    m0 = __builtin_amdgcn_alignbit(m0, mf_drop(q0, rho), 31);
+                    m1 = __builtin_amdgcn_alignbit(m1, mf_drop(q1, rho), 31);
+                    m2 = __builtin_amdgcn_alignbit(m2, mf_drop(q2, rho), 31);
+                    m3 = __builtin_amdgcn_alignbit(m3, mf_drop(q3, rho), 31);
                 };
 #if RT_MF_PINGPONG
                 // two operand sets in flight: group g + 2's fragment is loaded right after

@@ -9,6 +9,8 @@
 #   smoke                    __graft_entry__.smoke()
 #   tests[:<pytest args>]    pytest -m gpu (default: the whole GPU suite)
 #   bench[:<bench args>]     python bench.py --steps 20 --warmup 3 <args>
+#   wbench:<workload>        the bench line of a workload with the profiled command's arguments
+#                            (so its roofline takes that profile's frames)
 #   kt:<workload>            counter-free rocprofv3 --kernel-trace --stats of the bench
 #                            workload (profiles/<tag>_<workload>_kernel_stats.csv)
 #   pmc:<workload>           PMC passes of the bench workload, summarised into
@@ -59,6 +61,8 @@ for step in "$@"; do
     smoke) run smoke 240 python3 -u -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run "tests" 900 python3 -u -m pytest ${arg:-tests} -m gpu -x -q --timeout 240 --timeout-method thread ;;
     bench) run "bench${arg:+_$(echo "$arg" | tr -c 'a-z0-9' '_')}" 400 python3 -u bench.py --steps 20 --warmup 3 $arg ;;
+    wbench)
+      run "wbench_$arg" 400 $(bench_cmd "$arg" | sed 's/--cpu-seconds 0//') ;;
     kt)
       w=${arg:-cornell}
       steps=20; [ "$w" = cornell ] && steps=40
@@ -76,7 +80,7 @@ for step in "$@"; do
     collect)
       mkdir -p profiles
       for f in "$out"/profiles/*; do [ -e "$f" ] && cp -v "$f" profiles/; done
-      for f in "$out"/smoke.log "$out"/tests.log "$out"/bench*.log; do [ -e "$f" ] && cp "$f" "profiles/${tag}_$(basename "$f")"; done ;;
+      for f in "$out"/smoke.log "$out"/tests.log "$out"/bench*.log "$out"/wbench*.log; do [ -e "$f" ] && cp "$f" "profiles/${tag}_$(basename "$f")"; done ;;
     ab) run "ab" 400 python3 -u tools/ab_render.py $(echo "$arg" | tr ',' '\n' | sed 's#^#build/variants/#') --split 64 --rounds 7 ;;
     run)
       name=${arg%%:*}; rest=${arg#*:}; lim=${rest%%:*}; cmd=${rest#*:}
