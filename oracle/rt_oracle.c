@@ -875,43 +875,25 @@ static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint3
     uint32_t ctr[4] = {pix, smp, ev, 0u}, o[4];
     orc_philox4x32_10(ctr, key, o);
     float rv = u01(o[0]);
-    /* Q*cos per cell, then the sums of importance_sample_direction in a fixed two-level
-     * order (the device computes the quads of 4 cells in parallel, rt_dqn.hip
-     * dqn_cdf_select): quad sums ((x0 + x1) + x2) + x3, quads summed in order; the CDF
-     * walk steps over quads (P_{j+1} = P_j + Qd_j) and, in the first quad whose end
-     * exceeds rv, over its cells from P_j -- the reference's sequential walk
-     * (nn_rendering_helpers.cu:391-489) up to the association of the float sums */
     float total = 0.0f;
-    for (int j = 0; j < 36; j++) {
-        float qs = 0.0f;
-        for (int a2 = 2 * j; a2 < 2 * j + 2; a2++) {
-            ctr[3] = 1u + (uint32_t)a2;
-            orc_philox4x32_10(ctr, key, o);
-            for (int h = 0; h < 2; h++) {
-                int a = 2 * a2 + h;
-                int gxi = a / 12, gyi = a - gxi * 12;
-                float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
-                float qc = q[a] * c;
-                q[a] = qc;
-                qs = (a & 3) ? qs + qc : qc;
-            }
+    for (int a2 = 0; a2 < 72; a2++) {
+        ctr[3] = 1u + (uint32_t)a2;
+        orc_philox4x32_10(ctr, key, o);
+        for (int h = 0; h < 2; h++) {
+            int a = 2 * a2 + h;
+            int gxi = a / 12, gyi = a - gxi * 12;
+            float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
+            float qc = q[a] * c;
+            q[a] = qc;
+            total = total + qc;
         }
-        total = total + qs;
     }
     int act = -1;
-    float qd_sel = 0.0f, P = 0.0f;
-    for (int j = 0; j < 36 && act < 0; j++) {
-        float qd[4];
-        for (int k = 0; k < 4; k++) qd[k] = q[4 * j + k] / total;
-        const float Pn = P + (((qd[0] + qd[1]) + qd[2]) + qd[3]);
-        if (Pn > rv) {
-            float cum = P;
-            for (int k = 0; k < 4; k++) {
-                cum = cum + qd[k];
-                if (cum > rv) { act = 4 * j + k; qd_sel = qd[k]; break; }
-            }
-        }
-        P = Pn;
+    float q_sum = 0.0f, qd_sel = 0.0f;
+    for (int a = 0; a < 144; a++) {
+        float qd = q[a] / total;
+        q_sum = q_sum + qd;
+        if (q_sum > rv) { act = a; qd_sel = qd; break; }
     }
     *dir_out = mk(0.0f, 0.0f, 0.0f);
     if (act >= 0) {

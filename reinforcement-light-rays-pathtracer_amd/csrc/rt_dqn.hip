@@ -300,9 +300,9 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
 
 // One workgroup = MT*16 rays (LDS: MT=4 -> 77 KB, two workgroups per CU).
 // FUSED: instead of writing Q out, the workgroup runs importance_sample_direction's
-// selection (nn_rendering_helpers.cu:391-489) on its LDS tile -- Q*cos of every cell, the
-// total and the CDF walk in sample_from_q's two-level order, 256 threads over the
-// (ray, 4-cell quad) pairs and one lane per ray for the two sequential 36-step scans -- and
+// selection (nn_rendering_helpers.cu:391-489) on its LDS tile -- Q*cos and qd of every
+// cell with 4 threads per ray, the total and the CDF walk cell by cell in the reference's
+// order with one lane per ray (a float sum's order is its result) -- and
 // writes the chosen cell and its normalised Q*cos per ray (q[i] = action bits,
 // q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
 // direction.  Q never leaves the chip.
@@ -353,11 +353,8 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
     __syncthreads();
     if constexpr (FUSED) {
         static_assert(kRows == 64 && kMlpThreads == 256, "the fused sampler maps 4 threads to a ray");
-        constexpr int kQuads = kDqnActions / 4;  // 36
-        constexpr int kPart = kQuads + 1;        // odd row stride: conflict-free
         float* const stage = reinterpret_cast<float*>(bufA);  // [row][kStageStride]: Q -> Q*cos -> qd
-        float* const part = reinterpret_cast<float*>(bufB);   // [row][kPart]: quad sums (free after layer 3)
-        float* const tot = part + kRows * kPart;
+        float* const tot = reinterpret_cast<float*>(bufB);    // [row] totals (bufB is free after layer 3)
         const int r = threadIdx.x & 63, w = threadIdx.x >> 6;
         const bool live = r < rows_valid;
         uint32_t pixid = 0, sample = 0;
@@ -368,80 +365,61 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
             sample = (uint32_t)(smp.s0 + slot);
         }
         float* const srow = stage + r * kStageStride;
-        float* const prow = part + r * kPart;
-        // (1) Q*cos per cell (one Philox draw per two cells, counter 1 + a/2) and the quad sums
+        // (1) Q*cos per cell, 4 threads per ray (one Philox draw per two cells, counter 1 + a/2)
         if (live) {
 #pragma unroll 3
-            for (int j = w; j < kQuads; j += 4) {
-                const int a0 = 4 * j;
+            for (int a0 = 4 * w; a0 < kDqnActions; a0 += 16) {
                 uint32_t o0[4], o1[4];
                 philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o0);
                 philox4x32_10(pixid, sample, smp.ev, 2u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o1);
-                const float c0 = srow[a0 + 0] * chiu_cos_cell(a0 + 0, u01(o0[0]), u01(o0[1]));
-                const float c1 = srow[a0 + 1] * chiu_cos_cell(a0 + 1, u01(o0[2]), u01(o0[3]));
-                const float c2 = srow[a0 + 2] * chiu_cos_cell(a0 + 2, u01(o1[0]), u01(o1[1]));
-                const float c3 = srow[a0 + 3] * chiu_cos_cell(a0 + 3, u01(o1[2]), u01(o1[3]));
-                srow[a0 + 0] = c0;
-                srow[a0 + 1] = c1;
-                srow[a0 + 2] = c2;
-                srow[a0 + 3] = c3;
-                prow[j] = ((c0 + c1) + c2) + c3;
+                srow[a0 + 0] = srow[a0 + 0] * chiu_cos_cell(a0 + 0, u01(o0[0]), u01(o0[1]));
+                srow[a0 + 1] = srow[a0 + 1] * chiu_cos_cell(a0 + 1, u01(o0[2]), u01(o0[3]));
+                srow[a0 + 2] = srow[a0 + 2] * chiu_cos_cell(a0 + 2, u01(o1[0]), u01(o1[1]));
+                srow[a0 + 3] = srow[a0 + 3] * chiu_cos_cell(a0 + 3, u01(o1[2]), u01(o1[3]));
             }
         }
         __syncthreads();
-        // (2) the total, quads in order (one lane per ray)
+        // (2) the total in the reference's order, cell by cell (one lane per ray; the odd row
+        // stride keeps the 64 lanes' reads of one column conflict-free)
         if (w == 0 && live) {
-            float v[kQuads];
-#pragma unroll
-            for (int j = 0; j < kQuads; ++j) v[j] = prow[j];
             float t = 0.0f;
+            for (int g = 0; g < kDqnActions; g += 16) {
+                float v[16];
 #pragma unroll
-            for (int j = 0; j < kQuads; ++j) t = t + v[j];
+                for (int u = 0; u < 16; ++u) v[u] = srow[g + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) t = t + v[u];
+            }
             tot[r] = t;
         }
         __syncthreads();
-        // (3) qd = Q*cos / total per cell, and the quads' sums of qd
+        // (3) qd = Q*cos / total per cell, 4 threads per ray
         if (live) {
             const float t = tot[r];
-#pragma unroll 3
-            for (int j = w; j < kQuads; j += 4) {
-                const int a0 = 4 * j;
-                const float d0 = srow[a0 + 0] / t, d1 = srow[a0 + 1] / t;
-                const float d2 = srow[a0 + 2] / t, d3 = srow[a0 + 3] / t;
-                srow[a0 + 0] = d0;
-                srow[a0 + 1] = d1;
-                srow[a0 + 2] = d2;
-                srow[a0 + 3] = d3;
-                prow[j] = ((d0 + d1) + d2) + d3;
-            }
+#pragma unroll 4
+            for (int a = w; a < kDqnActions; a += 4) srow[a] = srow[a] / t;
         }
         __syncthreads();
-        // (4) the CDF walk over the quads, then the cells of the first quad past rv
+        // (4) the CDF walk, cell by cell as the reference adds (q_sum = q_sum + qd; first
+        // cell with q_sum > rv), one lane per ray
         if (w == 0 && live) {
             uint32_t o[4];
             philox4x32_10(pixid, sample, smp.ev, 0u, smp.k0, smp.k1, o);
             const float rv = u01(o[0]);
-            float v[kQuads];
+            int act = -1;
+            float cum = 0.0f, qsel = 0.0f;
+            for (int g = 0; g < kDqnActions && act < 0; g += 16) {
+                float v[16];
 #pragma unroll
-            for (int j = 0; j < kQuads; ++j) v[j] = prow[j];
-            int act = -1, jsel = -1;
-            float P = 0.0f, qsel = 0.0f;
+                for (int u = 0; u < 16; ++u) v[u] = srow[g + u];
 #pragma unroll
-            for (int j = 0; j < kQuads; ++j) {
-                const float Pn = P + v[j];
-                if (jsel < 0 && Pn > rv) {
-                    // the cells of quad j from P (rarely, rounding leaves rv unreached: go on)
-                    float cum = P;
-                    for (int u = 0; u < 4 && act < 0; ++u) {
-                        cum = cum + srow[4 * j + u];
-                        if (cum > rv) act = 4 * j + u;
-                    }
-                    if (act >= 0) {
-                        jsel = j;
-                        qsel = srow[act];
+                for (int u = 0; u < 16; ++u) {
+                    cum = cum + v[u];
+                    if (act < 0 && cum > rv) {
+                        act = g + u;
+                        qsel = v[u];
                     }
                 }
-                P = Pn;
             }
             q[row0 + r] = __int_as_float(act);
             q[(size_t)ldq + row0 + r] = qsel;
@@ -501,10 +479,8 @@ __device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 
 
 // importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray;
 // q: its 144 Q values, overwritten with Q*cos (as the reference does in place).  The
-// total and the CDF walk add in a fixed two-level order (quads of 4 consecutive cells,
-// ((x0 + x1) + x2) + x3, the quads in order; the walk steps over quad sums and then over
-// the cells of the first quad whose end exceeds rv): the fused forward + sampler computes
-// the quads in parallel (k_dqn_mlp<FUSED>), and the oracle's dqn_sample adds the same way.
+// total and the CDF walk add cell by cell in the reference's order (as k_dqn_mlp<FUSED>
+// and the oracle's dqn_sample).
 // q[a * qs]: qs = 1 for a [row][144] buffer, ldq for the action-major one.
 __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t qs, f3 N, f3 T, f3 B, f3 pos,
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
@@ -515,7 +491,6 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     // Q is read in groups of kQGroup cells (all loads of a group in flight at once:
     // one-at-a-time loads put an HBM round trip on every cell)
     constexpr int kQGroup = 16;  // 8 and 24 measure the same, 48 and 72 slower
-    // the sums in the fixed two-level order of dqn_cdf (quads of 4 cells; oracle dqn_sample)
     float total = 0.0f;
     for (int g = 0; g < kDqnActions; g += kQGroup) {
         float qv[kQGroup];
@@ -533,39 +508,29 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
                 const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
                 const float qc = qv[u2 + h] * c;
                 q[(size_t)a * qs] = qc;
-                qv[u2 + h] = qc;
+                total = total + qc;
             }
         }
-#pragma unroll
-        for (int k = 0; k < kQGroup; k += 4) total = total + (((qv[k] + qv[k + 1]) + qv[k + 2]) + qv[k + 3]);
     }
     SampleOut res;
     res.action = -1;
     res.dir = make3(0.0f, 0.0f, 0.0f);
-    float P = 0.0f;
+    float q_sum = 0.0f;
     float qd_sel = 0.0f;
     for (int g = 0; g < kDqnActions && res.action < 0; g += kQGroup) {
         float qv[kQGroup];
 #pragma unroll
         for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
 #pragma unroll
-        for (int k = 0; k < kQGroup; k += 4) {
-            float qd[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) qd[u] = qv[k + u] / total;
-            const float Pn = P + (((qd[0] + qd[1]) + qd[2]) + qd[3]);
-            if (res.action < 0 && Pn > rv) {
-                float cum = P;
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    cum = cum + qd[u];
-                    if (res.action < 0 && cum > rv) {
-                        res.action = g + k + u;
-                        qd_sel = qd[u];
-                    }
+        for (int u = 0; u < kQGroup; ++u) {
+            if (res.action < 0) {
+                const float qd = qv[u] / total;
+                q_sum = q_sum + qd;
+                if (q_sum > rv) {
+                    res.action = g + u;
+                    qd_sel = qd;
                 }
             }
-            P = Pn;
         }
     }
     return sample_finish(res.action, qd_sel, N, T, B, pos, pix, smp, ev, k0, k1, tp, update_tp);

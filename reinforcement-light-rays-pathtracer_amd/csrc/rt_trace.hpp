@@ -542,6 +542,9 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
     if (total == 0) return;
     const float* ray = wl;  // (o, -D) of every lane: written by closest_hit_mf before its masks
     uint16_t* pr = reinterpret_cast<uint16_t*>(wl + 6 * 64);
+    // the lane's pairs not yet folded (lowest bit first) and the list position of the next
+    uint64_t R = F;
+    int pos = excl;
     for (int cb = 0; cb < total; cb += kMfPairCap) {
         {
             uint64_t G = F;
@@ -567,19 +570,24 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
                 tr = exact_tv<RULE>(isect, tri0 + (int)(q & 63u), ro, ray[3 * 64 + rl], ray[4 * 64 + rl],
                                     ray[5 * 64 + rl]);
             }
-            uint64_t G = F;
-            int p = excl - cb - sb;
-            while (G != 0ull) {
-                const int b = __builtin_ctzll(G);
-                G &= G - 1ull;
-                if (p >= 0 && p < 64) {
-                    const float t = __shfl(tr, p, 64);
+            // The fold, one pair per lane and step, with the whole wave active: a cross-lane
+            // read (ds_bpermute) from a lane that is switched off returns 0, not its value,
+            // so the read must not sit in a lane-divergent loop.  A lane's next pair is in
+            // this window iff pos < base + 64 (earlier windows consumed those before it).
+            const int base = cb + sb;
+            for (;;) {
+                const bool has = (R != 0ull) && (pos < base + 64);
+                if (__ballot(has) == 0ull) break;
+                const float t = __shfl(tr, has ? pos - base : 0, 64);
+                if (has) {
+                    const int b = __builtin_ctzll(R);
+                    R &= R - 1ull;
+                    ++pos;
                     if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
                         h.t = t;
                         h.tri = tri0 + b;
                     }
                 }
-                ++p;
             }
         }
         wave_lds_sync();  // the pair list is read before the next window overwrites it
