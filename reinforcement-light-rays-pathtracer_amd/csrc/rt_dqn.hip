@@ -1017,7 +1017,7 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
 }
 
 #ifndef RT_DQN_FUSED
-#define RT_DQN_FUSED 1  // 0: Q written out by k_dqn_mlp, sampled by k_dqn_bounce (A/B builds)
+#define RT_DQN_FUSED 0  // 1: the sampler inside k_dqn_mlp (measured slower: 143.9 vs 131.8 ms, archway 512^2 x 16)
 #endif
 
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream) {

@@ -503,7 +503,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #endif
     f3 acc = make3(0.0f, 0.0f, 0.0f);
     int k = 0;          // next slot
-    [[maybe_unused]] int cur = 0;  // sample of the live path (the non-stealing build)
+    int cur = 0;        // sample of the live path
     int depth = 0;      // surface bounces of the live path so far
     f3 o = cam, d = make3(0.0f, 0.0f, 1.0f);
     f3 pos = cam;       // the live path's surface hit to shade next, and its triangle
@@ -526,10 +526,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         q_total += __builtin_popcountll(m);
     }
     int q_next = 0;       // wave-uniform: next queue entry
-    // the live path's queue entry (slot k << 6 | owner lane): its slot, pixel (RNG key) and
-    // sample index are recomputed from it where needed instead of held in registers
-    int oe = lane;
-    auto own_slot = [&]() { return wslots + (oe >> 6) * (kPsFields * 64) + (oe & 63); };
+    float* own = slots;   // slot of the live path's sample (any lane's)
+    uint32_t lpix = pix;  // its pixel (RNG key)
     bool live = false;
     auto claim = [&]() {  // wave-level: lanes without a path take the next queued samples
         const uint64_t need = __ballot(!live);
@@ -537,11 +535,15 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         const int j = q_next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         if (!live && j < q_total) {
-            oe = (int)queue[j];
-            const float* own = own_slot();
+            const uint32_t e = queue[j];
+            const int ol = (int)(e & 63u), kk = (int)(e >> 6);
+            own = wslots + kk * kPsFields * 64 + ol;
             pos = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
             hit_tri = __float_as_int(own[3 * 64]);
             depth = 0;
+            const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the lane's pixel
+            lpix = (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
+            cur = (ol & (a.split - 1)) * pc + kk;
             live = true;
         }
         q_next = min(q_total, q_next + __builtin_popcountll(need));
@@ -594,14 +596,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             const float4 B = shade[hit_tri * kShadeF4 + 2];
             float r1, r2;
 #if RT_PS_STEAL
-            {
-                const int ol = oe & 63, kk = oe >> 6;
-                const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the path's pixel
-                const uint32_t lpix =
-                    (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
-                const int scur = (ol & (a.split - 1)) * pc + kk;
-                draw2(lpix, (uint32_t)scur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
-            }
+            draw2(lpix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
 #else
             draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
 #endif
@@ -621,22 +616,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
                                 (sx * B.z + cos_theta * N.z) + sz * T.z);
             s_tri = hit_tri;
             s_cos = cos_theta;
-#if RT_PS_STEAL
-            // the path's factors wait in its own slot (consumed at the claim) instead of
-            // registers through the cast: [0, 1] the first bounce's, [2, 3] this one's
-            float* const own = own_slot();
-            if (depth == 0) {
-                own[0 * 64] = __int_as_float(s_tri);
-                own[1 * 64] = s_cos;
-            }
-            own[2 * 64] = __int_as_float(s_tri);
-            own[3 * 64] = s_cos;
-#else
             if (depth == 0) {
                 f_tri0 = s_tri;
                 f_cos0 = s_cos;
             }
-#endif
             o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
             d = normalize(sd);
             ++depth;
@@ -672,15 +655,6 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         } else if (h.tri >= n_surf) {
             const float4 e = shade[h.tri * kShadeF4 + 3];
             L = make3(e.x, e.y, e.z);
-#if RT_PS_STEAL
-            {
-                const float* own = own_slot();
-                f_tri0 = __float_as_int(own[0 * 64]);
-                f_cos0 = own[1 * 64];
-                s_tri = __float_as_int(own[2 * 64]);
-                s_cos = own[3 * 64];
-            }
-#endif
             // fold back through the surface bounces: depth 2 (this shading), then depth 1
             if (depth >= 2) {
                 const float4 c = shade[s_tri * kShadeF4 + (SAMPLER == 0 ? 3 : 4)];
@@ -706,20 +680,11 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             // bounces == MAX_RAY_BOUNCES -> vec3(0)
         } else {
             terminal = false;  // shade the hit on the next trip
-            if (use_mf) {
-                // o and -D from the exact phase's LDS (closest_hit_mf parks them there):
-                // o - t (-D) is o + t D bit for bit (negation and RN commute)
-                pos = make3(wl[0 * 64 + lane] - h.t * wl[3 * 64 + lane], wl[1 * 64 + lane] - h.t * wl[4 * 64 + lane],
-                            wl[2 * 64 + lane] - h.t * wl[5 * 64 + lane]);
-            } else {
-                pos = make3(o.x + h.t * (d.x * a.t_scale), o.y + h.t * (d.y * a.t_scale),
-                            o.z + h.t * (d.z * a.t_scale));
-            }
+            pos = make3(o.x + h.t * (d.x * a.t_scale), o.y + h.t * (d.y * a.t_scale), o.z + h.t * (d.z * a.t_scale));
             hit_tri = h.tri;
         }
         if (terminal) {
 #if RT_PS_STEAL
-            float* const own = own_slot();
             own[0 * 64] = L.x;
             own[1 * 64] = L.y;
             own[2 * 64] = L.z;

@@ -506,7 +506,7 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #define RT_MF_PINGPONG 1  // 0: one operand set prefetched a group ahead (copied each group)
 #endif
 #ifndef RT_MF_RHO_GROUP
-#define RT_MF_RHO_GROUP 0  // 1: one sign-test threshold per 4-triangle group (the largest); 2: 1/2
+#define RT_MF_RHO_GROUP 1  // one sign-test threshold per 4-triangle group, the largest (0: per slot, 2: 1/2; 1 measured fastest, profiles/r3i)
 #endif
 #ifndef RT_MF_COOP
 #define RT_MF_COOP 1  // 0: each lane runs its own candidates' exact tests (A/B builds)
@@ -517,8 +517,11 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #ifndef RT_MF_PAIR_CAP
 #define RT_MF_PAIR_CAP 256
 #endif
+#ifndef RT_MF_TV_LDS
+#define RT_MF_TV_LDS 1  // 0: t values by cross-lane reads (Cornell 512^2 x 256: 4.19 vs 3.96 ms)
+#endif
 constexpr int kMfPairCap = RT_MF_PAIR_CAP;
-constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2;
+constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2 + (RT_MF_TV_LDS ? kMfPairCap : 0);
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -558,6 +561,35 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
         }
         wave_lds_sync();
         const int nb = min(kMfPairCap, total - cb);
+#if RT_MF_TV_LDS
+        float* tv = wl + 6 * 64 + kMfPairCap / 2;
+        for (int k = lane; k < nb; k += 64) {
+            const uint32_t q = pr[k];
+            const int rl = (int)(q >> 6);
+            const f3 ro = make3(ray[0 * 64 + rl], ray[1 * 64 + rl], ray[2 * 64 + rl]);
+            tv[k] = exact_tv<RULE>(isect, tri0 + (int)(q & 63u), ro, ray[3 * 64 + rl], ray[4 * 64 + rl],
+                                   ray[5 * 64 + rl]);
+        }
+        wave_lds_sync();
+        {
+            uint64_t G = F;
+            int p = excl - cb;
+            while (G != 0ull) {
+                const int b = __builtin_ctzll(G);
+                G &= G - 1ull;
+                if (p >= 0 && p < kMfPairCap) {
+                    const float t = tv[p];
+                    if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
+                        h.t = t;
+                        h.tri = tri0 + b;
+                    }
+                }
+                ++p;
+            }
+        }
+        (void)R;
+        (void)pos;
+#else
         for (int sb = 0; sb < nb; sb += 64) {
             // 64 pairs at a time: lane k tests pair sb + k; each lane then takes its own pairs'
             // results from the testing lanes' registers (ds_bpermute: no LDS array for them)
@@ -590,6 +622,7 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
                 }
             }
         }
+#endif
         wave_lds_sync();  // the pair list is read before the next window overwrites it
     }
 }
@@ -622,7 +655,7 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
     wl[4 * 64 + lane] = nDy;
     wl[5 * 64 + lane] = nDz;
     const uint4* __restrict__ frag = s.mf_frag;
-    const int slot = lane >> 4;  // the lane's slot of the MFMA output
+    [[maybe_unused]] const int slot = lane >> 4;  // the lane's slot of the MFMA output
     const mf_f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
 
     Hit h;
