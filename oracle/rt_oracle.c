@@ -875,7 +875,15 @@ static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint3
     uint32_t ctr[4] = {pix, smp, ev, 0u}, o[4];
     orc_philox4x32_10(ctr, key, o);
     float rv = u01(o[0]);
-    float total = 0.0f;
+    /* Q*cos per cell, then importance_sample_direction's sums (nn_rendering_helpers.cu:391-489)
+     * in the fixed blocked order the device uses (rt_dqn.hip sample_from_q and the fused
+     * k_dqn_mlp): 4 blocks of 36 cells; B_w = sum of qc = Q*cos over block w in cell order,
+     * total = ((B_0 + B_1) + B_2) + B_3, P_0 = 0, P_{w+1} = P_w + B_w / total; the walk starts
+     * in the first block w with P_{w+1} > rv from cum = P_w, cell by cell cum = cum + qd
+     * (qd = qc / total), and takes the first cell with cum > rv and qd > 0 (on into the next
+     * block if rounding leaves the block without one).  Inside the chosen block this is the
+     * reference's own walk; the block sums only change the association of the float sums. */
+    float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int a2 = 0; a2 < 72; a2++) {
         ctr[3] = 1u + (uint32_t)a2;
         orc_philox4x32_10(ctr, key, o);
@@ -885,15 +893,24 @@ static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint3
             float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
             float qc = q[a] * c;
             q[a] = qc;
-            total = total + qc;
+            bsum[a / 36] = bsum[a / 36] + qc;
         }
     }
+    float total = 0.0f;
+    for (int w = 0; w < 4; w++) total = total + bsum[w];
     int act = -1;
-    float q_sum = 0.0f, qd_sel = 0.0f;
-    for (int a = 0; a < 144; a++) {
-        float qd = q[a] / total;
-        q_sum = q_sum + qd;
-        if (q_sum > rv) { act = a; qd_sel = qd; break; }
+    float P = 0.0f, qd_sel = 0.0f;
+    for (int w = 0; w < 4 && act < 0; w++) {
+        float Pn = P + bsum[w] / total;
+        if (Pn > rv) {
+            float cum = P;
+            for (int a = 36 * w; a < 36 * w + 36 && act < 0; a++) {
+                float qd = q[a] / total;
+                cum = cum + qd;
+                if (cum > rv && qd > 0.0f) { act = a; qd_sel = qd; }
+            }
+        }
+        P = Pn;
     }
     *dir_out = mk(0.0f, 0.0f, 0.0f);
     if (act >= 0) {

@@ -68,6 +68,9 @@ __device__ __forceinline__ int swz(int row, int k, int stride) {
     return row * stride + (((k >> 3) ^ ((row >> 2) & 7)) << 3) + (k & 7);
 }
 constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
+// the sampler's fixed sum order: kSampBlocks blocks of kSampCells cells (sample_from_q)
+constexpr int kSampBlocks = 4;
+constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 18 Philox draws
 static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
 
@@ -300,9 +303,9 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
 
 // One workgroup = MT*16 rays (LDS: MT=4 -> 77 KB, two workgroups per CU).
 // FUSED: instead of writing Q out, the workgroup runs importance_sample_direction's
-// selection (nn_rendering_helpers.cu:391-489) on its LDS tile -- Q*cos and qd of every
-// cell with 4 threads per ray, the total and the CDF walk cell by cell in the reference's
-// order with one lane per ray (a float sum's order is its result) -- and
+// selection (nn_rendering_helpers.cu:391-489) on its LDS tile in sample_from_q's blocked
+// order, one thread per (ray, block of 36 cells): Q*cos and the block sums, then the total,
+// the block prefixes and the walks of the reached blocks, the first block's cell winning -- and
 // writes the chosen cell and its normalised Q*cos per ray (q[i] = action bits,
 // q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
 // direction.  Q never leaves the chip.
@@ -352,10 +355,10 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
     }
     __syncthreads();
     if constexpr (FUSED) {
-        static_assert(kRows == 64 && kMlpThreads == 256, "the fused sampler maps 4 threads to a ray");
-        float* const stage = reinterpret_cast<float*>(bufA);  // [row][kStageStride]: Q -> Q*cos -> qd
-        float* const tot = reinterpret_cast<float*>(bufB);    // [row] totals (bufB is free after layer 3)
-        const int r = threadIdx.x & 63, w = threadIdx.x >> 6;
+        static_assert(kRows == 64 && kMlpThreads == 64 * kSampBlocks, "the fused sampler maps a thread to a block");
+        float* const stage = reinterpret_cast<float*>(bufA);  // [row][kStageStride]: Q -> Q*cos
+        float* const bsum = reinterpret_cast<float*>(bufB);   // [row][block] B_w (bufB is free after layer 3)
+        const int r = threadIdx.x & 63, w = threadIdx.x >> 6;  // ray, block (sample_from_q's order)
         const bool live = r < rows_valid;
         uint32_t pixid = 0, sample = 0;
         if (live) {
@@ -365,60 +368,73 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
             sample = (uint32_t)(smp.s0 + slot);
         }
         float* const srow = stage + r * kStageStride;
-        // (1) Q*cos per cell, 4 threads per ray (one Philox draw per two cells, counter 1 + a/2)
+        // (1) Q*cos of the block's cells (one Philox draw per two cells, counter 1 + a/2), B_w
         if (live) {
-#pragma unroll 3
-            for (int a0 = 4 * w; a0 < kDqnActions; a0 += 16) {
-                uint32_t o0[4], o1[4];
-                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o0);
-                philox4x32_10(pixid, sample, smp.ev, 2u + (uint32_t)(a0 >> 1), smp.k0, smp.k1, o1);
-                srow[a0 + 0] = srow[a0 + 0] * chiu_cos_cell(a0 + 0, u01(o0[0]), u01(o0[1]));
-                srow[a0 + 1] = srow[a0 + 1] * chiu_cos_cell(a0 + 1, u01(o0[2]), u01(o0[3]));
-                srow[a0 + 2] = srow[a0 + 2] * chiu_cos_cell(a0 + 2, u01(o1[0]), u01(o1[1]));
-                srow[a0 + 3] = srow[a0 + 3] * chiu_cos_cell(a0 + 3, u01(o1[2]), u01(o1[3]));
+            const int c0 = w * kSampCells;
+            float b = 0.0f;
+#pragma unroll 2
+            for (int a = c0; a < c0 + kSampCells; a += 2) {
+                uint32_t o[4];
+                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a >> 1), smp.k0, smp.k1, o);
+                const float q0 = srow[a] * chiu_cos_cell(a, u01(o[0]), u01(o[1]));
+                const float q1 = srow[a + 1] * chiu_cos_cell(a + 1, u01(o[2]), u01(o[3]));
+                srow[a] = q0;
+                srow[a + 1] = q1;
+                b = b + q0;
+                b = b + q1;
             }
+            bsum[r * kSampBlocks + w] = b;
         }
         __syncthreads();
-        // (2) the total in the reference's order, cell by cell (one lane per ray; the odd row
-        // stride keeps the 64 lanes' reads of one column conflict-free)
-        if (w == 0 && live) {
-            float t = 0.0f;
-            for (int g = 0; g < kDqnActions; g += 16) {
-                float v[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = srow[g + u];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) t = t + v[u];
-            }
-            tot[r] = t;
-        }
-        __syncthreads();
-        // (3) qd = Q*cos / total per cell, 4 threads per ray
+        // (2) every (ray, block) thread: the total and its block's prefixes; the block is walked
+        // iff it is reached (P_{w+1} > rv) -- in parallel, the first reached block that finds
+        // a cell winning (sample_from_q walks them in order and stops there: the same cell)
+        int* const hit = reinterpret_cast<int*>(bsum + kRows * kSampBlocks);  // [row][block]
+        float* const hq = reinterpret_cast<float*>(hit + kRows * kSampBlocks);
         if (live) {
-            const float t = tot[r];
-#pragma unroll 4
-            for (int a = w; a < kDqnActions; a += 4) srow[a] = srow[a] / t;
-        }
-        __syncthreads();
-        // (4) the CDF walk, cell by cell as the reference adds (q_sum = q_sum + qd; first
-        // cell with q_sum > rv), one lane per ray
-        if (w == 0 && live) {
             uint32_t o[4];
             philox4x32_10(pixid, sample, smp.ev, 0u, smp.k0, smp.k1, o);
             const float rv = u01(o[0]);
+            float bs[kSampBlocks];
+            float total = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kSampBlocks; ++k) {
+                bs[k] = bsum[r * kSampBlocks + k];
+                total = total + bs[k];
+            }
+            float P = 0.0f, Pn = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kSampBlocks; ++k) {
+                Pn = P + bs[k] / total;
+                if (k == w) break;
+                P = Pn;
+            }
             int act = -1;
-            float cum = 0.0f, qsel = 0.0f;
-            for (int g = 0; g < kDqnActions && act < 0; g += 16) {
-                float v[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = srow[g + u];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) {
-                    cum = cum + v[u];
-                    if (act < 0 && cum > rv) {
-                        act = g + u;
-                        qsel = v[u];
+            float qsel = 0.0f;
+            if (Pn > rv) {
+                float cum = P;
+                for (int a = w * kSampCells; a < (w + 1) * kSampCells && act < 0; ++a) {
+                    const float qd = srow[a] / total;
+                    cum = cum + qd;
+                    if (cum > rv && qd > 0.0f) {
+                        act = a;
+                        qsel = qd;
                     }
+                }
+            }
+            hit[r * kSampBlocks + w] = act;
+            hq[r * kSampBlocks + w] = qsel;
+        }
+        __syncthreads();
+        if (w == 0 && live) {
+            int act = -1;
+            float qsel = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kSampBlocks; ++k) {
+                const int h = hit[r * kSampBlocks + k];
+                if (act < 0 && h >= 0) {
+                    act = h;
+                    qsel = hq[r * kSampBlocks + k];
                 }
             }
             q[row0 + r] = __int_as_float(act);
@@ -477,11 +493,22 @@ __device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 
     return res;
 }
 
-// importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray;
-// q: its 144 Q values, overwritten with Q*cos (as the reference does in place).  The
-// total and the CDF walk add cell by cell in the reference's order (as k_dqn_mlp<FUSED>
-// and the oracle's dqn_sample).
-// q[a * qs]: qs = 1 for a [row][144] buffer, ldq for the action-major one.
+// importance_sample_direction (nn_rendering_helpers.cu:391-489) for one ray, on its 144 Q
+// values q[a * qs] (qs = 1 for a [row][144] buffer, ldq for the action-major one).
+// The sums run in a fixed blocked order (kSampBlocks blocks of kSampCells consecutive
+// cells; the fused k_dqn_mlp<.., true> gives each block its own thread, the oracle's
+// dqn_sample adds the same way):
+//   qc = Q * cos (the cell's jittered direction), B_w = sum of qc over block w in cell
+//   order, total = ((B_0 + B_1) + B_2) + B_3, P_0 = 0, P_{w+1} = P_w + B_w / total;
+//   the walk starts in the first block w with P_{w+1} > rv: cum = P_w, then cell by cell
+//   cum = cum + qc / total, taking the first cell with cum > rv and qd = qc / total > 0
+//   (on into the next block if rounding leaves the block without one).
+// Inside the chosen block this is the reference's own walk (cum = q_sum + qd per cell);
+// the block sums only change the association of the float sums.  Only one block's cells
+// are divided and walked.  WB: q is overwritten with Q * cos, as the reference does in
+// place (rt_dqn_sample, the Neural-Q sampler); without it the walk recomputes its block's
+// Q * cos (the same operations, so the same bits) instead of a 576-B store and reload.
+template <bool WB>
 __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t qs, f3 N, f3 T, f3 B, f3 pos,
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
                                                    uint32_t k0, uint32_t k1, f3* tp, bool update_tp) {
@@ -490,48 +517,68 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     const float rv = u01(o[0]);
     // Q is read in groups of kQGroup cells (all loads of a group in flight at once:
     // one-at-a-time loads put an HBM round trip on every cell)
-    constexpr int kQGroup = 16;  // 8 and 24 measure the same, 48 and 72 slower
-    float total = 0.0f;
-    for (int g = 0; g < kDqnActions; g += kQGroup) {
-        float qv[kQGroup];
+    constexpr int kQGroup = 12;
+    static_assert(kSampCells % kQGroup == 0, "groups tile the blocks");
+    // Q*cos of the group of cells g .. g + kQGroup - 1 into qv (q holds Q, or Q*cos if done)
+    auto qcos = [&](int g, float* qv, bool stored) {
 #pragma unroll
         for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
+        if (stored) return;
 #pragma unroll
         for (int u2 = 0; u2 < kQGroup; u2 += 2) {
-            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u2) >> 1), k0, k1, o);
+            uint32_t r[4];
+            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u2) >> 1), k0, k1, r);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int a = g + u2 + h;
                 const int gxi = a / kDqnGrid;
                 const int gyi = a - gxi * kDqnGrid;
-                const float r1 = u01(o[2 * h]), r2 = u01(o[2 * h + 1]);
-                const float c = chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
-                const float qc = qv[u2 + h] * c;
-                q[(size_t)a * qs] = qc;
-                total = total + qc;
+                qv[u2 + h] = qv[u2 + h] * chiu_cos((float)gxi + u01(r[2 * h]), (float)gyi + u01(r[2 * h + 1]));
             }
         }
+    };
+    float bs[kSampBlocks];
+#pragma unroll
+    for (int w = 0; w < kSampBlocks; ++w) {
+        float b = 0.0f;
+        for (int g = w * kSampCells; g < (w + 1) * kSampCells; g += kQGroup) {
+            float qv[kQGroup];
+            qcos(g, qv, false);
+#pragma unroll
+            for (int u = 0; u < kQGroup; ++u) {
+                if (WB) q[(size_t)(g + u) * qs] = qv[u];
+                b = b + qv[u];
+            }
+        }
+        bs[w] = b;
     }
+    float total = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kSampBlocks; ++w) total = total + bs[w];
     SampleOut res;
     res.action = -1;
     res.dir = make3(0.0f, 0.0f, 0.0f);
-    float q_sum = 0.0f;
     float qd_sel = 0.0f;
-    for (int g = 0; g < kDqnActions && res.action < 0; g += kQGroup) {
-        float qv[kQGroup];
+    float P = 0.0f;  // P_w
+    for (int w = 0; w < kSampBlocks && res.action < 0; ++w) {
+        const float Pn = P + bs[w] / total;
+        if (Pn > rv) {
+            float cum = P;
+            for (int g = w * kSampCells; g < (w + 1) * kSampCells && res.action < 0; g += kQGroup) {
+                float qv[kQGroup];
+                qcos(g, qv, WB);
 #pragma unroll
-        for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
-#pragma unroll
-        for (int u = 0; u < kQGroup; ++u) {
-            if (res.action < 0) {
-                const float qd = qv[u] / total;
-                q_sum = q_sum + qd;
-                if (q_sum > rv) {
-                    res.action = g + u;
-                    qd_sel = qd;
+                for (int u = 0; u < kQGroup; ++u) {
+                    const float qd = qv[u] / total;
+                    cum = cum + qd;
+                    if (res.action < 0 && cum > rv && qd > 0.0f) {
+                        res.action = g + u;
+                        qd_sel = qd;
+                    }
                 }
             }
         }
+        P = Pn;
     }
     return sample_finish(res.action, qd_sel, N, T, B, pos, pix, smp, ev, k0, k1, tp, update_tp);
 }
@@ -685,7 +732,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
             FUSED ? sample_finish(__float_as_int(a.rays.q[i]), a.rays.q[(size_t)a.rays.ldq + i], make3(N4.x, N4.y, N4.z),
                                   make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                                   1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true)
-                  : sample_from_q(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                  : sample_from_q<false>(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                                   make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                                   1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
@@ -751,7 +798,7 @@ __global__ __launch_bounds__(256) void k_dqn_sample_only(const DeviceScene s, fl
     const float4 T4 = s.shade[t * kShadeF4 + 1];
     const float4 B4 = s.shade[t * kShadeF4 + 2];
     f3 tpv = ld3(tp, i);
-    const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, 1, make3(N4.x, N4.y, N4.z),
+    const SampleOut so = sample_from_q<true>(q + (size_t)i * kDqnActions, 1, make3(N4.x, N4.y, N4.z),
                                        make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), ld3(loc, i),
                                        pix[i], (uint32_t)sample, 1u + (uint32_t)bounce, k0, k1, &tpv, true);
     st3(tp, i, tpv);
@@ -814,7 +861,7 @@ __global__ __launch_bounds__(256) void k_nq_sample(const DqnLaunch a, const NqRa
     philox4x32_10(r.pix[i], (uint32_t)sample, kNqEvGreedy + (uint32_t)bounce, 0u, a.seed_lo, a.seed_hi, o);
     const float rv = u01_oc(o[0]);
     if (rv > eps) {
-        const SampleOut so = sample_from_q(q + (size_t)i * kDqnActions, 1, N, T, B, pos, r.pix[i], (uint32_t)sample,
+        const SampleOut so = sample_from_q<true>(q + (size_t)i * kDqnActions, 1, N, T, B, pos, r.pix[i], (uint32_t)sample,
                                            1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, live);
         if (so.action >= 0) {
             st3(r.dir, i, so.dir);

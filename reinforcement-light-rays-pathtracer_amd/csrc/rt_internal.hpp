@@ -335,7 +335,7 @@ struct SarsaMap {
     int n_kd = 0;
     float root_x = 0.f, root_y = 0.f, root_z = 0.f;  // position of KD element 0 (0 if internal)
     float max_dist = 0.003f;            // MAX_DIST (compared with delta^2)
-    // Exact fast path of the nearest-volume search (rt_sarsa.hip sarsa_nearest_fast):
+    // Exact fast path of the nearest-volume search (rt_sarsa.hip sarsa_nearest_grid):
     // per normal class (volumes whose normals compare equal), a uniform grid of cell
     // size >= grid_h over the class's volume positions.
     int use_grid = 0;

@@ -101,10 +101,13 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
 // 3x3x3 cells around pos, if its distance is below grid_h (so the KD walk visits it)
 // and no other candidate has the same float distance (the KD walk's order would
 // break the tie).  cls: normal class of the hit surface (-1: no volume has its
-// normal, the KD walk keeps volume 0).
-__device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, int* st) {
+// normal, the KD walk keeps volume 0).  Otherwise kNeedWalk: the KD walk decides
+// (sarsa_resolve_walks).
+constexpr int kNeedWalk = -2;  // sarsa_nearest_grid: only the KD walk decides this query
+
+__device__ int sarsa_nearest_grid(const SarsaMap& m, int cls, f3 pos, f3 nrm) {
     if (RT_SARSA_NO_KD) return 0;
-    if (m.use_grid) {
+    {
         if (cls < 0) return 0;
         const float4 G = m.class_org[cls];
         const int4 D = m.class_dim[cls];
@@ -170,7 +173,124 @@ __device__ int sarsa_nearest_fast(const SarsaMap& m, int cls, f3 pos, f3 nrm, in
         if (m.grid_fallbacks != nullptr) atomicAdd(m.grid_fallbacks, 1ull);
         if (RT_SARSA_NO_FALLBACK) return bv >= 0 ? bv : 0;
     }
-    return sarsa_nearest(m, pos, nrm, st);
+    (void)nrm;
+    return kNeedWalk;
+}
+
+#ifndef RT_SARSA_COOP_KD
+#define RT_SARSA_COOP_KD 1  // 0: a grid miss walks the k-d tree on its own lane (A/B builds)
+#endif
+constexpr int kKdFront = kKdStack * 32;  // frontier entries per buffer: two fill a wave's stack block
+
+// sarsa_nearest for ONE query (pos, nrm: wave-uniform values) walked by the whole wave.
+// The walk of sarsa_nearest visits a node iff every ancestor's split lets it through
+// ((q_k - split)^2 < MAX_DIST for the far child), which does not depend on the best found
+// so far: the visited leaves are a fixed set.  Here the wave expands that set level by
+// level (breadth first, one node per lane and step, the frontier in the wave's LDS block)
+// instead of one dependent load per visited node on one lane.  The walk's answer is the
+// first leaf in its visit order with the smallest distance (same len3) and the query's
+// normal, if that distance is below the start distance d0, else volume 0: equal here
+// unless two visited leaves share the smallest distance (then the order decides) -- *ok is
+// false then, on a frontier overflow and for a non-finite query, and the caller walks.
+// All lanes of the wave take part; blk = the wave's kKdStack x 64 block.
+__device__ int sarsa_nearest_wave(const SarsaMap& m, f3 pos, f3 nrm, int* blk, int lane, bool* ok) {
+    const uint4* __restrict__ kd = m.kd4;
+    *ok = false;
+    if (!(__builtin_isfinite(pos.x) && __builtin_isfinite(pos.y) && __builtin_isfinite(pos.z))) return 0;
+    int* cur = blk;
+    int* nxt = blk + kKdFront;
+    wave_lds_sync();  // the block's previous use (stack, exact phase) is done
+    if (lane == 0) cur[0] = 0;
+    wave_lds_sync();
+    int n = 1;
+    float best_d = INFINITY;
+    int best = -1;
+    bool tie = false;
+    while (n > 0) {
+        int m_next = 0;
+        for (int base = 0; base < n; base += 64) {
+            const int i = base + lane;
+            int c0 = -1, c1 = -1;
+            if (i < n) {
+                const uint4 nd = kd[cur[i]];
+                if (nd.w != 0xFFFFFFFFu) {  // leaf
+                    const float d = len3(__uint_as_float(nd.x) - pos.x, __uint_as_float(nd.y) - pos.y,
+                                         __uint_as_float(nd.z) - pos.z);
+                    if (d <= best_d) {
+                        const float4 n4 = m.vol_frame[nd.w * 3];
+                        if (nrm.x == n4.x && nrm.y == n4.y && nrm.z == n4.z) {
+                            tie = (d == best_d);
+                            if (d < best_d) {
+                                best_d = d;
+                                best = (int)nd.w;
+                            }
+                        }
+                    }
+                } else {
+                    const float pc = (nd.z == 0u) ? pos.x : ((nd.z == 1u) ? pos.y : pos.z);
+                    const float delta = pc - __uint_as_float(nd.x);
+                    const int left = (int)nd.y;
+                    c0 = delta < 0.0f ? left : left + 1;
+                    if ((delta * delta) < m.max_dist) c1 = (left + left + 1) - c0;
+                }
+            }
+            // append the children: exclusive prefix of the lanes' counts (0..2) by ballots
+            const int cnt = (c0 >= 0 ? 1 : 0) + (c1 >= 0 ? 1 : 0);
+            const uint64_t b0 = __ballot(cnt & 1), b1 = __ballot(cnt >> 1);
+            const int excl = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u)) +
+                             2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+            const int tot = __builtin_popcountll(b0) + 2 * __builtin_popcountll(b1);
+            if (m_next + tot > kKdFront) return 0;  // (wave-uniform) overflow: the caller walks
+            if (c0 >= 0) nxt[m_next + excl] = c0;
+            if (c1 >= 0) nxt[m_next + excl + 1] = c1;
+            m_next += tot;
+        }
+        wave_lds_sync();  // the next level is written before any lane reads it
+        int* t = cur;
+        cur = nxt;
+        nxt = t;
+        n = m_next;
+    }
+    // the smallest distance over the wave, and whether it is unique
+    float g = best_d;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) g = fminf(g, __shfl_xor(g, off, 64));
+    const bool at_min = best >= 0 && best_d == g;
+    const uint64_t holders = __ballot(at_min), ties = __ballot(at_min && tie);
+    wave_lds_sync();  // the frontier reads are done before the block's next use
+    if (holders == 0ull) {  // no visited leaf has the normal: the start volume
+        *ok = true;
+        return 0;
+    }
+    if (__builtin_popcountll(holders) > 1 || ties != 0ull) return 0;  // the visit order decides
+    const int src = __builtin_ctzll(holders);
+    const int v = __shfl(best, src, 64);
+    const float d0 = len3(pos.x - m.root_x, pos.y - m.root_y, pos.z - m.root_z);
+    *ok = true;
+    return g < d0 ? v : 0;
+}
+
+// every lane with *rv == kNeedWalk gets sarsa_nearest's volume: the wave walks the queries
+// one after another (sarsa_nearest_wave), a lane whose query it cannot settle walks alone.
+// All lanes take part.
+__device__ void sarsa_resolve_walks(const SarsaMap& m, f3 pos, f3 nrm, int* rv, int* blk, int* st, int lane) {
+#if RT_SARSA_COOP_KD
+    uint64_t need = __ballot(*rv == kNeedWalk);
+    while (need != 0ull) {
+        const int L = __builtin_ctzll(need);
+        need &= need - 1ull;
+        const f3 q = make3(__shfl(pos.x, L, 64), __shfl(pos.y, L, 64), __shfl(pos.z, L, 64));
+        const f3 qn = make3(__shfl(nrm.x, L, 64), __shfl(nrm.y, L, 64), __shfl(nrm.z, L, 64));
+        bool ok;
+        const int v = sarsa_nearest_wave(m, q, qn, blk, lane, &ok);
+        if (lane == L && ok) *rv = v;
+    }
+#else
+    (void)blk;
+    (void)lane;
+#endif
+    if (*rv == kNeedWalk) *rv = sarsa_nearest(m, pos, nrm, st);
 }
 
 // normal class of a query normal (queries without a surface index)
@@ -336,17 +456,18 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         const bool active = s < s_end;
         if (__ballot(active) == 0ull) break;
         Hit h;
+        h.t = 0.0f;
+        h.tri = -1;
         if constexpr (MF > 0) {
             wave_lds_sync();  // the previous search's stack accesses stay before the exact phase
             h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active, wl);
             wave_lds_sync();  // and its LDS traffic before the next search
-            if (!active) continue;
-        } else {
-            if (!active) continue;
+        } else if (active) {
             h = closest_hit_sel<RULE>(a.scene, a.use_filter, o, d, a.t_scale);
         }
-        ++n_casts;
-        const bool is_surf = (h.tri >= 0) && (h.tri < n_surf);
+        // (inactive lanes go on to the volume search, which the whole wave runs, with no query)
+        if (active) ++n_casts;
+        const bool is_surf = active && (h.tri >= 0) && (h.tri < n_surf);
         f3 pos = o;
         f3 nrm = make3(0.f, 0.f, 0.f);
         if (is_surf) {
@@ -358,10 +479,15 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         // temporal_difference_update_radiance_volume_sector at every bounce after a
         // sampled sector; the volume at a surface hit serves both the TD target and
         // the next sampling step (one search call site: the search is divergent)
-        const bool td = depth > 0 && cur_rv >= 0 && cur_sector >= 0;
+        const bool td = active && depth > 0 && cur_rv >= 0 && cur_sector >= 0;
         int rv = -1;
         if (is_surf && (depth == 0 || td))
-            rv = sarsa_nearest_fast(m, m.use_grid ? m.tri_class[h.tri] : -1, pos, nrm, st);
+            rv = m.use_grid ? sarsa_nearest_grid(m, m.tri_class[h.tri], pos, nrm) : kNeedWalk;
+        if (m.use_grid)  // the grid's few undecided queries: walked by the whole wave
+            sarsa_resolve_walks(m, pos, nrm, &rv, kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64), st, lane);
+        else if (rv == kNeedWalk)
+            rv = sarsa_nearest(m, pos, nrm, st);
+        if (!active) continue;
         if (td) {
             float target;
             if (h.tri < 0) {
@@ -554,10 +680,19 @@ __global__ __launch_bounds__(256) void k_sarsa_nearest(const SarsaMap m, const f
                                                        const float* __restrict__ nrm, int n, int32_t* out) {
     __shared__ int kd_stack[kKdStack * 256];
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const f3 p = make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]);
-    const f3 nr = make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]);
-    out[i] = sarsa_nearest_fast(m, m.use_grid ? sarsa_class_of(m, nr) : -1, p, nr, kd_stack_of(kd_stack));
+    if (blockIdx.x * 256 + (threadIdx.x & ~63) >= n) return;  // (whole waves past the end)
+    const bool in = i < n;
+    const f3 p = in ? make3(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]) : make3(0.f, 0.f, 0.f);
+    const f3 nr = in ? make3(nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]) : make3(0.f, 0.f, 0.f);
+    int v = -1;
+    if (m.use_grid) {  // as k_sarsa_render searches
+        if (in) v = RT_SARSA_NO_KD ? 0 : sarsa_nearest_grid(m, sarsa_class_of(m, nr), p, nr);
+        sarsa_resolve_walks(m, p, nr, &v, kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64), kd_stack_of(kd_stack),
+                            threadIdx.x & 63);
+    } else if (in) {
+        v = sarsa_nearest(m, p, nr, kd_stack_of(kd_stack));
+    }
+    if (in) out[i] = v;
 }
 
 }  // namespace

@@ -186,7 +186,7 @@ struct Tree {
 };
 
 // Exact fast path of find_closest_radiance_volume_iterative (rt_sarsa.hip
-// sarsa_nearest_fast).  The KD search visits a leaf L iff, at every ancestor whose
+// sarsa_nearest_grid).  The KD search visits a leaf L iff, at every ancestor whose
 // split separates the query q from L, (q_k - split)^2 < MAX_DIST; the split lies
 // between q_k and L_k (left subtrees hold coordinates <= the median, right ones >=),
 // so a leaf whose float distance to q is below h = sqrt(MAX_DIST) * 0.999 is always

@@ -1,0 +1,6 @@
+# DQN sampler in the blocked sum order: tests on the unfused (default) and fused builds, A/B
+V=reinforcement-light-rays-pathtracer_amd/build/variants
+bash tools/gpu.sh r3m "tests:tests/test_dqn.py tests/test_neuralq.py" \
+ "run:tests_fused:400:RTMI_LIB=$V/dqnfused/librtmi.so python3 -u -m pytest tests/test_dqn.py tests/test_neuralq.py -m gpu -x -q --timeout 240 --timeout-method thread" \
+ "run:dqn:300:python3 tools/bench_dqn.py --scene archway --width 512 --spp 16 --steps 2" \
+ "run:dqn_fused:300:RTMI_LIB=$V/dqnfused/librtmi.so python3 tools/bench_dqn.py --scene archway --width 512 --spp 16 --steps 2"
