@@ -85,6 +85,35 @@ def test_oracle_sampler_properties(rtmi_mod, oracle_mod):
     assert np.all(act0 == -1) and np.all(d0 == 0) and np.all(tp0 == 1)
 
 
+def test_oracle_sampler_draws_cells_by_q_cos(rtmi_mod, oracle_mod):
+    """The blocked sum order is still importance_sample_direction's
+    distribution: over many rays the chosen cells follow Q*cos / total (chi-square against
+    the per-ray probabilities the sampler itself returns), a zero cell is never chosen, and
+    every block is reached (mass spread so that each block holds some)."""
+    g = door(rtmi_mod)
+    n = 40000
+    p, tri = room_points(g, n, 3)
+    rng = np.random.default_rng(7)
+    q = (rng.random((n, 144)) * (rng.random((n, 144)) < 0.5)).astype(np.float32)
+    q[:, 20] = 0.0  # a cell never to be drawn
+    pix = np.arange(n, dtype=np.uint32)
+    qc, _, _, act = oracle_mod.dqn_sample(g.all_triangles(), q, p, tri, pix, 0, 1, 1984,
+                                          np.ones((n, 3), np.float32))
+    ok = qc.sum(axis=1) > 0
+    assert ok.mean() > 0.99 and np.all(act[ok] >= 0)
+    act = act[ok]
+    prob = qc[ok] / qc[ok].sum(axis=1, keepdims=True)
+    assert np.all(prob[np.arange(len(act)), act] > 0)            # never a zero-probability cell
+    assert np.all(act != 20)
+    obs = np.bincount(act, minlength=144)
+    exp = prob.sum(axis=0)
+    assert np.all(np.bincount(act // 36, minlength=4) > 0.2 * len(act) / 4)
+    m = exp > 5
+    chi2 = float(((obs[m] - exp[m]) ** 2 / exp[m]).sum())
+    dof = int(m.sum()) - 1
+    assert chi2 < dof + 5.0 * np.sqrt(2.0 * dof), (chi2, dof)    # ~5 sigma
+
+
 # ---------------------------------------------------------------- GPU ----------
 
 @pytest.mark.gpu
