@@ -183,8 +183,6 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         line.update({"peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s"})
     # every timed kernel family's share of the frame's kernel time
     tot = sum(v[0] for v in kt.values())
-    line["kernel_ms_per_step"] = {rtmi.ktime_name(k): round(v[0] / steps, 4)
-                                  for k, v in kt.items() if v[1]}
     line["kernel_share"] = round(kt[fam][0] / tot, 4) if tot else None
     per, frames_matched = (frame_counters(prof, kname, args.warmup, steps) if prof is not None and match
                            else ({}, False))
@@ -220,6 +218,11 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         if bound == "mfma" and bf16:
             line["executed_bf16_tflops"] = round(bf16 * 16384 / t / 1e12, 1)  # 16x16x32 bf16
             line["executed_frac"] = round(line["executed_bf16_tflops"] / MFMA_BF16_PEAK_TFLOPS, 4)
+    if per and line["traffic"]:
+        # the HBM leg of the same kernel: measured DRAM bytes per frame / its time
+        line["hbm_gbs"] = round(line["traffic"] / t / 1e9, 1)
+        line["hbm_frac"] = round(line["hbm_gbs"] / HBM_PEAK_GBS, 4)
+    line["kernels"] = kernel_table(prof if match else None, args, kt)
     if bound == "mfma":
         n_in = geom.nn_vertices.size
         dims = [n_in, 200, 300, 200, 144]
@@ -230,6 +233,10 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         line["achieved"] = round(rows * flop_ray / t / 1e12, 1)
         line["frac"] = round(line["achieved"] / MFMA_BF16_PEAK_TFLOPS, 4)
     else:
+        if line.get("hbm_frac") is not None and line["frac"] is not None and line["hbm_frac"] > line["frac"]:
+            # more of the HBM roof than of the VALU issue roof is in use: HBM bounds it
+            line.update({"bound": "hbm", "achieved": line["hbm_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": line["hbm_frac"], "valu_frac": line["frac"]})
         n_tri = geom.n_tri
         useful = casts_per_frame * 71.0 * n_tri / t / 1e12
         line["brute_force_tflops"] = round(useful, 2)
@@ -238,6 +245,34 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         line["hbm_algorithmic_bytes_per_cast"] = b_cast
         line["hbm_algorithmic_ratio"] = round(casts_per_frame * b_cast / t / 1e9 / HBM_PEAK_GBS, 3)
     return line
+
+
+def kernel_table(prof, args, kt: dict) -> dict:
+    """Every timed kernel family of the frame: its time per step (HIP events) and share, and
+    from the build's profile (when it matches) its VALU issue, matrix-pipe and HBM fractions
+    over that time -- e.g. the DQN frame's k_dqn_bounce beside the k_dqn_mlp roofline."""
+    steps = args.steps
+    tot = sum(v[0] for v in kt.values()) or 1.0
+    out = {}
+    for fam, (ms, n) in kt.items():
+        if not n:
+            continue
+        name = rtmi.ktime_name(fam)
+        t = ms / steps * 1e-3
+        e = {"ms_per_step": round(t * 1e3, 4), "launches_per_step": n / steps, "share": round(ms / tot, 4)}
+        if prof is not None:
+            keys = prof["kernels"]
+            pref = name + "<" if any(k.startswith(name + "<") for k in keys) else name
+            per, _ = frame_counters(prof, pref, args.warmup, steps)
+            if per.get("SQ_INSTS_VALU"):
+                e["valu_issue_frac"] = round(per["SQ_INSTS_VALU"] / t / 1e9 / VALU_ISSUE_PEAK_G, 4)
+            if per.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+                e["mfma_busy_frac"] = round(per["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * 2.4e9 * t), 4)
+            if per.get("hbm_bytes"):
+                e["hbm_bytes_per_step"] = int(per["hbm_bytes"])
+                e["hbm_frac"] = round(per["hbm_bytes"] / t / 1e9 / HBM_PEAK_GBS, 4)
+        out[name] = e
+    return out
 
 
 def cpu_baseline(geom, params, cam_pos, seconds):

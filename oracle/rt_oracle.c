@@ -93,6 +93,9 @@ static float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 /* (0, 1], curand_uniform's range: the SARSA sector draws (r = 0 would pick sector 0 of a
  * zero-mass CDF prefix, which the reference's curand cannot) */
 static float u01_oc(uint32_t x) { return (float)((x >> 8) + 1u) * 0x1p-24f; }
+/* the two 16-bit uniforms of one word (the DQN sampler's cell jitters, rt_math.hpp u16lo/hi) */
+static float u16lo(uint32_t x) { return (float)(x & 0xffffu) * 0x1p-16f; }
+static float u16hi(uint32_t x) { return (float)(x >> 16) * 0x1p-16f; }
 
 /* two uniforms for (pixel, sample, event) */
 static void draw2(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t event, float *a, float *b) {
@@ -883,14 +886,16 @@ static int dqn_sample(float *q, v3 N, v3 pos, uint64_t seed, uint32_t pix, uint3
      * (qd = qc / total), and takes the first cell with cum > rv and qd > 0 (on into the next
      * block if rounding leaves the block without one).  Inside the chosen block this is the
      * reference's own walk; the block sums only change the association of the float sums. */
+    /* the cell jitters: one Philox draw per 4 cells (counter 1 + a/4), cell 4j + h takes the
+     * two 16-bit halves of word h as (x, y) in [0, 1) */
     float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int a2 = 0; a2 < 72; a2++) {
-        ctr[3] = 1u + (uint32_t)a2;
+    for (int j = 0; j < 36; j++) {
+        ctr[3] = 1u + (uint32_t)j;
         orc_philox4x32_10(ctr, key, o);
-        for (int h = 0; h < 2; h++) {
-            int a = 2 * a2 + h;
+        for (int h = 0; h < 4; h++) {
+            int a = 4 * j + h;
             int gxi = a / 12, gyi = a - gxi * 12;
-            float c = chiu_cos((float)gxi + u01(o[2 * h]), (float)gyi + u01(o[2 * h + 1]));
+            float c = chiu_cos((float)gxi + u16lo(o[h]), (float)gyi + u16hi(o[h]));
             float qc = q[a] * c;
             q[a] = qc;
             bsum[a / 36] = bsum[a / 36] + qc;

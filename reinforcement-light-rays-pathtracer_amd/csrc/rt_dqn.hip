@@ -70,7 +70,7 @@ __device__ __forceinline__ int swz(int row, int k, int stride) {
 constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
 // the sampler's fixed sum order: kSampBlocks blocks of kSampCells cells (sample_from_q)
 constexpr int kSampBlocks = 4;
-constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 18 Philox draws
+constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 9 Philox draws
 static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
 
@@ -368,20 +368,20 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
             sample = (uint32_t)(smp.s0 + slot);
         }
         float* const srow = stage + r * kStageStride;
-        // (1) Q*cos of the block's cells (one Philox draw per two cells, counter 1 + a/2), B_w
+        // (1) Q*cos of the block's cells (one Philox draw per four cells, counter 1 + a/4), B_w
         if (live) {
             const int c0 = w * kSampCells;
             float b = 0.0f;
-#pragma unroll 2
-            for (int a = c0; a < c0 + kSampCells; a += 2) {
+#pragma unroll 3
+            for (int a = c0; a < c0 + kSampCells; a += 4) {
                 uint32_t o[4];
-                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a >> 1), smp.k0, smp.k1, o);
-                const float q0 = srow[a] * chiu_cos_cell(a, u01(o[0]), u01(o[1]));
-                const float q1 = srow[a + 1] * chiu_cos_cell(a + 1, u01(o[2]), u01(o[3]));
-                srow[a] = q0;
-                srow[a + 1] = q1;
-                b = b + q0;
-                b = b + q1;
+                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a >> 2), smp.k0, smp.k1, o);
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const float qc = srow[a + h] * chiu_cos_cell(a + h, u16lo(o[h]), u16hi(o[h]));
+                    srow[a + h] = qc;
+                    b = b + qc;
+                }
             }
             bsum[r * kSampBlocks + w] = b;
         }
@@ -525,16 +525,11 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
         for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
         if (stored) return;
 #pragma unroll
-        for (int u2 = 0; u2 < kQGroup; u2 += 2) {
+        for (int u4 = 0; u4 < kQGroup; u4 += 4) {
             uint32_t r[4];
-            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u2) >> 1), k0, k1, r);
+            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u4) >> 2), k0, k1, r);
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int a = g + u2 + h;
-                const int gxi = a / kDqnGrid;
-                const int gyi = a - gxi * kDqnGrid;
-                qv[u2 + h] = qv[u2 + h] * chiu_cos((float)gxi + u01(r[2 * h]), (float)gyi + u01(r[2 * h + 1]));
-            }
+            for (int h = 0; h < 4; ++h) qv[u4 + h] = qv[u4 + h] * chiu_cos_cell(g + u4 + h, u16lo(r[h]), u16hi(r[h]));
         }
     };
     float bs[kSampBlocks];
@@ -1041,7 +1036,7 @@ hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
 }
 
 #ifndef RT_MF_DQN
-#define RT_MF_DQN 0  // 1: the casts on the matrix-core filter (measured equal: DESIGN.md §4)
+#define RT_MF_DQN 1  // 0: the casts on the fp32 filter (archway 512^2 x 16: 125.2 vs 120.9 ms, profiles/r3q)
 #endif
 // 64-triangle blocks of the matrix-core filter for this launch (0: the fp32 filter): the
 // image present and the camera inside its origin bound (as launch_render_t)

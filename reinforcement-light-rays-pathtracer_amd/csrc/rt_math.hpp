@@ -126,6 +126,10 @@ RT_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
 
 // 24-bit uniform in [0, 1)
 RT_HD float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
+// the two 16-bit uniforms of one Philox word, k/2^16 in [0, 1) (the DQN sampler's cell
+// jitters: 4 cells per draw)
+RT_HD float u16lo(uint32_t x) { return (float)(x & 0xffffu) * 0x1p-16f; }
+RT_HD float u16hi(uint32_t x) { return (float)(x >> 16) * 0x1p-16f; }
 // 24-bit uniform in (0, 1], the range of curand_uniform (the SARSA sector draws: r = 0
 // would select sector 0 of an all-zero-mass CDF prefix, which curand cannot)
 RT_HD float u01_oc(uint32_t x) { return (float)((x >> 8) + 1u) * 0x1p-24f; }

@@ -509,7 +509,10 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #define RT_MF_RHO_GROUP 1  // one sign-test threshold per 4-triangle group, the largest (0: per slot, 2: 1/2; 1 measured fastest, profiles/r3i)
 #endif
 #ifndef RT_MF_FIRST_OWN
-#define RT_MF_FIRST_OWN 0  // 1: each lane tests its first candidate itself, the rest shared (A/B)
+// 1: with one 64-triangle block (NB == 1) each lane tests its first candidate itself, the
+// rest shared (Cornell 512^2 x 256: 3.92 vs 4.00 ms; on complex_light_room's four blocks it
+// measured 314 vs 310 ms, so wider scenes share every pair: profiles/r3q/)
+#define RT_MF_FIRST_OWN 1
 #endif
 #ifndef RT_MF_COOP
 #define RT_MF_COOP 1  // 0: each lane runs its own candidates' exact tests (A/B builds)
@@ -794,7 +797,7 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
 #if RT_MF_FIRST_OWN
             // the lane's first candidate on its own lane (its own ray, no pair list: every live
             // lane has one, usually its hit), then the rest (≈ 0.3 per ray) shared by the wave
-            if (Fw != 0ull) {
+            if (NB == 1 && Fw != 0ull) {
                 const int b = __builtin_ctzll(Fw);
                 const float t = exact_tv<RULE>(s.isect, tri0 + b, o, nDx, nDy, nDz);
                 if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
