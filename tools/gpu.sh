@@ -76,7 +76,9 @@ for step in "$@"; do
       pmc_pass "$w" sq1 SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU
       pmc_pass "$w" sq2 SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_BRANCH
       pmc_pass "$w" sq3 SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_F32 GRBM_GUI_ACTIVE
-      run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" "$out/profiles" ;;
+      run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" "$out/profiles"
+      # (the box's scratch tree: later bench / wbench steps of this call find the profile)
+      cp "$out"/profiles/*_bench_pmc.json profiles/ ;;
     collect)
       mkdir -p profiles
       for f in "$out"/profiles/*; do [ -e "$f" ] && cp -v "$f" profiles/; done
