@@ -58,6 +58,10 @@ struct rt_ctx {
     // per-wave candidate masks of rt_cull_masks_device (RenderLaunch::cull)
     unsigned long long* d_cull = nullptr;
     size_t cull_cap = 0;
+    // the GPU preset's chunk sums and work counter (RenderLaunch::csum / work, k_render_pq)
+    float* d_csum = nullptr;
+    size_t csum_cap = 0;
+    unsigned long long* d_work = nullptr;
 };
 
 struct rt_scene {
@@ -220,6 +224,24 @@ int ctx_cull(rt_ctx* ctx, RenderLaunch* a) {
         ctx->cull_cap = words;
     }
     a->cull = ctx->d_cull;
+    return RT_OK;
+}
+
+// The GPU preset's chunk-queue workspace (k_render_pq): one float3 per (pixel, chunk) of the
+// launch and the work counter (grown on demand, kept by the context)
+int ctx_chunks(rt_ctx* ctx, RenderLaunch* a) {
+    if (a->preset != RT_PRESET_GPU) return RT_OK;
+    const size_t n = (size_t)a->n_blocks * 256 * (size_t)a->split * 3;
+    if (n > ctx->csum_cap) {
+        if (ctx->d_csum) RT_HIP(hipFree(ctx->d_csum));
+        ctx->d_csum = nullptr;
+        ctx->csum_cap = 0;
+        RT_HIP(hipMalloc(&ctx->d_csum, sizeof(float) * n));
+        ctx->csum_cap = n;
+    }
+    if (!ctx->d_work) RT_HIP(hipMalloc(&ctx->d_work, sizeof(unsigned long long)));
+    a->csum = ctx->d_csum;
+    a->work = ctx->d_work;
     return RT_OK;
 }
 }  // namespace rt
@@ -572,6 +594,8 @@ int rt_ctx_destroy(rt_ctx* ctx) {
     rt::release_dqn_workspace(ctx);
     if (ctx->d_blocks) (void)hipFree(ctx->d_blocks);
     if (ctx->d_cull) (void)hipFree(ctx->d_cull);
+    if (ctx->d_csum) (void)hipFree(ctx->d_csum);
+    if (ctx->d_work) (void)hipFree(ctx->d_work);
     delete ctx;
     return RT_OK;
 }
@@ -943,7 +967,8 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
         a.out_pitch = w;
         a.out = d_out;
         a.casts = d_casts;
-        e = rt::launch_render(a, 0);
+        if (rt::ctx_chunks(ctx, &a) != RT_OK) e = hipErrorOutOfMemory;
+        if (e == hipSuccess) e = rt::launch_render(a, 0);
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(out_rgb, d_out, out_bytes, hipMemcpyDeviceToHost);
@@ -986,6 +1011,8 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     a.out_pitch = tile_size;
     a.out = d_out;
     a.casts = reinterpret_cast<unsigned long long*>(d_casts);
+    rc = rt::ctx_chunks(ctx, &a);
+    if (rc != RT_OK) return rc;
     // RT_PS_PROF (with an RT_PROF=1 kernel build): k_render_ps's per-phase cycle sums to stderr
     static const bool prof = getenv("RT_PS_PROF") != nullptr;
     if (prof) RT_HIP(hipMalloc(&a.prof, 8 * sizeof(unsigned long long)));

@@ -175,6 +175,10 @@ struct RenderLaunch {
     unsigned long long* cull;
     // RT_PROF builds only: per-phase s_memtime cycle sums of k_render_ps (8 counters)
     unsigned long long* prof;
+    // GPU preset, persistent chunk queue (k_render_pq): the chunk sums [n_blocks * 256 *
+    // split][3] and the work counter (zeroed by the launcher); null: the per-pixel kernels
+    float* csum;
+    unsigned long long* work;
 };
 constexpr int kRenderCullWords = 4;  // candidate masks per wave: scenes of <= 256 triangles
 

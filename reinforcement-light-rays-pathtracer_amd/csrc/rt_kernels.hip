@@ -364,6 +364,185 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
     }
 }
 
+// ---- GPU preset: a persistent grid over a queue of (pixel, chunk) work items ----
+// k_render gives each wave a fixed set of pixels: once their samples are out, the wave's
+// lanes idle until its longest path (up to 80 casts) ends -- 3.21 MFMAs per cast against
+// the 2.63 of full waves on complex_light_room, and sample stealing within the wave does
+// not help.  Here a lane claims a chunk (pixel p, chunk c: samples
+// [c m, (c + 1) m), m = spp / split) from a launch-wide queue, traces its samples one after
+// another summing their values in sample order (k_render's fixed-chunk sum, bit for bit),
+// stores the chunk sum and claims the next; lanes idle only at the end of the whole launch.
+// k_fold_chunks then adds each pixel's chunk sums in chunk order (((P0 + P1) + P2) + ...)
+// and divides by spp, as k_render's fold does.  The wave takes items 64 at a time from the
+// global counter (one atomic per 64 chunks) and hands them to its lanes by ballot rank.
+// Camera inside the matrix-core image's bound (no camera-ray cull), MF > 0.
+template <int SAMPLER, int RULE, int MF>
+__global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const RenderLaunch a) {
+    __shared__ float s_mfw[4 * kMfWaveFloats];
+    float* const wl = s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats;
+    const int lane = threadIdx.x & 63;
+    const float4* __restrict__ shade = a.scene.shade;
+    const int n_surf = a.scene.n_surf;
+    const long long total = (long long)a.n_blocks * 256 * a.split;
+    const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
+    long long qb = 0, qe = 0;  // wave-uniform: the wave's claimed, not yet handed out items
+    bool exhausted = false;     // wave-uniform: the launch's queue is empty
+    bool have = false;          // the lane holds a chunk
+    long long item = 0;
+    int s = 0, s_end = 0, px = 0, py = 0;
+    uint32_t pix = 0;
+    int depth = 0;
+    f3 o = cam, d = make3(0.0f, 0.0f, 1.0f), tp = make3(1.0f, 1.0f, 1.0f), acc = make3(0.0f, 0.0f, 0.0f);
+    unsigned n_casts = 0;
+    auto camera = [&]() {
+        float r1, r2;
+        draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        camera_ray<1>(a, px, py, r1, r2, &d);
+        o = cam;
+        tp = make3(1.0f, 1.0f, 1.0f);
+        depth = 0;
+    };
+    for (;;) {
+        // lanes without a chunk take the next items of the queue
+        if (!exhausted) {
+            const uint64_t need = __ballot(!have);
+            if (need != 0ull) {
+                const int n_need = __builtin_popcountll(need);
+                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const long long avail = qe - qb;
+                long long nb = 0;
+                if (n_need > avail) {  // (wave-uniform) 64 more items
+                    unsigned long long v = 0;
+                    if (lane == 0) v = atomicAdd(a.work, 64ull);
+                    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+                    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+                    nb = (long long)(((unsigned long long)hi << 32) | lo);
+                }
+                if (!have) {
+                    const long long j = rank < avail ? qb + rank : nb + (rank - avail);
+                    if (j < total) {
+                        item = j;
+                        const long long p = j >> a.split_log2;
+                        const int c = (int)(j & (a.split - 1));
+                        const BlockDesc blk = a.blocks[p >> 8];
+                        const int q = (int)(p & 255);
+                        px = blk.px0 + (q & 15);
+                        py = blk.py0 + (q >> 4);
+                        if (px < a.clip_x1 && py < a.clip_y1) {  // (a clipped pixel's chunks: nothing)
+                            pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+                            s = c * a.per_chunk;
+                            s_end = s + a.per_chunk;
+                            acc = make3(0.0f, 0.0f, 0.0f);
+                            have = true;
+                            camera();
+                        }
+                    }
+                }
+                if (n_need > avail) {
+                    qb = nb + (n_need - avail);
+                    qe = nb + 64;
+                } else {
+                    qb += n_need;
+                }
+                if (qb >= total) exhausted = true;
+            }
+        }
+        const bool active = have;
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;  // (every claimed item was a clipped pixel's)
+        }
+        const Hit h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+        if (!active) continue;
+        ++n_casts;
+        bool terminal = false;
+        f3 L = make3(0.0f, 0.0f, 0.0f);
+        if (h.tri < 0) {
+            terminal = true;
+            L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
+        } else if (h.tri >= n_surf) {
+            terminal = true;
+            const float4 e = shade[h.tri * kShadeF4 + 3];
+            L = make3(tp.x * e.x, tp.y * e.y, tp.z * e.z);
+        } else {
+            // as k_render<1, ...>: position, sample a direction, update the throughput
+            const float Dx = d.x * a.t_scale, Dy = d.y * a.t_scale, Dz = d.z * a.t_scale;
+            const f3 pos = make3(o.x + h.t * Dx, o.y + h.t * Dy, o.z + h.t * Dz);
+            const float4 N = shade[h.tri * kShadeF4 + 0];
+            const float4 T = shade[h.tri * kShadeF4 + 1];
+            const float4 B = shade[h.tri * kShadeF4 + 2];
+            float r1, r2;
+            draw2(pix, (uint32_t)s, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
+            float cos_theta, sin_theta;
+            if (SAMPLER == 0) {
+                cos_theta = r1;
+                sin_theta = sqrtf(1.0f - r1 * r1);
+            } else {
+                cos_theta = sqrtf(r1);
+                sin_theta = sqrtf(1.0f - r1);
+            }
+            float sphi, cphi;
+            sincos_turn(r2, &sphi, &cphi);
+            const float sx = sin_theta * cphi, sz = sin_theta * sphi;
+            const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x, (sx * B.y + cos_theta * N.y) + sz * T.y,
+                                (sx * B.z + cos_theta * N.z) + sz * T.z);
+            if (SAMPLER == 0) {
+                const float4 c = shade[h.tri * kShadeF4 + 3];
+                tp.x = div_rho((tp.x * c.x) * cos_theta);
+                tp.y = div_rho((tp.y * c.y) * cos_theta);
+                tp.z = div_rho((tp.z * c.z) * cos_theta);
+            } else {
+                const float4 c = shade[h.tri * kShadeF4 + 4];
+                tp = make3(tp.x * c.x, tp.y * c.y, tp.z * c.z);
+            }
+            o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
+            d = normalize(sd);
+            ++depth;
+            if (depth == a.max_bounces) terminal = true;  // loop exhausted -> 0
+        }
+        if (terminal) {
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+            ++s;
+            if (s < s_end) {
+                camera();
+            } else {
+                store_rgb(a.csum + (size_t)item * 3, acc.x, acc.y, acc.z);
+                have = false;
+            }
+        }
+    }
+    if (a.casts != nullptr) {
+        const unsigned tot = wave_sum(n_casts);
+        if (lane == 0) atomicAdd(a.casts, (unsigned long long)tot);
+    }
+}
+
+// the pixels of k_render_pq's launch: chunk sums in chunk order, / spp (k_render's fold)
+__global__ __launch_bounds__(256) void k_fold_chunks(const RenderLaunch a) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    if (p >= (long long)a.n_blocks * 256) return;
+    const BlockDesc blk = a.blocks[p >> 8];
+    const int q = (int)(p & 255), lx = q & 15, ly = q >> 4;
+    if (blk.px0 + lx >= a.clip_x1 || blk.py0 + ly >= a.clip_y1) return;
+    const float* c = a.csum + (size_t)p * a.split * 3;
+    f3 tot = make3(c[0], c[1], c[2]);
+    for (int k = 1; k < a.split; ++k) {
+        tot.x = tot.x + c[3 * k + 0];
+        tot.y = tot.y + c[3 * k + 1];
+        tot.z = tot.z + c[3 * k + 2];
+    }
+    const float fs = (float)a.spp;
+    float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+    store_rgb(dst, tot.x / fs, tot.y / fs, tot.z / fs);
+}
+
+#ifndef RT_RENDER_PQ
+#define RT_RENDER_PQ 1  // 0: the GPU preset's matrix-core renders keep the per-pixel k_render (A/B)
+#endif
+
 // k_render_ps: the CPU-engine preset (PRESET 0) in two phases per wave.
 //
 // Primary rays are a known family: the camera position and the pixel rectangle of the
@@ -939,6 +1118,25 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
             RenderLaunch b = a;
             b.cam_cull = cam_in ? 0 : 1;
             const bool one = a.scene.n_tri <= 64;
+            if (RT_RENDER_PQ && cam_in && a.csum != nullptr && a.work != nullptr) {
+                (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
+                // a persistent grid: as many workgroups as the device holds at 4 waves per SIMD
+                static int n_cu = 0;
+                if (n_cu == 0) {
+                    int dev = 0;
+                    if (hipGetDevice(&dev) != hipSuccess ||
+                        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                        n_cu <= 0)
+                        n_cu = 256;
+                }
+                const unsigned wgs = (unsigned)min(a.n_blocks * a.split, 4 * n_cu);
+                if (one)
+                    hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1>), dim3(wgs), dim3(256), 0, stream, b);
+                else
+                    hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 4>), dim3(wgs), dim3(256), 0, stream, b);
+                hipLaunchKernelGGL(k_fold_chunks, dim3((unsigned)a.n_blocks), dim3(256), 0, stream, b);
+                return;
+            }
             if (steal && one)
                 hipLaunchKernelGGL((k_render<PRESET, SAMPLER, RULE, true, false, 1>), grid, dim3(256), lds, stream, b);
             else if (steal)
