@@ -409,6 +409,91 @@ __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, 
     atomicAdd(&m.acc_cnt[k], 1u);
 }
 
+// The path's state between casts (k_sarsa_render, k_sarsa_render_pq)
+struct SarsaPath {
+    f3 o, d, tp;
+    int depth, cur_rv, cur_sector;
+    float cur_brdf;
+};
+
+// One cast of path_trace_reinforcement_iterative after its closest hit h and the volume
+// rv at a surface hit: the TD event of the previous step, then light / miss / the next
+// direction from the volume's distribution.  Returns true when the path ends, with its
+// value in *L (n_casts counts the reference's extra cast of a zero direction).
+__device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap& m, const Hit& h, bool is_surf,
+                                           f3 pos, f3 nrm, int rv, bool td, uint32_t pix, int s, SarsaPath& P,
+                                           unsigned& n_casts, f3* L_out) {
+    const float4* __restrict__ shade = a.scene.shade;
+    if (td) {
+        float target;
+        if (h.tri < 0) {
+            target = P.cur_brdf * a.env_light;
+        } else if (!is_surf) {
+            target = P.cur_brdf * m.tri_lum[h.tri];
+        } else {
+            target = (m.accum[rv] * kIrrScale) * P.cur_brdf;
+        }
+        td_event(m, P.cur_rv, P.cur_sector, target);
+        P.cur_rv = rv;
+        P.cur_sector = -1;
+    } else if (P.depth == 0 && is_surf) {
+        P.cur_rv = rv;
+    }
+    bool terminal = false;
+    f3 L = make3(0.f, 0.f, 0.f);
+    if (h.tri < 0) {
+        terminal = true;
+        L = make3(P.tp.x * a.env_light, P.tp.y * a.env_light, P.tp.z * a.env_light);
+    } else if (!is_surf) {
+        terminal = true;
+        const float4 e = shade[h.tri * kShadeF4 + 3];
+        L = make3(P.tp.x * e.x, P.tp.y * e.y, P.tp.z * e.z);
+    } else {
+        uint32_t rn[4];
+        philox4x32_10(pix, a.sample_base + (uint32_t)s, 1u + (uint32_t)P.depth, 0u, a.seed_lo, a.seed_hi, rn);
+        f3 sd;
+        float pdf;
+        bool ok = true;
+        if (P.cur_rv < 0) {  // no volume: uniform hemisphere, pdf = RHO
+            const float4 T4 = shade[h.tri * kShadeF4 + 1], B4 = shade[h.tri * kShadeF4 + 2];
+            const float c = u01(rn[0]);
+            const float st = sqrtf(1.0f - c * c);
+            float sphi, cphi;
+            sincos_turn(u01(rn[1]), &sphi, &cphi);
+            const float sx = st * cphi, sz = st * sphi;
+            sd = make3((sx * B4.x + c * nrm.x) + sz * T4.x, (sx * B4.y + c * nrm.y) + sz * T4.y,
+                       (sx * B4.z + c * nrm.z) + sz * T4.z);
+            pdf = kRho;
+        } else if (m.sample_max) {
+            sarsa_sample_max(m, P.cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
+        } else {
+            ok = sarsa_sample(m, P.cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
+        }
+        if (!ok) {
+            // no sector: the reference traces the zero direction it returns, which
+            // hits nothing (one more cast; its radiance there is NaN, here the miss value)
+            terminal = true;
+            if (P.depth + 1 < a.max_bounces) {
+                ++n_casts;
+                L = make3(P.tp.x * a.env_light, P.tp.y * a.env_light, P.tp.z * a.env_light);
+            }
+        } else {
+            const float4 brdf = shade[h.tri * kShadeF4 + 3];
+            const float cos_theta = dot(nrm, sd);
+            P.cur_brdf = m.tri_lum[h.tri] / kPi;
+            P.tp.x = P.tp.x * ((brdf.x * cos_theta) / pdf);
+            P.tp.y = P.tp.y * ((brdf.y * cos_theta) / pdf);
+            P.tp.z = P.tp.z * ((brdf.z * cos_theta) / pdf);
+            P.o = make3(pos.x + sd.x * kEps, pos.y + sd.y * kEps, pos.z + sd.z * kEps);
+            P.d = normalize(sd);
+            ++P.depth;
+            if (P.depth == a.max_bounces) terminal = true;
+        }
+    }
+    *L_out = L;
+    return terminal;
+}
+
 // path_trace_reinforcement_iterative (reinforcement_path_tracing.cu:50-120), GPU preset
 // MF > 0: every cast on the matrix-core filter (closest_hit_mf, wave-level; the launcher
 // picks it as launch_render_t does for k_render: image present, camera inside its bound)
@@ -488,72 +573,16 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         else if (rv == kNeedWalk)
             rv = sarsa_nearest(m, pos, nrm, st);
         if (!active) continue;
-        if (td) {
-            float target;
-            if (h.tri < 0) {
-                target = cur_brdf * a.env_light;
-            } else if (!is_surf) {
-                target = cur_brdf * m.tri_lum[h.tri];
-            } else {
-                target = (m.accum[rv] * kIrrScale) * cur_brdf;
-            }
-            td_event(m, cur_rv, cur_sector, target);
-            cur_rv = rv;
-            cur_sector = -1;
-        } else if (depth == 0 && is_surf) {
-            cur_rv = rv;
-        }
-        bool terminal = false;
-        f3 L = make3(0.f, 0.f, 0.f);
-        if (h.tri < 0) {
-            terminal = true;
-            L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
-        } else if (!is_surf) {
-            terminal = true;
-            const float4 e = shade[h.tri * kShadeF4 + 3];
-            L = make3(tp.x * e.x, tp.y * e.y, tp.z * e.z);
-        } else {
-            uint32_t rn[4];
-            philox4x32_10(pix, a.sample_base + (uint32_t)s, 1u + (uint32_t)depth, 0u, a.seed_lo, a.seed_hi, rn);
-            f3 sd;
-            float pdf;
-            bool ok = true;
-            if (cur_rv < 0) {  // no volume: uniform hemisphere, pdf = RHO
-                const float4 T4 = shade[h.tri * kShadeF4 + 1], B4 = shade[h.tri * kShadeF4 + 2];
-                const float c = u01(rn[0]);
-                const float st = sqrtf(1.0f - c * c);
-                float sphi, cphi;
-                sincos_turn(u01(rn[1]), &sphi, &cphi);
-                const float sx = st * cphi, sz = st * sphi;
-                sd = make3((sx * B4.x + c * nrm.x) + sz * T4.x, (sx * B4.y + c * nrm.y) + sz * T4.y,
-                           (sx * B4.z + c * nrm.z) + sz * T4.z);
-                pdf = kRho;
-            } else if (m.sample_max) {
-                sarsa_sample_max(m, cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
-            } else {
-                ok = sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
-            }
-            if (!ok) {
-                // no sector: the reference traces the zero direction it returns, which
-                // hits nothing (one more cast; its radiance there is NaN, here the miss value)
-                terminal = true;
-                if (depth + 1 < a.max_bounces) {
-                    ++n_casts;
-                    L = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
-                }
-            } else {
-                const float4 brdf = shade[h.tri * kShadeF4 + 3];
-                const float cos_theta = dot(nrm, sd);
-                cur_brdf = m.tri_lum[h.tri] / kPi;
-                tp.x = tp.x * ((brdf.x * cos_theta) / pdf);
-                tp.y = tp.y * ((brdf.y * cos_theta) / pdf);
-                tp.z = tp.z * ((brdf.z * cos_theta) / pdf);
-                o = make3(pos.x + sd.x * kEps, pos.y + sd.y * kEps, pos.z + sd.z * kEps);
-                d = normalize(sd);
-                ++depth;
-                if (depth == a.max_bounces) terminal = true;
-            }
-        }
+        SarsaPath P{o, d, tp, depth, cur_rv, cur_sector, cur_brdf};
+        f3 L;
+        const bool terminal = sarsa_step(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
+        o = P.o;
+        d = P.d;
+        tp = P.tp;
+        depth = P.depth;
+        cur_rv = P.cur_rv;
+        cur_sector = P.cur_sector;
+        cur_brdf = P.cur_brdf;
         if (terminal) {
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
@@ -602,6 +631,182 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
         if (lane == 0) atomicAdd(a.casts, (unsigned long long)total);
+    }
+}
+
+// k_sarsa_render on a persistent grid over a launch-wide (pixel, chunk) queue, as
+// k_render_pq does for the GPU preset (rt_kernels.hip): a lane claims a chunk (the samples
+// [c m, (c + 1) m) of pixel p), traces them one after another with k_sarsa_render's
+// per-cast work (sarsa_step) and its fixed-chunk sum, stores the chunk's value sum and ray
+// casts, and claims the next, so lanes idle only at the end of the frame instead of at
+// each wave's longest path (frame 0: 41 casts per path on door_room, up to 80).
+// k_sarsa_fold adds each pixel's chunks in chunk order and takes its path-length statistic.
+// The volume search still runs with every lane of the wave (the walks of the grid's
+// undecided queries, sarsa_resolve_walks).  csum: float4 per chunk {r, g, b, casts (bits)}.
+template <int RULE, int MF = 0>
+__global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_render_pq(const RenderLaunch a,
+                                                                                        const SarsaMap m) {
+    __shared__ int kd_stack[kKdStack * 256];
+    int* const st = kd_stack_of(kd_stack);
+    int* const blk_ws = kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64);  // the wave's block
+    float* const wl = reinterpret_cast<float*>(blk_ws);
+    const int lane = threadIdx.x & 63;
+    const float4* __restrict__ shade = a.scene.shade;
+    const int n_surf = a.scene.n_surf;
+    const long long total = (long long)a.n_blocks * 256 * a.split;
+    const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
+    long long qb = 0, qe = 0;  // wave-uniform: the wave's claimed, not yet handed out items
+    bool exhausted = false;
+    bool have = false;
+    long long item = 0;
+    int s = 0, s_end = 0, px = 0, py = 0;
+    uint32_t pix = 0;
+    SarsaPath P{cam, make3(0.f, 0.f, 1.f), make3(1.f, 1.f, 1.f), 0, -1, -1, 0.0f};
+    f3 acc = make3(0.f, 0.f, 0.f);
+    unsigned n_casts = 0, n_zero = 0, casts0 = 0;
+    auto camera = [&]() {
+        float r1, r2;
+        draw2(pix, a.sample_base + (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        camera_ray<1>(a, px, py, r1, r2, &P.d);
+        P.o = cam;
+        P.tp = make3(1.f, 1.f, 1.f);
+        P.depth = 0;
+        P.cur_rv = -1;
+        P.cur_sector = -1;
+    };
+    for (;;) {
+        if (!exhausted) {
+            const uint64_t need = __ballot(!have);
+            if (need != 0ull) {
+                const int n_need = __builtin_popcountll(need);
+                const int rank = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const long long avail = qe - qb;
+                long long nb = 0;
+                if (n_need > avail) {  // (wave-uniform) 64 more items
+                    unsigned long long v = 0;
+                    if (lane == 0) v = atomicAdd(a.work, 64ull);
+                    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+                    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+                    nb = (long long)(((unsigned long long)hi << 32) | lo);
+                }
+                if (!have) {
+                    const long long j = rank < avail ? qb + rank : nb + (rank - avail);
+                    if (j < total) {
+                        item = j;
+                        const long long p = j >> a.split_log2;
+                        const int c = (int)(j & (a.split - 1));
+                        const BlockDesc blk = a.blocks[p >> 8];
+                        const int q = (int)(p & 255);
+                        px = blk.px0 + (q & 15);
+                        py = blk.py0 + (q >> 4);
+                        if (px < a.clip_x1 && py < a.clip_y1) {
+                            pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+                            s = c * a.per_chunk;
+                            s_end = s + a.per_chunk;
+                            acc = make3(0.f, 0.f, 0.f);
+                            casts0 = n_casts;
+                            have = true;
+                            camera();
+                        }
+                    }
+                }
+                if (n_need > avail) {
+                    qb = nb + (n_need - avail);
+                    qe = nb + 64;
+                } else {
+                    qb += n_need;
+                }
+                if (qb >= total) exhausted = true;
+            }
+        }
+        const bool active = have;
+        if (__ballot(active) == 0ull) {
+            if (exhausted) break;
+            continue;
+        }
+        Hit h;
+        h.t = 0.0f;
+        h.tri = -1;
+        if constexpr (MF > 0) {
+            wave_lds_sync();
+            h = closest_hit_mf<RULE, false, MF>(a.scene, P.o, P.d, a.t_scale, active, wl);
+            wave_lds_sync();
+        } else if (active) {
+            h = closest_hit_sel<RULE>(a.scene, a.use_filter, P.o, P.d, a.t_scale);
+        }
+        if (active) ++n_casts;
+        const bool is_surf = active && (h.tri >= 0) && (h.tri < n_surf);
+        f3 pos = P.o;
+        f3 nrm = make3(0.f, 0.f, 0.f);
+        if (is_surf) {
+            const float Dx = P.d.x * a.t_scale, Dy = P.d.y * a.t_scale, Dz = P.d.z * a.t_scale;
+            pos = make3(P.o.x + h.t * Dx, P.o.y + h.t * Dy, P.o.z + h.t * Dz);
+            const float4 N4 = shade[h.tri * kShadeF4 + 0];
+            nrm = make3(N4.x, N4.y, N4.z);
+        }
+        const bool td = active && P.depth > 0 && P.cur_rv >= 0 && P.cur_sector >= 0;
+        int rv = -1;
+        if (is_surf && (P.depth == 0 || td))
+            rv = m.use_grid ? sarsa_nearest_grid(m, m.tri_class[h.tri], pos, nrm) : kNeedWalk;
+        if (m.use_grid)
+            sarsa_resolve_walks(m, pos, nrm, &rv, blk_ws, st, lane);
+        else if (rv == kNeedWalk)
+            rv = sarsa_nearest(m, pos, nrm, st);
+        if (!active) continue;
+        f3 L;
+        if (sarsa_step(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L)) {
+            acc.x = acc.x + L.x;
+            acc.y = acc.y + L.y;
+            acc.z = acc.z + L.z;
+            n_zero += ((L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
+            ++s;
+            if (s < s_end) {
+                camera();
+            } else {
+                reinterpret_cast<float4*>(a.csum)[item] = make_float4(acc.x, acc.y, acc.z, __uint_as_float(n_casts - casts0));
+                have = false;
+            }
+        }
+    }
+    if (m.stats != nullptr) {
+        const unsigned sz = wave_sum(n_zero);
+        if (lane == 0) atomicAdd(&m.stats[1], (unsigned long long)sz);
+    }
+    if (a.casts != nullptr) {
+        const unsigned tot = wave_sum(n_casts);
+        if (lane == 0) atomicAdd(a.casts, (unsigned long long)tot);
+    }
+}
+
+// the pixels of k_sarsa_render_pq's launch: the chunk sums in chunk order / spp, and the
+// per-pixel statistic int(path lengths / SAMPLES_PER_PIXEL) (main.cu:321-339)
+__global__ __launch_bounds__(256) void k_sarsa_fold(const RenderLaunch a, const SarsaMap m) {
+    const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+    const BlockDesc blk = a.blocks[blockIdx.x];
+    const int q = threadIdx.x, lx = q & 15, ly = q >> 4;
+    const bool valid = (blk.px0 + lx < a.clip_x1) && (blk.py0 + ly < a.clip_y1);
+    unsigned pf = 0;
+    if (valid) {
+        const float4* c = reinterpret_cast<const float4*>(a.csum) + (size_t)p * a.split;
+        float4 v = c[0];
+        f3 tot = make3(v.x, v.y, v.z);
+        unsigned pix_casts = __float_as_uint(v.w);
+        for (int k = 1; k < a.split; ++k) {
+            v = c[k];
+            tot.x = tot.x + v.x;
+            tot.y = tot.y + v.y;
+            tot.z = tot.z + v.z;
+            pix_casts += __float_as_uint(v.w);
+        }
+        pf = pix_casts / (unsigned)a.spp;
+        const float fs = (float)a.spp;
+        float* dst = a.out + ((size_t)(blk.oy0 + ly) * (size_t)a.out_pitch + (size_t)(blk.ox0 + lx)) * 3;
+        store_rgb(dst, tot.x / fs, tot.y / fs, tot.z / fs);
+    }
+    if (m.stats != nullptr) {
+        const unsigned sp = wave_sum(pf);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&m.stats[0], (unsigned long long)sp);
     }
 }
 
@@ -708,6 +913,10 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 #define RT_MF_SARSA 0  // 1: the casts on the matrix-core filter (measured slower: DESIGN.md §4)
 #endif
 
+#ifndef RT_SARSA_PQ
+#define RT_SARSA_PQ 1  // 0: the per-pixel k_sarsa_render (A/B builds)
+#endif
+
 hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
     if (a.n_blocks <= 0) return hipSuccess;
     KernelTimer kt(KT_SARSA_RENDER, stream);
@@ -715,6 +924,34 @@ hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStre
     const bool mf = RT_MF_SARSA && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
                     fabsf(a.cam_z) <= cb;
+    if (RT_SARSA_PQ && a.csum != nullptr && a.work != nullptr) {
+        (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
+        static int n_cu = 0;
+        if (n_cu == 0) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+                n_cu = 256;
+        }
+        const dim3 grid((unsigned)min(a.n_blocks * a.split, 5 * n_cu));  // 5 workgroups per CU fit (89 VGPRs, 32 KB)
+        const bool one = a.scene.n_tri <= 64;
+        if (mf) {
+            if (a.hit_rule == 0 && one)
+                hipLaunchKernelGGL((k_sarsa_render_pq<0, 1>), grid, dim3(256), 0, stream, a, m);
+            else if (a.hit_rule == 0)
+                hipLaunchKernelGGL((k_sarsa_render_pq<0, 4>), grid, dim3(256), 0, stream, a, m);
+            else if (one)
+                hipLaunchKernelGGL((k_sarsa_render_pq<1, 1>), grid, dim3(256), 0, stream, a, m);
+            else
+                hipLaunchKernelGGL((k_sarsa_render_pq<1, 4>), grid, dim3(256), 0, stream, a, m);
+        } else if (a.hit_rule == 0) {
+            hipLaunchKernelGGL((k_sarsa_render_pq<0>), grid, dim3(256), 0, stream, a, m);
+        } else {
+            hipLaunchKernelGGL((k_sarsa_render_pq<1>), grid, dim3(256), 0, stream, a, m);
+        }
+        hipLaunchKernelGGL(k_sarsa_fold, dim3((unsigned)a.n_blocks), dim3(256), 0, stream, a, m);
+        return hipGetLastError();
+    }
     if (mf) {
         const dim3 grid((unsigned)(a.n_blocks * a.split));
         const bool one = a.scene.n_tri <= 64;

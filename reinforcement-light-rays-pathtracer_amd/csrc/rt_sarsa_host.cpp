@@ -358,9 +358,15 @@ struct rt_sarsa {
     int64_t grid_cells = 0;   // nearest-volume grid (0: none, every search walks the KD tree)
     rt::SarsaMap m;
     std::vector<void*> allocs;
+    // k_sarsa_render_pq's chunk sums and work counter (grown on demand)
+    float* d_csum = nullptr;
+    size_t csum_cap = 0;
+    unsigned long long* d_work = nullptr;
     ~rt_sarsa() {
         (void)hipSetDevice(device);
         for (void* p : allocs) (void)hipFree(p);
+        if (d_csum) (void)hipFree(d_csum);
+        if (d_work) (void)hipFree(d_work);
     }
     template <class T>
     hipError_t alloc(T** p, size_t count) {
@@ -410,6 +416,18 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
     a.out = d_out;
     a.casts = d_casts;
     a.sample_base = sa->frames * (uint32_t)p->spp;
+    // the persistent kernel's chunk sums (float4 per (pixel, chunk)) and work counter
+    const size_t nc = (size_t)n_blocks * 256 * (size_t)a.split * 4;
+    if (nc > sa->csum_cap) {
+        if (sa->d_csum) (void)hipFree(sa->d_csum);
+        sa->d_csum = nullptr;
+        sa->csum_cap = 0;
+        RT_HIPE(hipMalloc(&sa->d_csum, sizeof(float) * nc));
+        sa->csum_cap = nc;
+    }
+    if (!sa->d_work) RT_HIPE(hipMalloc(&sa->d_work, sizeof(unsigned long long)));
+    a.csum = sa->d_csum;
+    a.work = sa->d_work;
     RT_HIPE(hipMemsetAsync(sa->m.stats, 0, 2 * sizeof(unsigned long long), stream));
     RT_HIPE(rt::launch_sarsa_render(a, sa->m, stream));
     if (apply) RT_HIPE(rt::launch_sarsa_apply(sa->m, stream));
