@@ -31,6 +31,7 @@ import glob
 import hashlib
 import json
 import os
+import re
 import sys
 import time
 
@@ -68,6 +69,21 @@ ROOF = {
     "door_room_sarsa": (rtmi.RT_KT_SARSA_RENDER, "k_sarsa_render<", "valu", "rt_sarsa.o"),
     "archway_dqn": (rtmi.RT_KT_DQN_MLP, "k_dqn_mlp<", "mfma", "rt_dqn.o"),
 }
+# the kernels a timed family launches (rt_ktime times the launcher, so its time covers them
+# all): the persistent GPU-preset and SARSA renders and their folds (k_render_pq,
+# k_fold_chunks; k_sarsa_render_pq, k_sarsa_fold) count with k_render / k_sarsa_render
+FAMILY_RE = {
+    "k_render<": r"^k_render(_pq)?<|^k_fold_chunks$",
+    "k_sarsa_render<": r"^k_sarsa_render(_pq)?<|^k_sarsa_fold$",
+}
+
+
+def family_re(kernel: str) -> str:
+    """profile-key pattern of the kernels behind a family name ('k_x<' or 'k_x')"""
+    if kernel in FAMILY_RE:
+        return FAMILY_RE[kernel]
+    base = re.escape(kernel.rstrip("<"))
+    return rf"^{base}(<|$)"
 # committed rocprofv3 PMC profiles (tools/gpu.sh pmc:<workload> -> tools/bench_pmc_summary.py)
 PMC_GLOB = os.path.join(ROOT, "profiles", "*_bench_pmc.json")
 
@@ -130,7 +146,7 @@ def frame_counters(prof, kernel: str, warmup: int, steps: int):
     """Counters of the kernel per frame: the profiled frames [warmup, warmup + steps) when the
     profile ran the bench's own frames (learning workloads differ frame to frame), else the
     mean over its frames; old profiles: the per-dispatch means (one launch per frame)."""
-    ks = [k for k in prof["kernels"] if k.startswith(kernel) or ("::" + kernel) in k]
+    ks = [k for k in prof["kernels"] if re.search(family_re(kernel), k.split("::")[-1])]
     per = {}
     matched = False
     for k in ks:
@@ -261,9 +277,7 @@ def kernel_table(prof, args, kt: dict) -> dict:
         t = ms / steps * 1e-3
         e = {"ms_per_step": round(t * 1e3, 4), "launches_per_step": n / steps, "share": round(ms / tot, 4)}
         if prof is not None:
-            keys = prof["kernels"]
-            pref = name + "<" if any(k.startswith(name + "<") for k in keys) else name
-            per, _ = frame_counters(prof, pref, args.warmup, steps)
+            per, _ = frame_counters(prof, name + "<", args.warmup, steps)
             if per.get("SQ_INSTS_VALU"):
                 e["valu_issue_frac"] = round(per["SQ_INSTS_VALU"] / t / 1e9 / VALU_ISSUE_PEAK_G, 4)
             if per.get("SQ_VALU_MFMA_BUSY_CYCLES"):

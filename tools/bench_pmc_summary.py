@@ -38,9 +38,10 @@ LIB = os.path.join(BUILD, "librtmi.so")
 WORKLOADS = {
     "cornell": (r"::k_render_ps<|::k_cull", r"::k_render_ps<", "rt_kernels.o",
                 "--steps 4 --warmup 3 --cpu-seconds 0 --no-parity"),
-    "complex_light": (r"::k_render<", r"::k_render<", "rt_kernels.o",
+    # (the GPU preset's matrix-core renders run k_render_pq + k_fold_chunks; per-pixel k_render otherwise)
+    "complex_light": (r"::k_render(_pq)?<|::k_fold_chunks", r"::k_render(_pq)?<", "rt_kernels.o",
                       "--workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity"),
-    "door_room_sarsa": (r"::k_sarsa_", r"::k_sarsa_render<", "rt_sarsa.o",
+    "door_room_sarsa": (r"::k_sarsa_", r"::k_sarsa_render(_pq)?<", "rt_sarsa.o",
                         "--workload door_room_sarsa --steps 4 --warmup 1 --cpu-seconds 0"),
     "archway_dqn": (r"::k_dqn_", r"::k_dqn_frame_begin", "rt_dqn.o",
                     "--workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0"),
