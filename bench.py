@@ -188,7 +188,12 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
     triangle per cast as if streamed: not a bound on these kernels)."""
     fam, kname, bound, _ = ROOF[args.workload]
     steps = args.steps
+    if not kt[fam][1]:  # (this configuration ran another kernel family: the one that took the time)
+        fam = max(kt, key=lambda f: kt[f][0])
+        kname = rtmi.ktime_name(fam) + "<"
     t = kt[fam][0] / steps * 1e-3  # s per frame in the dominant kernel
+    if t <= 0.0:
+        return {"bound": bound, "achieved": None, "frac": None, "traffic": None, "kernel": None}
     path, prof, match = load_profile(args.workload)
     line = {"bound": bound, "achieved": None, "frac": None, "traffic": None, "kernel": kname.rstrip("<"),
             "kernel_ms": round(t * 1e3, 4), "kernel_launches_per_step": kt[fam][1] / steps,
