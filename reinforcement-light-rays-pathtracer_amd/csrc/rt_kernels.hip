@@ -1129,7 +1129,7 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                         n_cu <= 0)
                         n_cu = 256;
                 }
-                const unsigned wgs = (unsigned)min(a.n_blocks * a.split, 4 * n_cu);
+                const unsigned wgs = (unsigned)min(a.n_blocks * a.split, RT_MF_RENDER_WAVES * n_cu);
                 if (one)
                     hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1>), dim3(wgs), dim3(256), 0, stream, b);
                 else
