@@ -13,7 +13,7 @@ so their TD sums are all-reduced between ranks every step).
 
 Multi-GPU: the frame is cut into 32x32 tiles dealt to the ranks by diagonals (rtmi.tiles; one
 process per GPU); each rank renders its tiles with the HIP kernels, and the per-rank tile
-buffers are all-gathered over RCCL into the full image -- asynchronously, into one of two
+buffers are gathered to rank 0 over RCCL into the full image -- asynchronously, into one of two
 buffers, so frame i+1 renders while frame i is exchanged.  The frame is fixed as N grows:
 strong scaling.
 
@@ -436,7 +436,7 @@ def main():
             rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(), casts.data_ptr(),
                                      stream.cuda_stream)
 
-    # two frame buffers: frame i+1 renders while frame i is all-gathered over RCCL
+    # two frame buffers: frame i+1 renders while frame i is gathered to rank 0 over RCCL
     pipe = rtmi.dist.FramePipeline(render, (k, TILE, TILE, 3), world, dev)
     for i in range(args.warmup):
         pipe.gather_frame(pipe.render_frame(i))
