@@ -130,9 +130,9 @@ def c4(ctx, stream, spp):
             "ms_512spp_extrapolated": round(ms * 512 / spp, 0), "weights": "synthetic He-normal seed 1984"}
 
 
-def c5(ctx, stream, spp, world=8):
+def c5(ctx, stream, spp, world=8, split=8):
     g = rtmi.obj_geometry(os.path.join(MODELS, "complex_light_room.obj"), "complex_light_room")
-    p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=2048, height=2048, spp=spp, spp_split=8)
+    p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=2048, height=2048, spp=spp, spp_split=split)
     cam = rtmi.camera(rtmi.CAMERAS["complex_light_room"])
     per = []
     tot = 0
@@ -143,7 +143,7 @@ def c5(ctx, stream, spp, world=8):
             ms, casts, _ = tile_render(ctx, sc, cam, p, tiles, stream, 1)
             per.append(round(ms, 2))
             tot += casts
-    return {"spp": spp, "ranks": world, "ms_per_rank": per, "ms_8gpu_kernel": max(per),
+    return {"spp": spp, "spp_split": split, "ranks": world, "ms_per_rank": per, "ms_8gpu_kernel": max(per),
             "ms_1gpu": round(sum(per), 2), "kernel_speedup_8": round(sum(per) / max(per), 3),
             "ray_casts": tot, "mrays_s_1gpu": round(tot / sum(per) / 1e3, 1),
             "ms_1024spp_8gpu_extrapolated": round(max(per) * 1024 / spp, 0)}
@@ -195,6 +195,7 @@ def main():
     ap.add_argument("--sarsa-frames", type=int, default=3)
     ap.add_argument("--dqn-spp", type=int, default=16)
     ap.add_argument("--c5-spp", type=int, default=64)
+    ap.add_argument("--c5-split", type=int, default=32)  # bench.py's config-5 split
     ap.add_argument("--only", nargs="*", default=None)
     ap.add_argument("--cpu", nargs="*", default=["c3", "c4", "c5"],
                     help="configs whose CPU-restatement rate to measure (empty: none)")
@@ -204,7 +205,7 @@ def main():
     with rtmi.Context(0) as ctx:
         steps = {"c1": lambda: c1(ctx, stream), "c2": lambda: c2(ctx, stream),
                  "c3": lambda: c3(ctx, stream, args.sarsa_frames), "c4": lambda: c4(ctx, stream, args.dqn_spp),
-                 "c5": lambda: c5(ctx, stream, args.c5_spp)}
+                 "c5": lambda: c5(ctx, stream, args.c5_spp, split=args.c5_split)}
         for k, fn in steps.items():
             if args.only and k not in args.only:
                 continue
