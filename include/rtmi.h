@@ -360,6 +360,21 @@ int rt_sarsa_set_search(rt_sarsa* sarsa, int mode);
 #define RT_SARSA_SAMPLE_CDF 0
 #define RT_SARSA_SAMPLE_MAX 1
 int rt_sarsa_set_sampling(rt_sarsa* sarsa, int mode);
+/* TD learning rule (replaces the reference's in-kernel update,
+ * GPU/radiance_volumes/radiance_volume.cu:282-301 temporal_difference_update and :93-112
+ * expected_sarsa_irradiance, called from radiance_map.cu:90-146):
+ * RT_SARSA_TD_FRAME (default) every TD target of a frame goes into a per-sector
+ *   fixed-point sum and count; the frame end folds them into Q in closed form (the running
+ *   mean alpha = 1/(1 + visits) gives) -- deterministic, bit-exact against oracle/, the same
+ *   on any GPU count;
+ * RT_SARSA_TD_INFRAME the reference's own rule: each event updates the sector's Q, visits
+ *   and the volume's irradiance in place while the frame renders (later targets of the same
+ *   frame see it; concurrent updates race as in the reference).  The CDFs still change only
+ *   at the frame end (update_radiance_volume_distributions).  Not reproducible run to run;
+ *   one GPU only (the cross-GPU TD sums stay empty). */
+#define RT_SARSA_TD_FRAME 0
+#define RT_SARSA_TD_INFRAME 1
+int rt_sarsa_set_td_mode(rt_sarsa* sarsa, int mode);
 /* Training statistics of the last frame rendered (GPU/main.cu:321-339, one line of
  * Radiance_Map_Data/sarsa_training_stats.txt per frame): path_floor_sum = the sum over the
  * frame's pixels of int(path lengths / spp) (path_trace_reinforcement,

@@ -357,6 +357,9 @@ struct SarsaMap {
     // sampling rule: 0 = the CDF (sample_direction_from_radiance_distribution), 1 = the
     // sector of largest Q (sample_max_direction_from_radiance_distribution)
     int sample_max = 0;
+    // TD rule: 0 = frame-synchronous sums folded by k_sarsa_apply (deterministic), 1 = the
+    // reference's in-frame update of Q, visits and irradiance at each event (racy)
+    int td_inframe = 0;
     int32_t* qmax = nullptr;               // [n] first sector of largest Q (k_sarsa_apply)
     unsigned long long* stats = nullptr;   // [2] launch: sum of per-pixel int(mean path length), zero paths
 };

@@ -401,8 +401,31 @@ __device__ void sarsa_sample_max(const SarsaMap& m, int rv, float rx, float ry, 
                           make3(B4.x, B4.y, B4.z), make3(N4.w, T4.w, B4.w));
 }
 
+// temporal_difference_update + expected_sarsa_irradiance as the reference runs them
+// (radiance_volume.cu:282-301, :93-112): read-modify-write of the sector's Q and the
+// volume's irradiance while other lanes do the same -- a lost update is the reference's own
+// race.  The visit count comes from the atomic's return (the reference reads it first).
+__device__ __forceinline__ void td_event_inframe(const SarsaMap& m, int rv, int sector, float target) {
+    const size_t k = (size_t)rv * kSarsaSectors + sector;
+    const uint32_t vs = atomicAdd(&m.visits[k], 1u);
+    const float alpha = 1.f / (1.f + (float)vs);
+    const float q_old = m.Q[k];
+    float upd = ((1.f - alpha) * q_old) + (alpha * target);
+    upd = upd > kRadianceThreshold ? upd : kRadianceThreshold;
+    const float cc = m.cos_corner[k];
+    const float brdf = m.vol_brdf[rv];
+    const float acc = m.accum[rv];
+    const float acc_new = (acc - ((q_old * cc) * brdf)) + ((upd * cc) * brdf);
+    atomicExch(&m.Q[k], upd);
+    atomicExch(&m.accum[rv], acc_new);
+}
+
 __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, float target) {
     if (RT_SARSA_NO_TD) return;
+    if (m.td_inframe) {
+        td_event_inframe(m, rv, sector, target);
+        return;
+    }
     const long long v = __float2ll_rn(target * 4294967296.0f);
     const size_t k = (size_t)rv * kSarsaSectors + sector;
     atomicAdd(&m.acc_sum[k], (unsigned long long)v);

@@ -819,6 +819,13 @@ int rt_sarsa_set_sampling(rt_sarsa* sa, int mode) {
     return RT_OK;
 }
 
+int rt_sarsa_set_td_mode(rt_sarsa* sa, int mode) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (mode != RT_SARSA_TD_FRAME && mode != RT_SARSA_TD_INFRAME) return err(RT_E_INVALID, "bad TD mode");
+    sa->m.td_inframe = mode == RT_SARSA_TD_INFRAME;
+    return RT_OK;
+}
+
 int rt_sarsa_frame_stats(const rt_sarsa* sa, uint64_t* path_floor_sum, uint64_t* zero_paths) {
     if (!sa) return err(RT_E_INVALID, "NULL argument");
     unsigned long long v[2] = {0, 0};

@@ -92,6 +92,11 @@ class RadianceMap {
     void set_sample_max_direction(bool on) {
         detail::check(rt_sarsa_set_sampling(map_, on ? RT_SARSA_SAMPLE_MAX : RT_SARSA_SAMPLE_CDF));
     }
+    // the reference's racy in-frame TD update (radiance_volume.cu:282-301) instead of the
+    // deterministic frame-synchronous fold (one GPU)
+    void set_in_frame_td(bool on) {
+        detail::check(rt_sarsa_set_td_mode(map_, on ? RT_SARSA_TD_INFRAME : RT_SARSA_TD_FRAME));
+    }
     // GPU/main.cu:321-339 after a frame: the average path length as the reference computes it
     // (int(sum over pixels of int(path lengths / spp)) / pixels)) and the zero-contribution
     // paths; append_training_stats writes its "avg 0 zero" line.

@@ -8,6 +8,7 @@
   .read() / .volumes() / .nearest(pos, nrm)   Q-table, placement, KD queries (parity)
   .save_q(path) / .load_q(path)   radiance_map_data.txt out and back in (resume a trained map)
   .set_sampling(SAMPLE_MAX)       sample_max_direction_from_radiance_distribution
+  .set_td_mode(TD_INFRAME)        the reference's racy in-frame TD update (one GPU)
   .frame_stats() / .append_stats_line(path)   sarsa_training_stats.txt (GPU/main.cu:321-339)
 """
 from __future__ import annotations
@@ -25,6 +26,8 @@ SEARCH_KD = 0    # RT_SARSA_SEARCH_KD
 SEARCH_GRID = 1  # RT_SARSA_SEARCH_GRID
 SAMPLE_CDF = 0   # RT_SARSA_SAMPLE_CDF
 SAMPLE_MAX = 1   # RT_SARSA_SAMPLE_MAX
+TD_FRAME = 0     # RT_SARSA_TD_FRAME
+TD_INFRAME = 1   # RT_SARSA_TD_INFRAME
 
 SECTORS = 144  # GRID_RESOLUTION^2
 
@@ -42,6 +45,7 @@ class RadianceMap:
         nv, nk, fr = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_uint32(0)
         check(lib().rt_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk), ctypes.byref(fr)))
         self.n_volumes, self.n_nodes = nv.value, nk.value
+        self.td_mode = TD_FRAME
 
     @property
     def handle(self):
@@ -77,6 +81,12 @@ class RadianceMap:
     def set_sampling(self, mode: int) -> None:
         """SAMPLE_CDF (default) or SAMPLE_MAX (the sector of largest Q, radiance_volume.cu:246-278)."""
         check(lib().rt_sarsa_set_sampling(self._h, mode))
+
+    def set_td_mode(self, mode: int) -> None:
+        """TD_FRAME (default: frame-synchronous, deterministic) or TD_INFRAME (the reference's
+        in-frame read-modify-write, radiance_volume.cu:282-301; racy, one GPU only)."""
+        check(lib().rt_sarsa_set_td_mode(self._h, mode))
+        self.td_mode = mode
 
     def frame_stats(self):
         """(sum over pixels of int(mean path length), zero-contribution paths) of the last frame."""

@@ -362,6 +362,51 @@ def test_gpu_max_direction_sampling_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx,
 
 
 @pytest.mark.gpu
+def test_gpu_in_frame_td_mode(rtmi_mod, oracle_mod, gpu_ctx):
+    """RT_SARSA_TD_INFRAME, the reference's racy in-frame update (radiance_volume.cu:282-301,
+    :93-112).  Exact where the rule leaves nothing to the race: frame 0 samples from the
+    initial CDFs in both modes, so its image and casts equal the deterministic mode's and the
+    restatement's, and so do the visit counts (integer atomics); unvisited sectors keep
+    their Q.  Statistical after that (parity unpinned: the reference's interleaving is not
+    reproducible): Q stays finite and >= RADIANCE_THRESHOLD, the learned Q-tables of the
+    two modes agree closely where visited, and later frames render the same radiance
+    (image means within 5 %; both are unbiased estimators of the same image)."""
+    S = rtmi_mod.sarsa
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, "door_room")
+    rf = S.RadianceMap(gpu_ctx, sc, 1984)
+    try:
+        rf.set_td_mode(S.TD_INFRAME)
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=16, spp_split=4)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+        q0 = rf.read()[0]
+        img_d, casts_d = rm.render(cam, p, 1)
+        img_f, casts_f = rf.render(cam, p, 1)
+        img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS["door_room"]), oracle_mod.params_from(p), 1)
+        assert casts_f == casts_d == casts_o
+        assert np.array_equal(img_f, img_d) and np.array_equal(img_d, img_o)
+        qd, _, vd, _ = rm.read()
+        qf, cf, vf, af = rf.read()
+        assert np.array_equal(vf, vd) and vd.sum() > 0
+        assert np.array_equal(qf[vf == 0], q0[vf == 0])
+        assert np.isfinite(qf).all() and np.isfinite(af).all() and np.isfinite(cf).all()
+        assert (qf >= np.float32(0.8 / 144) * np.float32(0.999)).all()
+        vis = vf > 0
+        corr = np.corrcoef(qd[vis], qf[vis])[0, 1]
+        assert corr > 0.9, corr
+        means_d, means_f = [], []
+        for _ in range(3):
+            means_d.append(float(rm.render(cam, p, 1)[0].mean()))
+            means_f.append(float(rf.render(cam, p, 1)[0].mean()))
+        assert abs(np.mean(means_f) / np.mean(means_d) - 1.0) < 0.05, (means_d, means_f)
+        with pytest.raises(rtmi_mod.RtError):
+            rf.set_td_mode(7)
+    finally:
+        rf.close()
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
 def test_gpu_max_direction_sector0_pdf_is_zero(rtmi_mod, oracle_mod, gpu_ctx):
     """Frame 0 in max mode: every Q equal, so every volume's first largest sector is 0, whose
     pdf the reference computes as cdf[0] - cdf[0] = 0 (radiance_volume.cu:274): paths that
