@@ -59,7 +59,9 @@ WORKLOADS = {
     "cornell": ("cornell", rtmi.RT_PRESET_CPU, "uniform", 512, 512, 256, 64, 2),
     "door_room_sarsa": ("door_room", rtmi.RT_PRESET_GPU, "sarsa", 512, 512, 256, 8, 3),
     "archway_dqn": ("archway", rtmi.RT_PRESET_GPU, "dqn", 1024, 1024, 512, 1, 4),
-    "complex_light": ("complex_light_room", rtmi.RT_PRESET_GPU, "uniform", 2048, 2048, 1024, 8, 5),
+    # (config 5: spp_split 32 -- 2-sample chunks end each rank's launch of the P = 8 split
+    # sooner: 121.6 vs 131.3 ms per rank set at 64 spp, profiles/r3ag/; one GPU unchanged)
+    "complex_light": ("complex_light_room", rtmi.RT_PRESET_GPU, "uniform", 2048, 2048, 1024, 32, 5),
 }
 # the roofline's dominant kernel per workload: (rt_ktime family timed live, its name in the
 # profiles, bound, object file holding it -- the profile must come from the same object)
