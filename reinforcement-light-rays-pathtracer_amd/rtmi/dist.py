@@ -106,10 +106,10 @@ def sarsa_frame(radiance_map, cam, params, tiles, n_real: int, tile_size: int, o
     """One multi-GPU SARSA frame: render this rank's n_real real tiles (the padding slots
     of `tiles` are left untouched so no pixel is learned from twice; TD sums stay in the
     map), all-reduce the TD sums over ranks, apply the shared update on every rank."""
-    stream = torch.cuda.current_stream(out.device).cuda_stream
     world = dist.get_world_size() if dist.is_initialized() else 1
     if world > 1 and getattr(radiance_map, "td_mode", 0) != 0:
         raise ValueError("the in-frame TD mode updates one GPU's map in place: no TD sums to share")
+    stream = torch.cuda.current_stream(out.device).cuda_stream
     radiance_map.render_tiles_device(cam, params, tiles[:n_real], tile_size, out.data_ptr(), casts.data_ptr(),
                                      apply=(world == 1), stream=stream)
     if world > 1:

@@ -140,3 +140,36 @@ def test_gloo_world2_frame_pipeline_double_buffer():
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
     assert q.get(timeout=5) is True and q.get(timeout=5) is True
+
+
+def _inframe_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import sys
+    import types
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "reinforcement-light-rays-pathtracer_amd"))
+    import rtmi
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    stub = types.SimpleNamespace(td_mode=rtmi.sarsa.TD_INFRAME)  # refused before any render call
+    try:
+        rtmi.dist.sarsa_frame(stub, None, None, [], 0, 32, torch.zeros(1), torch.zeros(1))
+        q.put(False)
+    except ValueError:
+        q.put(True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sarsa_frame_refuses_in_frame_td():
+    """the in-frame TD mode (RT_SARSA_TD_INFRAME) leaves no TD sums to all-reduce, so a
+    multi-rank SARSA frame refuses it on every rank instead of letting the maps diverge"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inframe_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs)
+    assert [q.get(timeout=5), q.get(timeout=5)] == [True, True]
