@@ -370,11 +370,15 @@ int rt_sarsa_set_sampling(rt_sarsa* sarsa, int mode);
  * RT_SARSA_TD_INFRAME the reference's own rule: each event updates the sector's Q, visits
  *   and the volume's irradiance in place while the frame renders (later targets of the same
  *   frame see it; concurrent updates race as in the reference).  The CDFs still change only
- *   at the frame end (update_radiance_volume_distributions).  Not reproducible run to run;
- *   one GPU only (the cross-GPU TD sums stay empty). */
+ *   at the frame end (update_radiance_volume_distributions).  SAMPLE_MAX then scans the
+ *   live Q at every sample, as the reference's scan of its radiance grid does.  Not
+ *   reproducible run to run (a launch with one active lane is: the events then run in the
+ *   restatement's order); one GPU only: rt_sarsa_td_device and a tile render with apply = 0
+ *   return RT_E_UNSUPPORTED in this mode. */
 #define RT_SARSA_TD_FRAME 0
 #define RT_SARSA_TD_INFRAME 1
 int rt_sarsa_set_td_mode(rt_sarsa* sarsa, int mode);
+int rt_sarsa_get_td_mode(const rt_sarsa* sarsa, int* mode);
 /* Training statistics of the last frame rendered (GPU/main.cu:321-339, one line of
  * Radiance_Map_Data/sarsa_training_stats.txt per frame): path_floor_sum = the sum over the
  * frame's pixels of int(path lengths / spp) (path_trace_reinforcement,
@@ -433,10 +437,17 @@ int rt_render_sarsa_tiles_device(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* s
 int rt_sarsa_td_device(rt_sarsa* sarsa, void** d_sum, void** d_count, int64_t* n_entries);
 int rt_sarsa_apply(rt_sarsa* sarsa, void* stream);
 
-/* Device self-tests of numeric building blocks (no reference counterpart).
- * RT_SELFTEST_RCP: the kernels' correctly-rounded reciprocal vs IEEE 1.0f/x over
- * all 2^32 floats; result[0] = mismatches, result[1] = first mismatching bits. */
+/* Device self-tests of numeric building blocks (no reference counterpart): every
+ * bit-exact claim against oracle/ rests on them.  result[0] = mismatches, result[1] = the
+ * lowest mismatching input bits (0xffffffff: none).
+ * RT_SELFTEST_RCP: the kernels' correctly-rounded reciprocal (Cramer's 1/detA, normalize)
+ *   vs IEEE 1.0f / x over all 2^32 floats;
+ * RT_SELFTEST_DIV12: the grid-coordinate x / 12 (Chiu map) vs IEEE over its domain,
+ *   +0 and |x| in [2^-100, 2^100];
+ * RT_SELFTEST_DIVRHO: the estimator's x / RHO vs IEEE over all 2^32 floats. */
 #define RT_SELFTEST_RCP 1
+#define RT_SELFTEST_DIV12 2
+#define RT_SELFTEST_DIVRHO 3
 int rt_selftest(rt_ctx* ctx, int which, uint64_t* result /* 2 */);
 
 /* Host-side checks of the CPU-preset primary-ray cull (k_cull_ps; no GPU needed).

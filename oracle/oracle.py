@@ -345,6 +345,10 @@ class Sarsa:
         L.orc_render_sarsa.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
                                        _FP, ctypes.POINTER(ctypes.c_uint64)]
         L.orc_sarsa_set_sampling.argtypes = [VP, ctypes.c_int]
+        L.orc_sarsa_set_td_mode.argtypes = [VP, ctypes.c_int]
+        L.orc_render_sarsa_rect.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams)] + \
+            [ctypes.c_int] * 4 + [_FP, ctypes.POINTER(ctypes.c_uint64)]
+        L.orc_sarsa_sample_stats.argtypes = [VP] + [ctypes.POINTER(ctypes.c_uint64)] * 3
         L.orc_sarsa_stats.argtypes = [VP, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.orc_sarsa_load_q.argtypes = [VP, _FP]
         L.orc_sarsa_td_rect.argtypes = [VP, ctypes.POINTER(OrcCamera), ctypes.POINTER(OrcParams), ctypes.c_int,
@@ -398,11 +402,23 @@ class Sarsa:
         """0: CDF importance sampling, 1: sample_max_direction_from_radiance_distribution"""
         self._L.orc_sarsa_set_sampling(self._h, mode)
 
+    def set_td_mode(self, mode: int):
+        """0: frame-synchronous integer TD sums (the default), 1: the reference's in-frame rule
+        applied event by event in the render's fixed order (the frame then renders on one
+        thread: pixels row by row, each pixel's chunks and samples in order)"""
+        self._L.orc_sarsa_set_td_mode(self._h, mode)
+
     def stats(self):
         """(sum over pixels of int(path length mean), zero-contribution paths) of the last frame"""
         a, b = ctypes.c_uint64(0), ctypes.c_uint64(0)
         self._L.orc_sarsa_stats(self._h, ctypes.byref(a), ctypes.byref(b))
         return int(a.value), int(b.value)
+
+    def sample_stats(self):
+        """last frame: (CDF samples, failed ones -- the null ray --, samples of sector 0)"""
+        v = [ctypes.c_uint64(0) for _ in range(3)]
+        self._L.orc_sarsa_sample_stats(self._h, *[ctypes.byref(x) for x in v])
+        return tuple(int(x.value) for x in v)
 
     def load_q(self, q):
         q = np.ascontiguousarray(q, np.float32).reshape(self.n_volumes, 144)
@@ -418,6 +434,16 @@ class Sarsa:
                                   s.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                                   c.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)))
         return s, c
+
+    def render_rect(self, cam: OrcCamera, params: OrcParams, rect):
+        """(image (h, w, 3), casts) of the rectangle (x, y, w, h) of the current frame; the
+        frame is not applied (its TD sums are dropped)"""
+        x, y, w, h = rect
+        out = np.zeros((h, w, 3), np.float32)
+        casts = ctypes.c_uint64(0)
+        self._L.orc_render_sarsa_rect(self._h, ctypes.byref(cam), ctypes.byref(params), x, y, w, h, _f(out),
+                                      ctypes.byref(casts))
+        return out, int(casts.value)
 
     def render(self, cam: OrcCamera, params: OrcParams, frames: int = 1):
         out = np.zeros((params.height, params.width, 3), np.float32)

@@ -1167,7 +1167,10 @@ typedef struct {
     uint32_t frames;
     uint64_t seed;
     int sample_max;                 /* 1: sample_max_direction_from_radiance_distribution */
+    int inframe;                    /* 1: the reference's in-frame TD rule, one event at a time */
     uint64_t stat_paths, stat_zero; /* last frame: sum of per-pixel floor(path length mean), zero paths */
+    uint64_t stat_null, stat_sector0, stat_cdf; /* last frame: failed CDF samples (null rays), CDF samples
+                                                   that chose sector 0, all CDF samples */
     /* scene (copied) */
     int n_surf, n_light;
     float *tri, *albedo, *emission, *normal;
@@ -1473,7 +1476,42 @@ ORC_API void orc_sarsa_stats(const orc_sarsa *m, uint64_t *path_floor_sum, uint6
     *zero_paths = m->stat_zero;
 }
 
+/* instrumentation of the last frame: CDF samples, failed ones (the null ray), sector 0 taken */
+ORC_API void orc_sarsa_sample_stats(const orc_sarsa *m, uint64_t *cdf_samples, uint64_t *null_samples,
+                                    uint64_t *sector0) {
+    *cdf_samples = m->stat_cdf;
+    *null_samples = m->stat_null;
+    *sector0 = m->stat_sector0;
+}
+
+/* The reference's own rule, applied in place event by event (sequential restatement of
+ * RadianceVolume::temporal_difference_update, radiance_volume.cu:282-301, and
+ * expected_sarsa_irradiance, :93-112): alpha from the sector's visits, the running update
+ * clamped at RADIANCE_THRESHOLD, visits + 1, the volume's irradiance moved by the sector's
+ * change times its corner cosine and BRDF.  One event at a time in the render's fixed
+ * order (orc_render_sarsa runs serially in this mode): the reference's atomics and races
+ * reduced to one interleaving, so the rule has a deterministic expected image. */
+static void td_inframe(orc_sarsa *m, int rv, int sector, float target) {
+    const float thr = (1.f / (12.0f * 12.0f)) * 0.8f;
+    size_t k = (size_t)rv * 144 + sector;
+    uint32_t vs = m->visits[k];
+    float alpha = 1.f / (1.f + (float)vs);
+    float q_old = m->Q[k];
+    float upd = ((1.f - alpha) * q_old) + (alpha * target);
+    upd = upd > thr ? upd : thr;
+    m->visits[k] = vs + 1u;
+    float cc = m->ck[k], brdf = m->brdf[rv];
+    m->accum[rv] = (m->accum[rv] - ((q_old * cc) * brdf)) + ((upd * cc) * brdf);
+    m->Q[k] = upd;
+}
+
+ORC_API void orc_sarsa_set_td_mode(orc_sarsa *m, int mode) { m->inframe = mode == 1; }
+
 static void td_add(orc_sarsa *m, int rv, int sector, float target) {
+    if (m->inframe) {
+        td_inframe(m, rv, sector, target);
+        return;
+    }
     int64_t v = (int64_t)llrintf(target * 4294967296.0f);
     size_t k = (size_t)rv * 144 + sector;
     #pragma omp atomic
@@ -1536,9 +1574,21 @@ static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t 
         } else if (m->sample_max) {
             sarsa_sample_max(m, cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf);
         } else if (!sarsa_sample(m, cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &cur_sector, &sd, &pdf)) {
+            #pragma omp atomic
+            m->stat_null += 1u;
+            #pragma omp atomic
+            m->stat_cdf += 1u;
             if (i + 1 >= p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
             (*casts)++; /* the zero direction is traced and misses */
             return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
+        }
+        if (cur_rv >= 0 && !m->sample_max) {
+            #pragma omp atomic
+            m->stat_cdf += 1u;
+            if (cur_sector == 0) {
+                #pragma omp atomic
+                m->stat_sector0 += 1u;
+            }
         }
         const float *al = sc.albedo + (size_t)h.tri * 3;
         float cos_theta = dot3(nrm, sd);
@@ -1650,54 +1700,84 @@ ORC_API int orc_sarsa_td_rect(orc_sarsa *m, const orc_camera *cam, const orc_par
     return (int)(total > 0);
 }
 
-/* `frames` frames of the whole width x height image (GPU-engine preset); out_rgb = last frame */
-ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int frames, float *out_rgb,
-                             uint64_t *out_casts) {
+/* One frame's rectangle (x0, y0, w, h) of the width x height image (GPU-engine preset) into
+ * out_rgb (w x h x 3, may be NULL): pixels row by row, each pixel's chunks in order (OpenMP
+ * over rows; one thread in the in-frame TD mode).  The frame's TD is accumulated (or applied
+ * in place, in-frame mode) but not folded; *paths / *zero: the frame statistics. */
+static uint64_t sarsa_frame_rect(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int x0, int y0, int w,
+                                 int h, float *out_rgb, uint64_t *paths_out, uint64_t *zero_out) {
     float cy = (float)cos((double)cam->yaw_y), sy = (float)sin((double)cam->yaw_y);
     float cx = (float)cos((double)cam->yaw_x), sx = (float)sin((double)cam->yaw_x);
     orc_params pg = *p;
     pg.preset = 1;
-    uint64_t total = 0;
-    int W = p->width, H = p->height;
+    uint64_t total = 0, paths = 0, zero = 0;
+    int W = p->width;
     int S = p->spp_split <= 0 ? 1 : p->spp_split;
     int per = p->spp / S;
-    for (int f = 0; f < frames; f++) {
-        uint32_t base = m->frames * (uint32_t)p->spp;
-        uint64_t paths = 0, zero = 0;
-        #pragma omp parallel for schedule(dynamic, 1) reduction(+:total, paths, zero)
-        for (int py = 0; py < H; py++) {
-            for (int px = 0; px < W; px++) {
-                uint32_t pix = (uint32_t)py * (uint32_t)W + (uint32_t)px;
-                v3 acc = mk(0.0f, 0.0f, 0.0f);
-                uint64_t casts = 0;
-                for (int c = 0; c < S; c++) {
-                    v3 part = mk(0.0f, 0.0f, 0.0f);
-                    for (int s = c * per; s < (c + 1) * per; s++) {
-                        float r1, r2;
-                        draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
-                        v3 o, d;
-                        camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
-                        v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
-                        part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
-                        /* path_trace_reinforcement (reinforcement_path_tracing.cu:28-41): a
-                         * zero-contribution path; its path length is its ray casts */
-                        if ((L.x + L.y + L.z) / 3.f < 0.0001f) zero++;
-                    }
-                    if (c == 0) acc = part;
-                    else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }
+    uint32_t base = m->frames * (uint32_t)p->spp;
+    m->stat_null = m->stat_sector0 = m->stat_cdf = 0;
+    /* in-frame TD: one thread, pixels row by row, each pixel's chunks and samples in order */
+    #pragma omp parallel for schedule(dynamic, 1) reduction(+:total, paths, zero) if(!m->inframe)
+    for (int py = y0; py < y0 + h; py++) {
+        for (int px = x0; px < x0 + w; px++) {
+            uint32_t pix = (uint32_t)py * (uint32_t)W + (uint32_t)px;
+            v3 acc = mk(0.0f, 0.0f, 0.0f);
+            uint64_t casts = 0;
+            for (int c = 0; c < S; c++) {
+                v3 part = mk(0.0f, 0.0f, 0.0f);
+                for (int s = c * per; s < (c + 1) * per; s++) {
+                    float r1, r2;
+                    draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
+                    v3 o, d;
+                    camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
+                    v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
+                    part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
+                    /* path_trace_reinforcement (reinforcement_path_tracing.cu:28-41): a
+                     * zero-contribution path; its path length is its ray casts */
+                    if ((L.x + L.y + L.z) / 3.f < 0.0001f) zero++;
                 }
-                float fs = (float)p->spp;
-                float *dst = out_rgb + ((size_t)py * W + px) * 3;
-                dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
-                total += casts;
-                paths += casts / (uint64_t)p->spp; /* int(total_path_lengths / SAMPLES_PER_PIXEL) */
+                if (c == 0) acc = part;
+                else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }
             }
+            if (out_rgb) {
+                float fs = (float)p->spp;
+                float *dst = out_rgb + ((size_t)(py - y0) * w + (px - x0)) * 3;
+                dst[0] = acc.x / fs; dst[1] = acc.y / fs; dst[2] = acc.z / fs;
+            }
+            total += casts;
+            paths += casts / (uint64_t)p->spp; /* int(total_path_lengths / SAMPLES_PER_PIXEL) */
         }
+    }
+    *paths_out = paths;
+    *zero_out = zero;
+    return total;
+}
+
+/* `frames` frames of the whole width x height image (GPU-engine preset); out_rgb = last frame */
+ORC_API int orc_render_sarsa(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int frames, float *out_rgb,
+                             uint64_t *out_casts) {
+    uint64_t total = 0;
+    for (int f = 0; f < frames; f++) {
+        uint64_t paths = 0, zero = 0;
+        total += sarsa_frame_rect(m, cam, p, 0, 0, p->width, p->height, out_rgb, &paths, &zero);
         m->stat_paths = paths;
         m->stat_zero = zero;
         sarsa_apply(m);
         m->frames++;
     }
+    if (out_casts) *out_casts = total;
+    return 0;
+}
+
+/* A rectangle of the current frame, not applied (the map is left as it was, apart from the
+ * in-frame mode's in-place updates): the bounded CPU-baseline sample of bench.py. */
+ORC_API int orc_render_sarsa_rect(orc_sarsa *m, const orc_camera *cam, const orc_params *p, int x0, int y0, int w,
+                                  int h, float *out_rgb, uint64_t *out_casts) {
+    uint64_t paths = 0, zero = 0;
+    uint64_t total = sarsa_frame_rect(m, cam, p, x0, y0, w, h, out_rgb, &paths, &zero);
+    size_t n = (size_t)m->n_vol * 144;
+    memset(m->sum, 0, sizeof(int64_t) * n);
+    memset(m->cnt, 0, sizeof(uint32_t) * n);
     if (out_casts) *out_casts = total;
     return 0;
 }

@@ -1031,7 +1031,8 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
 
 int rt_selftest(rt_ctx* ctx, int which, uint64_t* result) {
     if (!ctx || !result) return fail(RT_E_INVALID, "NULL argument");
-    if (which != RT_SELFTEST_RCP) return fail(RT_E_INVALID, "unknown self-test %d", which);
+    if (which != RT_SELFTEST_RCP && which != RT_SELFTEST_DIV12 && which != RT_SELFTEST_DIVRHO)
+        return fail(RT_E_INVALID, "unknown self-test %d", which);
     int rc = set_device(ctx);
     if (rc != RT_OK) return rc;
     unsigned long long* d_m = nullptr;
@@ -1040,7 +1041,7 @@ int rt_selftest(rt_ctx* ctx, int which, uint64_t* result) {
     if (e == hipSuccess) e = hipMalloc(&d_f, sizeof(unsigned));
     if (e == hipSuccess) e = hipMemset(d_m, 0, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(d_f, 0xff, sizeof(unsigned));
-    if (e == hipSuccess) e = rt::launch_selftest_rcp(d_m, d_f, 0);
+    if (e == hipSuccess) e = rt::launch_selftest(which, d_m, d_f, 0);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     unsigned long long m = 0;
     unsigned f = 0;

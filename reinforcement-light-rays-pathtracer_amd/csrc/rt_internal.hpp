@@ -25,13 +25,18 @@ enum KtimeKernel {
     KT_COUNT = 7
 };
 struct KernelTimer {
-    int slot = -1;
+    int kernel = -1;  // -1: not timing
     hipStream_t stream = nullptr;
+    hipEvent_t ev_a = nullptr, ev_b = nullptr;  // owned by this scope until its end is recorded
     KernelTimer(int kernel, hipStream_t s);
     ~KernelTimer();
     KernelTimer(const KernelTimer&) = delete;
     KernelTimer& operator=(const KernelTimer&) = delete;
 };
+
+// CUs of the current device (persistent-grid launch sizes), cached per device ordinal;
+// safe to call from several host threads (rt_ktime.cpp)
+int device_cu_count();
 
 // Device layout of one triangle for the hit test: 3 x float4 = 48 B
 //   [0] = {v0.x, v0.y, v0.z, c0}   c0 = e1.y*e2.z - e2.y*e1.z (the determinant
@@ -382,7 +387,7 @@ hipError_t launch_intersect_mf(const DeviceScene& s, const float* orig, const fl
                                int hit_rule, float* out_t, int32_t* out_hit, int32_t* cand, hipStream_t stream);
 
 // exhaustive rcp_rn == 1.0f/x check over all 2^32 floats (4096 x 256 threads x 4096)
-hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream);
+hipError_t launch_selftest(int which, unsigned long long* mism, unsigned* first, hipStream_t stream);
 
 // "x y z nx ny nz" location files (to_select.txt); RT_OK or RT_E_IO (rt_sarsa_host.cpp)
 int read_locations(const char* path, std::vector<float>* loc, std::vector<float>* nrm);

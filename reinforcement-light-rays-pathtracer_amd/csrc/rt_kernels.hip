@@ -983,14 +983,33 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
 // Exhaustive check of rcp_rn against IEEE division: thread g covers the
 // 4096 bit patterns [g*4096, (g+1)*4096).  Counts mismatches (ignoring NaN
 // payloads) and keeps the smallest mismatching pattern.
-__global__ __launch_bounds__(256) void k_selftest_rcp(unsigned long long* mism, unsigned* first) {
+// WHICH = RT_SELFTEST_RCP: rcp_rn(x) vs IEEE 1.0f / x over all 2^32 floats;
+// RT_SELFTEST_DIV12: div12(x) vs x / 12.0f over its domain (+0, |x| in [2^-100, 2^100]);
+// RT_SELFTEST_DIVRHO: div_rho(x) vs x / RHO over all 2^32 floats (its fallback included).
+// NaNs compare equal to NaNs.
+constexpr int kSelfRcp = 1, kSelfDiv12 = 2, kSelfDivRho = 3;  // RT_SELFTEST_* (rtmi.h)
+
+template <int WHICH>
+__global__ __launch_bounds__(256) void k_selftest(unsigned long long* mism, unsigned* first) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     unsigned bad = 0;
     for (uint32_t k = 0; k < 4096u; ++k) {
         const uint32_t bits = (uint32_t)(g * 4096u + k);
         const float x = __uint_as_float(bits);
-        const float a = rcp_rn(x);
-        const float b = 1.0f / x;
+        float a, b;
+        if constexpr (WHICH == kSelfRcp) {
+            a = rcp_rn(x);
+            b = 1.0f / x;
+        } else if constexpr (WHICH == kSelfDiv12) {
+            const float ax = fabsf(x);
+            if (!(bits == 0u || (ax >= 0x1p-100f && ax <= 0x1p100f))) continue;
+            a = div12(x);
+            b = x / 12.0f;
+        } else {
+            constexpr float rho = 1.0f / (2.0f * 3.14159265358979323846f);
+            a = div_rho(x);
+            b = x / rho;
+        }
         const bool same = (__float_as_uint(a) == __float_as_uint(b)) || (a != a && b != b);
         if (!same) {
             ++bad;
@@ -1002,8 +1021,15 @@ __global__ __launch_bounds__(256) void k_selftest_rcp(unsigned long long* mism, 
 
 }  // namespace
 
-hipError_t launch_selftest_rcp(unsigned long long* mism, unsigned* first, hipStream_t stream) {
-    hipLaunchKernelGGL(k_selftest_rcp, dim3(4096), dim3(256), 0, stream, mism, first);
+hipError_t launch_selftest(int which, unsigned long long* mism, unsigned* first, hipStream_t stream) {
+    if (which == kSelfRcp)
+        hipLaunchKernelGGL(k_selftest<kSelfRcp>, dim3(4096), dim3(256), 0, stream, mism, first);
+    else if (which == kSelfDiv12)
+        hipLaunchKernelGGL(k_selftest<kSelfDiv12>, dim3(4096), dim3(256), 0, stream, mism, first);
+    else if (which == kSelfDivRho)
+        hipLaunchKernelGGL(k_selftest<kSelfDivRho>, dim3(4096), dim3(256), 0, stream, mism, first);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -1121,15 +1147,7 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
             if (RT_RENDER_PQ && cam_in && a.csum != nullptr && a.work != nullptr) {
                 (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
                 // a persistent grid: as many workgroups as the device holds at 4 waves per SIMD
-                static int n_cu = 0;
-                if (n_cu == 0) {
-                    int dev = 0;
-                    if (hipGetDevice(&dev) != hipSuccess ||
-                        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                        n_cu <= 0)
-                        n_cu = 256;
-                }
-                const unsigned wgs = (unsigned)min(a.n_blocks * a.split, RT_MF_RENDER_WAVES * n_cu);
+                const unsigned wgs = (unsigned)min(a.n_blocks * a.split, RT_MF_RENDER_WAVES * device_cu_count());
                 if (one)
                     hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1>), dim3(wgs), dim3(256), 0, stream, b);
                 else

@@ -53,31 +53,60 @@ void drain(bool keep) {
 
 namespace rt {
 
-KernelTimer::KernelTimer(int kernel, hipStream_t s) : stream(s) {
-    if (!g_on.load(std::memory_order_relaxed) || kernel < 0 || kernel >= KT_COUNT) return;
-    std::lock_guard<std::mutex> lk(g_mu);
+KernelTimer::KernelTimer(int k, hipStream_t s) : stream(s) {
+    if (!g_on.load(std::memory_order_relaxed) || k < 0 || k >= KT_COUNT) return;
     hipEvent_t a = nullptr, b = nullptr;
-    if (!g_pool.empty()) {
-        a = g_pool.back().first;
-        b = g_pool.back().second;
-        g_pool.pop_back();
-    } else if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_pool.empty()) {
+            a = g_pool.back().first;
+            b = g_pool.back().second;
+            g_pool.pop_back();
+        }
+    }
+    if (a == nullptr && (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)) {
+        std::lock_guard<std::mutex> lk(g_mu);
         ++g_errors;
         return;
     }
     if (hipEventRecord(a, s) != hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_mu);
         g_pool.emplace_back(a, b);
         ++g_errors;
         return;
     }
-    slot = (int)g_pending.size();
-    g_pending.push_back(Rec{kernel, a, b});
+    kernel = k;
+    ev_a = a;
+    ev_b = b;
 }
 
+// the pair joins the pending list only once both events are recorded, so a concurrent
+// rt_ktime_read / rt_ktime_enable never recycles the events of an open scope
 KernelTimer::~KernelTimer() {
-    if (slot < 0) return;
+    if (kernel < 0) return;
+    const bool ok = hipEventRecord(ev_b, stream) == hipSuccess;
     std::lock_guard<std::mutex> lk(g_mu);
-    if (slot < (int)g_pending.size() && hipEventRecord(g_pending[(size_t)slot].b, stream) != hipSuccess) ++g_errors;
+    if (ok) {
+        g_pending.push_back(Rec{kernel, ev_a, ev_b});
+    } else {
+        ++g_errors;
+        g_pool.emplace_back(ev_a, ev_b);
+    }
+}
+
+int device_cu_count() {
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> cache[kMaxDev];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+    if (dev < kMaxDev) {
+        const int c = cache[dev].load(std::memory_order_relaxed);
+        if (c > 0) return c;
+    }
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev < kMaxDev) cache[dev].store(n, std::memory_order_relaxed);
+    return n;
 }
 
 }  // namespace rt

@@ -383,13 +383,37 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     return true;
 }
 
+// a live value of the in-frame TD mode's shared state (Q, irradiance): read at device scope,
+// past this CU's L1, so a lane sees the other lanes' (and its own earlier) atomicExch writes
+__device__ __forceinline__ float live_load(const float* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // sample_max_direction_from_radiance_distribution (radiance_volume.cu:246-278): the first
-// sector of largest Q (qmax, kept by k_sarsa_apply), uniform within it; the pdf is the CDF
-// step of that sector, 0 for sector 0 (the reference's last_pdf is cdf[0] there, :274)
+// sector of largest Q, uniform within it; the pdf is the CDF step of that sector, 0 for
+// sector 0 (the reference's last_pdf is cdf[0] there, :274).  Frame-synchronous TD: Q is
+// fixed within the frame, so its argmax (qmax) is kept by k_sarsa_apply; in-frame TD
+// (TD = 1): the reference's scan of the live radiance grid at every sample (:251-257), the
+// CDF still the frame's (update_radiance_volume_distributions runs between frames).
+template <int TD>
 __device__ void sarsa_sample_max(const SarsaMap& m, int rv, float rx, float ry, int* sector, f3* dir,
                                  float* pdf) {
     const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
-    const int mi = m.qmax[rv];
+    int mi;
+    if constexpr (TD == 1) {
+        const float* q = m.Q + (size_t)rv * kSarsaSectors;
+        mi = 0;
+        float mq = live_load(q);
+        for (int k = 0; k < kSarsaSectors; ++k) {
+            const float v = live_load(q + k);
+            if (mq < v) {
+                mq = v;
+                mi = k;
+            }
+        }
+    } else {
+        mi = m.qmax[rv];
+    }
     const float mv = cdf[mi];
     const float last = cdf[mi > 0 ? mi - 1 : 0];
     const int sx = mi / kGridRes;
@@ -409,20 +433,21 @@ __device__ __forceinline__ void td_event_inframe(const SarsaMap& m, int rv, int 
     const size_t k = (size_t)rv * kSarsaSectors + sector;
     const uint32_t vs = atomicAdd(&m.visits[k], 1u);
     const float alpha = 1.f / (1.f + (float)vs);
-    const float q_old = m.Q[k];
+    const float q_old = live_load(&m.Q[k]);
     float upd = ((1.f - alpha) * q_old) + (alpha * target);
     upd = upd > kRadianceThreshold ? upd : kRadianceThreshold;
     const float cc = m.cos_corner[k];
     const float brdf = m.vol_brdf[rv];
-    const float acc = m.accum[rv];
+    const float acc = live_load(&m.accum[rv]);
     const float acc_new = (acc - ((q_old * cc) * brdf)) + ((upd * cc) * brdf);
     atomicExch(&m.Q[k], upd);
     atomicExch(&m.accum[rv], acc_new);
 }
 
+template <int TD>
 __device__ __forceinline__ void td_event(const SarsaMap& m, int rv, int sector, float target) {
     if (RT_SARSA_NO_TD) return;
-    if (m.td_inframe) {
+    if constexpr (TD == 1) {
         td_event_inframe(m, rv, sector, target);
         return;
     }
@@ -443,6 +468,7 @@ struct SarsaPath {
 // rv at a surface hit: the TD event of the previous step, then light / miss / the next
 // direction from the volume's distribution.  Returns true when the path ends, with its
 // value in *L (n_casts counts the reference's extra cast of a zero direction).
+template <int TD>
 __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap& m, const Hit& h, bool is_surf,
                                            f3 pos, f3 nrm, int rv, bool td, uint32_t pix, int s, SarsaPath& P,
                                            unsigned& n_casts, f3* L_out) {
@@ -454,9 +480,9 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
         } else if (!is_surf) {
             target = P.cur_brdf * m.tri_lum[h.tri];
         } else {
-            target = (m.accum[rv] * kIrrScale) * P.cur_brdf;
+            target = ((TD == 1 ? live_load(&m.accum[rv]) : m.accum[rv]) * kIrrScale) * P.cur_brdf;
         }
-        td_event(m, P.cur_rv, P.cur_sector, target);
+        td_event<TD>(m, P.cur_rv, P.cur_sector, target);
         P.cur_rv = rv;
         P.cur_sector = -1;
     } else if (P.depth == 0 && is_surf) {
@@ -488,7 +514,7 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
                        (sx * B4.z + c * nrm.z) + sz * T4.z);
             pdf = kRho;
         } else if (m.sample_max) {
-            sarsa_sample_max(m, P.cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
+            sarsa_sample_max<TD>(m, P.cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
         } else {
             ok = sarsa_sample(m, P.cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
         }
@@ -527,7 +553,7 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
 #ifndef RT_MF_SARSA_WAVES
 #define RT_MF_SARSA_WAVES 4
 #endif
-template <int RULE, int MF = 0>
+template <int RULE, int MF, int TD>
 __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_render(const RenderLaunch a,
                                                                                      const SarsaMap m) {
     const int lg = a.split_log2;
@@ -598,7 +624,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         if (!active) continue;
         SarsaPath P{o, d, tp, depth, cur_rv, cur_sector, cur_brdf};
         f3 L;
-        const bool terminal = sarsa_step(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
+        const bool terminal = sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
         o = P.o;
         d = P.d;
         tp = P.tp;
@@ -666,7 +692,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
 // k_sarsa_fold adds each pixel's chunks in chunk order and takes its path-length statistic.
 // The volume search still runs with every lane of the wave (the walks of the grid's
 // undecided queries, sarsa_resolve_walks).  csum: float4 per chunk {r, g, b, casts (bits)}.
-template <int RULE, int MF = 0>
+template <int RULE, int MF, int TD>
 __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_render_pq(const RenderLaunch a,
                                                                                         const SarsaMap m) {
     __shared__ int kd_stack[kKdStack * 256];
@@ -778,7 +804,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
             rv = sarsa_nearest(m, pos, nrm, st);
         if (!active) continue;
         f3 L;
-        if (sarsa_step(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L)) {
+        if (sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L)) {
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
@@ -940,59 +966,71 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 #define RT_SARSA_PQ 1  // 0: the per-pixel k_sarsa_render (A/B builds)
 #endif
 
-hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
-    if (a.n_blocks <= 0) return hipSuccess;
-    KernelTimer kt(KT_SARSA_RENDER, stream);
+namespace {
+
+// the render launch of one TD rule (TD: k_sarsa_render's template argument, so the default
+// frame-synchronous kernel carries no in-frame branch)
+template <int TD>
+hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
     const float cb = a.scene.mf_bound;
     const bool mf = RT_MF_SARSA && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
                     fabsf(a.cam_z) <= cb;
-    if (RT_SARSA_PQ && a.csum != nullptr && a.work != nullptr) {
+    const bool one = a.scene.n_tri <= 64;
+    if constexpr (RT_SARSA_PQ) {
+        if (a.csum == nullptr || a.work == nullptr) return hipErrorInvalidValue;
         (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
-        static int n_cu = 0;
-        if (n_cu == 0) {
-            int dev = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-                n_cu = 256;
+        const dim3 grid((unsigned)min(a.n_blocks * a.split, 5 * device_cu_count()));  // 5 workgroups per CU fit
+        if constexpr (RT_MF_SARSA) {
+            if (mf) {
+                if (a.hit_rule == 0 && one)
+                    hipLaunchKernelGGL((k_sarsa_render_pq<0, 1, TD>), grid, dim3(256), 0, stream, a, m);
+                else if (a.hit_rule == 0)
+                    hipLaunchKernelGGL((k_sarsa_render_pq<0, 4, TD>), grid, dim3(256), 0, stream, a, m);
+                else if (one)
+                    hipLaunchKernelGGL((k_sarsa_render_pq<1, 1, TD>), grid, dim3(256), 0, stream, a, m);
+                else
+                    hipLaunchKernelGGL((k_sarsa_render_pq<1, 4, TD>), grid, dim3(256), 0, stream, a, m);
+            }
         }
-        const dim3 grid((unsigned)min(a.n_blocks * a.split, 5 * n_cu));  // 5 workgroups per CU fit (89 VGPRs, 32 KB)
-        const bool one = a.scene.n_tri <= 64;
-        if (mf) {
-            if (a.hit_rule == 0 && one)
-                hipLaunchKernelGGL((k_sarsa_render_pq<0, 1>), grid, dim3(256), 0, stream, a, m);
-            else if (a.hit_rule == 0)
-                hipLaunchKernelGGL((k_sarsa_render_pq<0, 4>), grid, dim3(256), 0, stream, a, m);
-            else if (one)
-                hipLaunchKernelGGL((k_sarsa_render_pq<1, 1>), grid, dim3(256), 0, stream, a, m);
+        if (!mf) {
+            if (a.hit_rule == 0)
+                hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD>), grid, dim3(256), 0, stream, a, m);
             else
-                hipLaunchKernelGGL((k_sarsa_render_pq<1, 4>), grid, dim3(256), 0, stream, a, m);
-        } else if (a.hit_rule == 0) {
-            hipLaunchKernelGGL((k_sarsa_render_pq<0>), grid, dim3(256), 0, stream, a, m);
-        } else {
-            hipLaunchKernelGGL((k_sarsa_render_pq<1>), grid, dim3(256), 0, stream, a, m);
+                hipLaunchKernelGGL((k_sarsa_render_pq<1, 0, TD>), grid, dim3(256), 0, stream, a, m);
         }
         hipLaunchKernelGGL(k_sarsa_fold, dim3((unsigned)a.n_blocks), dim3(256), 0, stream, a, m);
         return hipGetLastError();
-    }
-    if (mf) {
+    } else {
         const dim3 grid((unsigned)(a.n_blocks * a.split));
-        const bool one = a.scene.n_tri <= 64;
-        if (a.hit_rule == 0 && one)
-            hipLaunchKernelGGL((k_sarsa_render<0, 1>), grid, dim3(256), 0, stream, a, m);
-        else if (a.hit_rule == 0)
-            hipLaunchKernelGGL((k_sarsa_render<0, 4>), grid, dim3(256), 0, stream, a, m);
-        else if (one)
-            hipLaunchKernelGGL((k_sarsa_render<1, 1>), grid, dim3(256), 0, stream, a, m);
-        else
-            hipLaunchKernelGGL((k_sarsa_render<1, 4>), grid, dim3(256), 0, stream, a, m);
+        if constexpr (RT_MF_SARSA) {
+            if (mf) {
+                if (a.hit_rule == 0 && one)
+                    hipLaunchKernelGGL((k_sarsa_render<0, 1, TD>), grid, dim3(256), 0, stream, a, m);
+                else if (a.hit_rule == 0)
+                    hipLaunchKernelGGL((k_sarsa_render<0, 4, TD>), grid, dim3(256), 0, stream, a, m);
+                else if (one)
+                    hipLaunchKernelGGL((k_sarsa_render<1, 1, TD>), grid, dim3(256), 0, stream, a, m);
+                else
+                    hipLaunchKernelGGL((k_sarsa_render<1, 4, TD>), grid, dim3(256), 0, stream, a, m);
+            }
+        }
+        if (!mf) {
+            if (a.hit_rule == 0)
+                hipLaunchKernelGGL((k_sarsa_render<0, 0, TD>), grid, dim3(256), 0, stream, a, m);
+            else
+                hipLaunchKernelGGL((k_sarsa_render<1, 0, TD>), grid, dim3(256), 0, stream, a, m);
+        }
         return hipGetLastError();
     }
-    if (a.hit_rule == 0)
-        hipLaunchKernelGGL(k_sarsa_render<0>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
-    else
-        hipLaunchKernelGGL(k_sarsa_render<1>, dim3((unsigned)(a.n_blocks * a.split)), dim3(256), 0, stream, a, m);
-    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_sarsa_render(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
+    if (a.n_blocks <= 0) return hipSuccess;
+    KernelTimer kt(KT_SARSA_RENDER, stream);
+    return m.td_inframe ? launch_sarsa_render_t<1>(a, m, stream) : launch_sarsa_render_t<0>(a, m, stream);
 }
 
 hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream) {

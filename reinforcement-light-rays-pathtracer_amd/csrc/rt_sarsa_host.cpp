@@ -826,6 +826,12 @@ int rt_sarsa_set_td_mode(rt_sarsa* sa, int mode) {
     return RT_OK;
 }
 
+int rt_sarsa_get_td_mode(const rt_sarsa* sa, int* mode) {
+    if (!sa || !mode) return err(RT_E_INVALID, "NULL argument");
+    *mode = sa->m.td_inframe ? RT_SARSA_TD_INFRAME : RT_SARSA_TD_FRAME;
+    return RT_OK;
+}
+
 int rt_sarsa_frame_stats(const rt_sarsa* sa, uint64_t* path_floor_sum, uint64_t* zero_paths) {
     if (!sa) return err(RT_E_INVALID, "NULL argument");
     unsigned long long v[2] = {0, 0};
@@ -914,6 +920,8 @@ int rt_render_sarsa_tiles_device(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* s
     if (rc != RT_OK) return rc;
     if (n_tiles < 0 || (n_tiles > 0 && (!tiles || !d_out))) return err(RT_E_INVALID, "bad tiles/out");
     if (sa->device != rt::ctx_device(ctx)) return err(RT_E_INVALID, "radiance map belongs to another device");
+    if (!apply && sa->m.td_inframe)
+        return err(RT_E_UNSUPPORTED, "in-frame TD mode: the frame's TD is applied in place, nothing to exchange");
     RT_HIPE(hipSetDevice(sa->device));
     const rt::BlockDesc* d_blocks = nullptr;
     int n_blocks = 0;
@@ -927,6 +935,8 @@ int rt_render_sarsa_tiles_device(rt_ctx* ctx, const rt_scene* scene, rt_sarsa* s
 
 int rt_sarsa_td_device(rt_sarsa* sa, void** d_sum, void** d_count, int64_t* n_entries) {
     if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (sa->m.td_inframe)
+        return err(RT_E_UNSUPPORTED, "in-frame TD mode: no frame TD sums (the map is updated in place)");
     if (d_sum) *d_sum = sa->m.acc_sum;
     if (d_count) *d_count = sa->m.acc_cnt;
     if (n_entries) *n_entries = (int64_t)sa->n_vol * rt::kSarsaSectors;

@@ -55,7 +55,7 @@ EXPORTS = (
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
     "rt_neuralq_create", "rt_neuralq_destroy", "rt_neuralq_epsilon", "rt_neuralq_render_frame",
-    "rt_sarsa_save_selected", "rt_sarsa_load_q", "rt_sarsa_set_sampling", "rt_sarsa_set_td_mode", "rt_sarsa_frame_stats",
+    "rt_sarsa_save_selected", "rt_sarsa_load_q", "rt_sarsa_set_sampling", "rt_sarsa_set_td_mode", "rt_sarsa_get_td_mode", "rt_sarsa_frame_stats",
     "rt_dqn_save_selected",
     "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
     "rt_dqn_td_targets_device",
@@ -153,6 +153,7 @@ def _declare(lib):
         "rt_sarsa_set_search": (i, [_P, i]),
         "rt_sarsa_set_sampling": (i, [_P, i]),
         "rt_sarsa_set_td_mode": (i, [_P, i]),
+        "rt_sarsa_get_td_mode": (i, [_P, _IP]),
         "rt_neuralq_create": (i, [_P, _P, _P, i, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                   ctypes.POINTER(_P)]),
         "rt_neuralq_destroy": (i, [_P]),

@@ -45,7 +45,6 @@ class RadianceMap:
         nv, nk, fr = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_uint32(0)
         check(lib().rt_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk), ctypes.byref(fr)))
         self.n_volumes, self.n_nodes = nv.value, nk.value
-        self.td_mode = TD_FRAME
 
     @property
     def handle(self):
@@ -86,7 +85,13 @@ class RadianceMap:
         """TD_FRAME (default: frame-synchronous, deterministic) or TD_INFRAME (the reference's
         in-frame read-modify-write, radiance_volume.cu:282-301; racy, one GPU only)."""
         check(lib().rt_sarsa_set_td_mode(self._h, mode))
-        self.td_mode = mode
+
+    @property
+    def td_mode(self) -> int:
+        """the map's TD rule, read from the library (rt_sarsa_get_td_mode)"""
+        m = ctypes.c_int32(0)
+        check(lib().rt_sarsa_get_td_mode(self._h, ctypes.byref(m)))
+        return int(m.value)
 
     def frame_stats(self):
         """(sum over pixels of int(mean path length), zero-contribution paths) of the last frame."""

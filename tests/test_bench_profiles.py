@@ -38,6 +38,21 @@ def test_family_patterns_separate_the_kernels(bench):
     assert pick("k_dqn_bounce<") == ["k_dqn_bounce<4, false>"]
 
 
+def test_profile_table_matches_bench_frames(bench):
+    """tools/bench_pmc_summary.py keys profiles by the frame it ran: its frame defaults are
+    bench.py's, and every profiled command parses to the frame bench.py would match"""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_pmc_summary as bps
+    for wl, (_, _, _, W, H, spp, split, _) in bench.WORKLOADS.items():
+        assert bps.BENCH_FRAMES[wl] == (W, H, spp, split)
+    for name, (_, _, _, args, scale) in bps.WORKLOADS.items():
+        wl, *frame = bps.frame_of_args(args)
+        prof = {"workload_name": wl, "command": "python3 bench.py " + args}
+        assert bench.profile_frame(prof) == tuple(frame), name
+        assert scale in (1, 2)
+    assert bps.WORKLOADS["door_room_sarsa"][4] == 1  # gathers: FETCH_SIZE not doubled
+
+
 @pytest.mark.parametrize("workload", ["cornell", "complex_light", "door_room_sarsa", "archway_dqn"])
 def test_newest_profile_has_the_dominant_kernel(bench, workload):
     """the newest committed profile of each workload yields per-frame counters for the

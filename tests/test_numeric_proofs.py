@@ -1,0 +1,46 @@
+"""Exhaustive proofs of the numeric building blocks every bit-exact claim rests on.
+
+The kernels replace three IEEE divisions by cheaper sequences and claim the same bits:
+  * rcp_rn (rt_math.hpp): 1 / x as v_rcp_f32 + one FMA Newton step (Cramer's 1/detA,
+    normalize), equal to IEEE 1.0f / x for every float (out-of-range inputs divide);
+  * div12: the Chiu-map grid coordinate x / 12, equal to IEEE over +0 and |x| in
+    [2^-100, 2^100];
+  * div_rho: the estimator's x / RHO, equal to IEEE for every float.
+CPU: the host restatements of div12 / div_rho (tools/check_div12.c, check_divrho.c; IEEE fmaf
+on both sides) over all 2^32 inputs.  GPU: the device functions themselves, through
+rt_selftest, over all 2^32 inputs.
+"""
+import ctypes
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("name", ["check_div12", "check_divrho"])
+def test_host_exhaustive_division_checks(name, tmp_path):
+    exe = str(tmp_path / name)
+    subprocess.run(["gcc", "-O2", "-fopenmp", "-ffp-contract=off", os.path.join(ROOT, "tools", name + ".c"),
+                    "-o", exe, "-lm"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout
+    words = r.stdout.split()
+    tested = int(words[words.index("tested") + 1])
+    assert int(words[words.index("mismatches") + 1]) == 0
+    assert tested > 3_000_000_000  # (+0 and the 2^-100 .. 2^100 binades of both signs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which,name", [(1, "RT_SELFTEST_RCP"), (2, "RT_SELFTEST_DIV12"), (3, "RT_SELFTEST_DIVRHO")])
+def test_device_exhaustive_selftest(rtmi_mod, gpu_ctx, which, name):
+    res = (ctypes.c_uint64 * 2)()
+    rtmi_mod.check(rtmi_mod.lib().rt_selftest(gpu_ctx.handle, which, res))
+    assert int(res[0]) == 0, (name, int(res[0]), hex(int(res[1])))
+    assert int(res[1]) == 0xFFFFFFFF  # no mismatching input recorded
+
+
+def test_selftest_refuses_null_context(rtmi_mod):
+    res = (ctypes.c_uint64 * 2)()
+    assert rtmi_mod.lib().rt_selftest(None, 1, res) != 0

@@ -362,51 +362,6 @@ def test_gpu_max_direction_sampling_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx,
 
 
 @pytest.mark.gpu
-def test_gpu_in_frame_td_mode(rtmi_mod, oracle_mod, gpu_ctx):
-    """RT_SARSA_TD_INFRAME, the reference's racy in-frame update (radiance_volume.cu:282-301,
-    :93-112).  Exact where the rule leaves nothing to the race: frame 0 samples from the
-    initial CDFs in both modes, so its image and casts equal the deterministic mode's and the
-    restatement's, and so do the visit counts (integer atomics); unvisited sectors keep
-    their Q.  Statistical after that (parity unpinned: the reference's interleaving is not
-    reproducible): Q stays finite and >= RADIANCE_THRESHOLD, the learned Q-tables of the
-    two modes agree closely where visited, and later frames render the same radiance
-    (image means within 5 %; both are unbiased estimators of the same image)."""
-    S = rtmi_mod.sarsa
-    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, "door_room")
-    rf = S.RadianceMap(gpu_ctx, sc, 1984)
-    try:
-        rf.set_td_mode(S.TD_INFRAME)
-        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=16, spp_split=4)
-        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
-        q0 = rf.read()[0]
-        img_d, casts_d = rm.render(cam, p, 1)
-        img_f, casts_f = rf.render(cam, p, 1)
-        img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS["door_room"]), oracle_mod.params_from(p), 1)
-        assert casts_f == casts_d == casts_o
-        assert np.array_equal(img_f, img_d) and np.array_equal(img_d, img_o)
-        qd, _, vd, _ = rm.read()
-        qf, cf, vf, af = rf.read()
-        assert np.array_equal(vf, vd) and vd.sum() > 0
-        assert np.array_equal(qf[vf == 0], q0[vf == 0])
-        assert np.isfinite(qf).all() and np.isfinite(af).all() and np.isfinite(cf).all()
-        assert (qf >= np.float32(0.8 / 144) * np.float32(0.999)).all()
-        vis = vf > 0
-        corr = np.corrcoef(qd[vis], qf[vis])[0, 1]
-        assert corr > 0.9, corr
-        means_d, means_f = [], []
-        for _ in range(3):
-            means_d.append(float(rm.render(cam, p, 1)[0].mean()))
-            means_f.append(float(rf.render(cam, p, 1)[0].mean()))
-        assert abs(np.mean(means_f) / np.mean(means_d) - 1.0) < 0.05, (means_d, means_f)
-        with pytest.raises(rtmi_mod.RtError):
-            rf.set_td_mode(7)
-    finally:
-        rf.close()
-        rm.close()
-        sc.close()
-
-
-@pytest.mark.gpu
 def test_gpu_max_direction_sector0_pdf_is_zero(rtmi_mod, oracle_mod, gpu_ctx):
     """Frame 0 in max mode: every Q equal, so every volume's first largest sector is 0, whose
     pdf the reference computes as cdf[0] - cdf[0] = 0 (radiance_volume.cu:274): paths that
@@ -586,3 +541,140 @@ def test_gpu_q_table_and_selected_volume_dumps(rtmi_mod, gpu_ctx, tmp_path):
             assert np.all(np.abs(sdist.sum(axis=1) - 1) < 1e-4)
         finally:
             rm.close()
+
+
+# ------------------------------------------ in-frame TD mode (the reference's racy rule) -----
+# Last in the file: its statistical gate must never stop `pytest -x` before the exact tests.
+
+def _paired_z(a, b):
+    """z score of the mean per-pixel difference of two images (channel means): the pixels'
+    estimates are independent given the frame's CDFs, and under H0 both images are unbiased
+    estimates of the same pixel values, so mean(d) / (std(d) / sqrt(n)) ~ N(0, 1)."""
+    d = (a.mean(axis=2) - b.mean(axis=2)).ravel().astype(np.float64)
+    return float(d.mean() / (d.std(ddof=1) / np.sqrt(d.size)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", ("door_room", "cornell"))
+def test_gpu_in_frame_single_lane_equals_sequential_restatement(rtmi_mod, oracle_mod, gpu_ctx, scene):
+    """RT_SARSA_TD_INFRAME with one active lane (a 1 x 1 image, spp_split 1): the TD events
+    then run one at a time in sample order, which is exactly the restatement's sequential
+    in-frame rule (rt_oracle.c td_inframe: temporal_difference_update + expected_sarsa_irradiance,
+    radiance_volume.cu:282-301, :93-112, applied in place).  Image, casts, Q, CDF, visits and
+    irradiance bit-exact over three CDF frames, then two frames of max-direction sampling,
+    whose argmax the in-frame mode takes from the live Q at every sample (:251-257)."""
+    S = rtmi_mod.sarsa
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
+    try:
+        rm.set_td_mode(S.TD_INFRAME)
+        om.set_td_mode(1)
+        assert rm.td_mode == S.TD_INFRAME
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1, height=1, spp=512, spp_split=1)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+        ocam, op = oracle_mod.camera(rtmi_mod.CAMERAS[scene]), oracle_mod.params_from(p)
+        q0 = rm.read()[0]
+        for frame in range(5):
+            if frame == 3:
+                rm.set_sampling(S.SAMPLE_MAX)
+                om.set_sampling(1)
+            img_g, casts_g = rm.render(cam, p, 1)
+            img_o, casts_o = om.render(ocam, op, 1)
+            assert casts_g == casts_o, (frame, casts_g, casts_o)
+            assert _same_bits_nan_aware(img_g, img_o), frame
+            for a, b in zip(rm.read(), om.read()):
+                assert _same_bits_nan_aware(a, b), frame
+        q, _, vis, _ = rm.read()
+        assert vis.sum() > 100                      # the rule ran, in place
+        assert not np.array_equal(q, q0)
+    finally:
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_in_frame_td_mode(rtmi_mod, oracle_mod, gpu_ctx):
+    """RT_SARSA_TD_INFRAME on a 64^2 x 16 door_room frame, every lane racing as in the
+    reference.  Exact where the rule leaves nothing to the race: frame 0 samples from the
+    initial CDFs in both modes, so its image and casts equal the deterministic mode's and the
+    restatement's, and so do the visit counts (integer atomics); unvisited sectors keep their
+    Q; Q stays finite and >= RADIANCE_THRESHOLD.
+
+    Statistical after that: the race decides which interleaving of the events happens, so the
+    GPU's Q-table is one of many the rule allows.  Whatever the (full-support) CDFs, each
+    frame is an unbiased estimate of the same pixel values, so frames 1-3 are gated against
+    the sequential restatement of the rule (oracle in-frame mode) by the paired z score of
+    the mean per-pixel difference (_paired_z), combined over the frames: |z| < 4 (two-sided
+    p = 6e-5 under H0).  The fixed 5 % ratio this replaces failed on the driver's round-3 run
+    (GPU in-frame means 0.322 / 0.308 / 0.326; the restatement's in-frame rule gives
+    0.341 / 0.331 / 0.314, its frame-synchronous rule 0.341 / 0.335 / 0.334): at this size one
+    frame's mean has a standard error of about 0.01 (3 %), so a 5 % bound on the ratio of two
+    differently learned estimators is a 1.7-sigma gate.  Per-frame z of both rules over 4
+    seeds: profiles/r4b/sarsa_inframe_probe.json (tools/sarsa_inframe_probe.py)."""
+    S = rtmi_mod.sarsa
+    g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, "door_room")
+    rf = S.RadianceMap(gpu_ctx, sc, 1984)
+    of = oracle_mod.Sarsa(g, 1984)
+    try:
+        rf.set_td_mode(S.TD_INFRAME)
+        of.set_td_mode(1)
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=64, height=64, spp=16, spp_split=4)
+        cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+        ocam, op = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"]), oracle_mod.params_from(p)
+        q0 = rf.read()[0]
+        img_d, casts_d = rm.render(cam, p, 1)
+        img_f, casts_f = rf.render(cam, p, 1)
+        img_o, casts_o = om.render(ocam, op, 1)
+        img_s, casts_s = of.render(ocam, op, 1)
+        assert casts_f == casts_d == casts_o == casts_s
+        assert np.array_equal(img_f, img_d) and np.array_equal(img_d, img_o) and np.array_equal(img_o, img_s)
+        qd, _, vd, _ = rm.read()
+        qf, cf, vf, af = rf.read()
+        assert np.array_equal(vf, vd) and vd.sum() > 0
+        assert np.array_equal(vf, of.read()[2])
+        assert np.array_equal(qf[vf == 0], q0[vf == 0])
+        assert np.isfinite(qf).all() and np.isfinite(af).all() and np.isfinite(cf).all()
+        assert (qf >= np.float32(0.8 / 144) * np.float32(0.999)).all()
+        vis = vf > 0
+        corr = np.corrcoef(of.read()[0][vis], qf[vis])[0, 1]
+        assert corr > 0.9, corr
+        zs = []
+        for _ in range(3):
+            zs.append(_paired_z(rf.render(cam, p, 1)[0], of.render(ocam, op, 1)[0]))
+        z = sum(zs) / np.sqrt(len(zs))
+        assert abs(z) < 4.0, (zs, z)
+        assert np.isfinite(rf.read()[0]).all()
+        with pytest.raises(rtmi_mod.RtError):
+            rf.set_td_mode(7)
+    finally:
+        rf.close()
+        rm.close()
+        sc.close()
+
+
+@pytest.mark.gpu
+def test_gpu_in_frame_mode_refuses_td_exchange(rtmi_mod, gpu_ctx):
+    """The in-frame rule updates the map in place: the C ABI hands out no TD sums and refuses
+    a tile render that would leave them for a cross-GPU exchange (apply = 0)."""
+    import torch
+    S = rtmi_mod.sarsa
+    g = geometry(rtmi_mod, "door_room")
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        rf = S.RadianceMap(gpu_ctx, sc, 1984)
+        try:
+            rf.set_td_mode(S.TD_INFRAME)
+            with pytest.raises(rtmi_mod.RtError):
+                rf.td_device()
+            p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=32, height=32, spp=4)
+            out = torch.zeros(1, 32, 32, 3, device="cuda:0")
+            casts = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+            cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+            with pytest.raises(rtmi_mod.RtError):
+                rf.render_tiles_device(cam, p, np.zeros((1, 2), np.int32), 32, out.data_ptr(), casts.data_ptr(),
+                                       False, 0)
+            rf.render_tiles_device(cam, p, np.zeros((1, 2), np.int32), 32, out.data_ptr(), casts.data_ptr(), True, 0)
+            torch.cuda.synchronize()
+            assert rf.read()[2].sum() > 0
+            rf.set_td_mode(S.TD_FRAME)
+            assert rf.td_device()[2] == rf.n_volumes * 144
+        finally:
+            rf.close()

@@ -17,8 +17,15 @@ profiles/<tag>_<workload>_bench_pmc.json, holding
     ran at (GRBM_GUI_ACTIVE / 8 / duration).
 
 HBM bytes (MI355X_MICROARCH.md, HBM/rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB per
-dispatch, in separate passes; FETCH_SIZE counts half the bytes of wide streaming reads on
-gfx950, so fetch bytes = 2 x FETCH_SIZE x 1024; write bytes = WRITE_SIZE x 1024.
+dispatch, in separate passes, counted at the L2's fabric side (Infinity-Cache hits included).
+FETCH_SIZE counts half the bytes of wide (16-B-per-lane) coalesced streaming reads on gfx950:
+for kernels whose reads are such streams (the DQN forward's weight fragments, the frame
+stores' read-for-ownership) fetch bytes = 2 x FETCH_SIZE x 1024 (fetch_scale 2).  Other access
+widths are uncalibrated; the SARSA kernels read by gathers (grid lists, CDF rows, TD atomics)
+and keep fetch_scale 1 -- their FETCH_SIZE is L2-miss traffic that the 256 MB Infinity Cache
+largely serves (door_room's 170 MB map fits), not HBM bytes.  write bytes = WRITE_SIZE x 1024.
+Profiles are keyed by the bench frame they ran (workload, width, height, spp, spp_split):
+bench.py takes counters only from a profile of its own frame.
 """
 import csv
 import datetime
@@ -33,19 +40,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "reinforcement-light-rays-pathtracer_amd", "build")
 LIB = os.path.join(BUILD, "librtmi.so")
 
-# workload -> (kernel-name pattern kept, frame-marker pattern, object file of those kernels,
-#              bench arguments: must equal tools/gpu.sh bench_cmd)
+# profile name -> (kernel-name pattern kept, frame-marker pattern, object file of those kernels,
+#                 bench arguments: must equal tools/gpu.sh bench_cmd, FETCH_SIZE scale)
+# The BASELINE configs at their stated sizes: c1 (Cornell 256^2 x 4), cornell (= c2, the
+# driver's line), door_room_sarsa (c3), archway_dqn (c4, 1024^2 x 512), complex_light (c5,
+# 2048^2 x 1024 on one GPU); *_s16 / *_s64: the reduced-spp frames of earlier rounds.
 WORKLOADS = {
     "cornell": (r"::k_render_ps<|::k_cull", r"::k_render_ps<", "rt_kernels.o",
-                "--steps 4 --warmup 3 --cpu-seconds 0 --no-parity"),
+                "--steps 4 --warmup 3 --cpu-seconds 0 --no-parity", 2),
+    "cornell_c1": (r"::k_render_ps<|::k_cull", r"::k_render_ps<", "rt_kernels.o",
+                   "--width 256 --height 256 --spp 4 --spp-split 4 --steps 20 --warmup 3 --cpu-seconds 0 "
+                   "--no-parity", 2),
     # (the GPU preset's matrix-core renders run k_render_pq + k_fold_chunks; per-pixel k_render otherwise)
     "complex_light": (r"::k_render(_pq)?<|::k_fold_chunks", r"::k_render(_pq)?<", "rt_kernels.o",
-                      "--workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity"),
+                      "--workload complex_light --steps 1 --warmup 1 --cpu-seconds 0 --no-parity", 2),
+    "complex_light_s64": (r"::k_render(_pq)?<|::k_fold_chunks", r"::k_render(_pq)?<", "rt_kernels.o",
+                          "--workload complex_light --spp 64 --steps 2 --warmup 1 --cpu-seconds 0 --no-parity", 2),
     "door_room_sarsa": (r"::k_sarsa_", r"::k_sarsa_render(_pq)?<", "rt_sarsa.o",
-                        "--workload door_room_sarsa --steps 4 --warmup 1 --cpu-seconds 0"),
+                        "--workload door_room_sarsa --steps 4 --warmup 1 --cpu-seconds 0", 1),
     "archway_dqn": (r"::k_dqn_", r"::k_dqn_frame_begin", "rt_dqn.o",
-                    "--workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0"),
+                    "--workload archway_dqn --steps 1 --warmup 1 --cpu-seconds 0", 2),
+    "archway_dqn_s16": (r"::k_dqn_", r"::k_dqn_frame_begin", "rt_dqn.o",
+                        "--workload archway_dqn --spp 16 --steps 2 --warmup 1 --cpu-seconds 0", 2),
 }
+
+# bench.py's per-workload frame defaults (width, height, spp, spp_split)
+BENCH_FRAMES = {"cornell": (512, 512, 256, 64), "door_room_sarsa": (512, 512, 256, 8),
+                "archway_dqn": (1024, 1024, 512, 1), "complex_light": (2048, 2048, 1024, 32)}
+
+
+def frame_of_args(args: str):
+    """(workload, width, height, spp, spp_split) of a bench argument string"""
+    def opt(name, default):
+        m = re.search(rf"--{name} (\S+)", args)
+        return m.group(1) if m else default
+    wl = opt("workload", "cornell")
+    W, H, spp, split = BENCH_FRAMES[wl]
+    return (wl, int(opt("width", W)), int(opt("height", H)), int(opt("spp", spp)), int(opt("spp-split", split)))
 
 
 def sha(path):
@@ -77,10 +108,12 @@ def main():
         return
     d, tag = sys.argv[1], sys.argv[2]
     wl = sys.argv[3] if len(sys.argv) > 3 else "cornell"
-    keep, marker, obj, args = WORKLOADS[wl]
+    keep, marker, obj, args, fetch_scale = WORKLOADS[wl]
     w = re.search(r"--warmup (\d+)", args)
     s = re.search(r"--steps (\d+)", args)
-    out = {"tag": tag, "workload_name": wl, "command": "python3 bench.py " + args,
+    bench_wl, fw, fh, fspp, fsplit = frame_of_args(args)
+    out = {"tag": tag, "workload_name": bench_wl, "profile_name": wl, "command": "python3 bench.py " + args,
+           "frame": {"width": fw, "height": fh, "spp": fspp, "spp_split": fsplit}, "fetch_scale": fetch_scale,
            "warmup": int(w.group(1)), "steps": int(s.group(1)),
            "created": datetime.datetime.now(datetime.timezone.utc).isoformat(timespec="seconds"),
            "lib_sha256": sha(LIB), "obj": obj, "obj_sha256": sha(os.path.join(BUILD, obj)), "kernels": {}}
@@ -131,10 +164,10 @@ def main():
             k["calls"] = len(dur)
         c = k["per_dispatch"]
         if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
-            k["hbm_bytes_per_dispatch"] = 2.0 * c["FETCH_SIZE"] * 1024.0 + c["WRITE_SIZE"] * 1024.0
+            k["hbm_bytes_per_dispatch"] = fetch_scale * c["FETCH_SIZE"] * 1024.0 + c["WRITE_SIZE"] * 1024.0
         for fr in k["per_frame"]:
             if "FETCH_SIZE" in fr and "WRITE_SIZE" in fr:
-                fr["hbm_bytes"] = 2.0 * fr["FETCH_SIZE"] * 1024.0 + fr["WRITE_SIZE"] * 1024.0
+                fr["hbm_bytes"] = fetch_scale * fr["FETCH_SIZE"] * 1024.0 + fr["WRITE_SIZE"] * 1024.0
             if "GRBM_GUI_ACTIVE" in fr and fr.get("duration_ns"):
                 fr["clock_ghz"] = fr["GRBM_GUI_ACTIVE"] / 8.0 / fr["duration_ns"]
         if "GRBM_GUI_ACTIVE" in c and "avg_ns" in k:
