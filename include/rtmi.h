@@ -263,7 +263,10 @@ int rt_dqn_sample(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float* q, c
                   float* dir_out, int32_t* action);
 /* PretrainedPathtracer::render_frame (pre_trained_pathtracer.cu:188-376), GPU-engine preset:
  * rectangle render into host memory, and tile-list render into device memory (stream-ordered;
- * synchronises the stream every few bounces to stop once all paths have ended). */
+ * synchronises the stream every few bounces to stop once all paths have ended).  Between the
+ * forward and the sampler each ray's 144 Q values are kept in bf16 (round to nearest even of
+ * the forward's fp32 Q, within the forward's own bf16 tolerance): the per-bounce Q buffer's
+ * HBM round trip is half the bytes (the sampler itself is rt_dqn_sample's, on those values). */
 int rt_render_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_camera* cam,
                   const rt_params* params, int x0, int y0, int w, int h, float* out_rgb,
                   uint64_t* out_ray_casts);

@@ -1010,6 +1010,10 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
                     for (int bnc = 1; alive && bnc < p->max_bounces; bnc++) {
                         float locf[3] = {loc.x, loc.y, loc.z};
                         dqn_forward_one(&net, locf, bf16, q, scratch);
+                        /* the kernel arithmetic (bf16 = 1) keeps the renderer's Q in bf16
+                         * between the forward and the sampler (k_dqn_mlp<.., QB>) */
+                        if (bf16)
+                            for (int a = 0; a < 144; a++) q[a] = bf16_round(q[a]);
                         const float *nn = sc.normal + (size_t)tri_i * 3;
                         v3 dir;
                         int act = dqn_sample(q, mk(nn[0], nn[1], nn[2]), loc, p->seed, pix, (uint32_t)s,
@@ -1044,7 +1048,8 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
  * batch, so with the network's own Q this equals orc_render_dqn).  The tests pass the GPU
  * forward (k_dqn_mlp through rt_dqn_forward) as q_fn: everything downstream of the bf16
  * GEMM is then checked bit for bit against the device render
- * (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491). */
+ * (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491).  As the device
+ * renderer does, the batch's Q is rounded to bf16 (RNE) before the sampler. */
 typedef void (*orc_q_fn)(const float *loc, int n, float *q, void *user);
 
 ORC_API int orc_render_dqn_wave(const float *tri, const float *albedo, int n_surf, const float *emission,
@@ -1083,6 +1088,7 @@ ORC_API int orc_render_dqn_wave(const float *tri, const float *albedo, int n_sur
             bl[3 * (size_t)k + 2] = loc[live[k]].z;
         }
         q_fn(bl, n_live, bq, user);
+        for (size_t i = 0; i < (size_t)n_live * 144; i++) bq[i] = bf16_round(bq[i]);
         int m = 0;
         for (int k = 0; k < n_live; k++) {
             const int r = live[k], s = r / n_pix, pi = r % n_pix;

@@ -287,6 +287,9 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
 }
 
+typedef float mlp_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 mlp_bf16x2 __attribute__((ext_vector_type(2)));
+
 // The fused Q.cos sampler's per-ray inputs (k_dqn_mlp<MT, true>): the rays' pixel keys and
 // sample (ray id = slot * n_pix + pixel slot, as k_dqn_bounce), the Philox event and key.
 struct MlpSample {
@@ -309,7 +312,7 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
 // writes the chosen cell and its normalised Q*cos per ray (q[i] = action bits,
 // q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
 // direction.  Q never leaves the chip.
-template <int MT, bool FUSED = false>
+template <int MT, bool FUSED = false, bool QB = false>
 __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
@@ -453,6 +456,21 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
             const float* sp = stage + r * kStageStride + c;
             *reinterpret_cast<float4*>(dst + (size_t)r * kDqnActions + c) = make_float4(sp[0], sp[1], sp[2], sp[3]);
         }
+    } else if constexpr (QB) {
+        // the renderer's Q in bf16 (RNE), cells 2j and 2j + 1 of a ray in one dword (low,
+        // high): q2[j * ldq + ray], 16-B runs of four rays -- half the bytes of the fp32 tile
+        uint32_t* const q2 = reinterpret_cast<uint32_t*>(q);
+        for (int t = threadIdx.x; t < (kDqnActions / 2) * (kRows / 4); t += kMlpThreads) {
+            const int j = t / (kRows / 4), r = (t - j * (kRows / 4)) * 4;
+            const float* sp = stage + r * kStageStride + 2 * j;
+            uint32_t w[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const mlp_f32x2 v = {sp[k * kStageStride], sp[k * kStageStride + 1]};
+                w[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, mlp_bf16x2));
+            }
+            *reinterpret_cast<uint4*>(q2 + (size_t)j * ldq + row0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
     } else {
         for (int t = threadIdx.x; t < kDqnActions * (kRows / 4); t += kMlpThreads) {
             const int c = t / (kRows / 4), r = (t - c * (kRows / 4)) * 4;
@@ -508,10 +526,12 @@ __device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 
 // are divided and walked.  WB: q is overwritten with Q * cos, as the reference does in
 // place (rt_dqn_sample, the Neural-Q sampler); without it the walk recomputes its block's
 // Q * cos (the same operations, so the same bits) instead of a 576-B store and reload.
-template <bool WB>
+// QB: q holds the renderer's bf16 Q (k_dqn_mlp<.., QB>): cells 2j, 2j + 1 in dword j * qs
+template <bool WB, bool QB = false>
 __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t qs, f3 N, f3 T, f3 B, f3 pos,
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
                                                    uint32_t k0, uint32_t k1, f3* tp, bool update_tp) {
+    static_assert(!(WB && QB), "the in-place Q*cos store needs the fp32 buffer");
     uint32_t o[4];
     philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
     const float rv = u01(o[0]);
@@ -521,8 +541,18 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
     static_assert(kSampCells % kQGroup == 0, "groups tile the blocks");
     // Q*cos of the group of cells g .. g + kQGroup - 1 into qv (q holds Q, or Q*cos if done)
     auto qcos = [&](int g, float* qv, bool stored) {
+        if constexpr (QB) {
+            const uint32_t* q2 = reinterpret_cast<const uint32_t*>(q);
 #pragma unroll
-        for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
+            for (int u = 0; u < kQGroup; u += 2) {
+                const uint32_t w = q2[(size_t)((g + u) >> 1) * qs];
+                qv[u] = __uint_as_float(w << 16);
+                qv[u + 1] = __uint_as_float(w & 0xffff0000u);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kQGroup; ++u) qv[u] = q[(size_t)(g + u) * qs];
+        }
         if (stored) return;
 #pragma unroll
         for (int u4 = 0; u4 < kQGroup; u4 += 4) {
@@ -698,7 +728,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camer
 
 // one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
 // FUSED: the cell was chosen by k_dqn_mlp<MT, true> (q[i] = its index bits, q[ldq + i] = qd)
-template <int MF, bool FUSED = false>
+template <int MF, bool FUSED = false, bool QB = false>
 __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounce(const DqnLaunch a, int bounce) {
     __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
@@ -727,7 +757,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
             FUSED ? sample_finish(__float_as_int(a.rays.q[i]), a.rays.q[(size_t)a.rays.ldq + i], make3(N4.x, N4.y, N4.z),
                                   make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                                   1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true)
-                  : sample_from_q<false>(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
+                  : sample_from_q<false, QB>(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                                   make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                                   1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
         casts = 1;
@@ -995,16 +1025,16 @@ __global__ __launch_bounds__(256) void k_nq_image(const DqnLaunch a, const NqRay
 
 static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, const int32_t* list,
                                        const int32_t* count, int max_rows, float* q, int ldq, const MlpSample* smp,
-                                       hipStream_t stream);
+                                       bool qb, hipStream_t stream);
 
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
                           int max_rows, float* q, int ldq, hipStream_t stream) {
-    return launch_dqn_mlp_fused(net, loc, list, count, max_rows, q, ldq, nullptr, stream);
+    return launch_dqn_mlp_fused(net, loc, list, count, max_rows, q, ldq, nullptr, false, stream);
 }
 
 // fused (smp != nullptr): the sampler runs in the forward kernel (k_dqn_mlp<MT, true>)
 static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
-                                int max_rows, float* q, int ldq, const MlpSample* smp, hipStream_t stream) {
+                                int max_rows, float* q, int ldq, const MlpSample* smp, bool qb, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
     KernelTimer kt(KT_DQN_MLP, stream);
     // this file's weight-streaming kernel; the weight-stationary one (rt_dqn_ws.hip) when
@@ -1014,13 +1044,16 @@ static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, cons
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
         if (e != hipSuccess) return e;
-        return launch_dqn_mlp_ws(net, loc, list, count, max_rows, q, ldq, n_cu, stream);
+        return launch_dqn_mlp_ws(net, loc, list, count, max_rows, q, ldq, n_cu, qb, stream);
     }
     const int blocks = (max_rows + kTileM - 1) / kTileM;
     if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
     if (smp != nullptr)
         hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc,
                            list, count, max_rows, q, ldq, *smp);
+    else if (qb && ldq != 0)
+        hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, false, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net,
+                           loc, list, count, max_rows, q, ldq, MlpSample());
     else
         hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, false>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc,
                            list, count, max_rows, q, ldq, MlpSample());
@@ -1058,6 +1091,9 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#ifndef RT_DQN_QBF16
+#define RT_DQN_QBF16 1  // the renderer's Q between the forward and the sampler in bf16 (0: fp32; archway 512^2 x 16: 110.7 vs 121.0 ms, profiles/r4c)
+#endif
 #ifndef RT_DQN_FUSED
 #define RT_DQN_FUSED 0  // 1: the sampler inside k_dqn_mlp (measured slower: 143.9 vs 131.8 ms, archway 512^2 x 16)
 #endif
@@ -1074,11 +1110,21 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
     smp.ev = 1u + (uint32_t)bounce;
     smp.k0 = a.seed_lo;
     smp.k1 = a.seed_hi;
+    // the renderer's Q in bf16 (either forward kernel writes it)
+    const bool qb = RT_DQN_QBF16 && !fused && a.net.N[3] == kDqnActions;
     hipError_t e = launch_dqn_mlp_fused(a.net, a.rays.loc, a.rays.list[cur], a.rays.count + cur, a.rays.n,
-                                        a.rays.q, a.rays.ldq, fused ? &smp : nullptr, stream);
+                                        a.rays.q, a.rays.ldq, fused ? &smp : nullptr, qb, stream);
     if (e != hipSuccess) return e;
     KernelTimer kt(KT_DQN_BOUNCE, stream);
     const dim3 grid(ray_blocks(a));
+    if (qb) {
+        switch (dqn_mf(a)) {
+            case 1: hipLaunchKernelGGL((k_dqn_bounce<1, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
+            case 4: hipLaunchKernelGGL((k_dqn_bounce<4, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
+            default: hipLaunchKernelGGL((k_dqn_bounce<0, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
+        }
+        return hipGetLastError();
+    }
     switch (dqn_mf(a) * 2 + (fused ? 1 : 0)) {
         case 2: hipLaunchKernelGGL((k_dqn_bounce<1, false>), grid, dim3(256), 0, stream, a, bounce); break;
         case 3: hipLaunchKernelGGL((k_dqn_bounce<1, true>), grid, dim3(256), 0, stream, a, bounce); break;

@@ -182,7 +182,7 @@ __device__ __forceinline__ int row_id(const int32_t* __restrict__ list, int row,
 
 template <int NT1, int NT2, int NT3>
 __device__ void ws_wave(const DqnNet& net, const float* __restrict__ loc, const int32_t* __restrict__ list,
-                        int n_rows, float* __restrict__ q, int ldq, __bf16* bufA, __bf16* bufB, float* locs,
+                        int n_rows, float* __restrict__ q, int ldq, bool qb, __bf16* bufA, __bf16* bufB, float* locs,
                         const float4* l0s, const float* bias1, const float* bias2, const float* bias3, int wave,
                         int lane) {
     bf16x8 w1[NT1][kKs1], w2[NT2][kKs2], w3[NT3][kKs3];
@@ -235,6 +235,21 @@ __device__ void ws_wave(const DqnNet& net, const float* __restrict__ loc, const 
                 const float* sp = stage + r * kQStage + c;
                 *reinterpret_cast<float4*>(dst + (size_t)r * kDqnActions + c) = make_float4(sp[0], sp[1], sp[2], sp[3]);
             }
+        } else if (qb) {  // the renderer's bf16 Q (k_dqn_mlp<.., QB>'s layout): q2[j * ldq + ray]
+            typedef float f32x2 __attribute__((ext_vector_type(2)));
+            typedef __bf16 b16x2 __attribute__((ext_vector_type(2)));
+            uint32_t* const q2 = reinterpret_cast<uint32_t*>(q);
+            for (int i = threadIdx.x; i < (kDqnActions / 2) * (kRows / 4); i += kWsThreads) {
+                const int j = i / (kRows / 4), r = (i - j * (kRows / 4)) * 4;
+                const float* sp = stage + r * kQStage + 2 * j;
+                uint32_t w[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const f32x2 v = {sp[k * kQStage], sp[k * kQStage + 1]};
+                    w[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, b16x2));
+                }
+                *reinterpret_cast<uint4*>(q2 + (size_t)j * ldq + row0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+            }
         } else {
             for (int i = threadIdx.x; i < kDqnActions * (kRows / 4); i += kWsThreads) {
                 const int c = i / (kRows / 4), r = (i - c * (kRows / 4)) * 4;
@@ -251,7 +266,7 @@ __device__ void ws_wave(const DqnNet& net, const float* __restrict__ loc, const 
 __global__ __launch_bounds__(kWsThreads, 1) void k_dqn_mlp_ws(const DqnNet net, const float* __restrict__ loc,
                                                               const int32_t* __restrict__ list,
                                                               const int32_t* __restrict__ count, int max_rows,
-                                                              float* __restrict__ q, int ldq) {
+                                                              float* __restrict__ q, int ldq, int qb) {
     __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrA];
     __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrB];
     __shared__ float locs[kRows * 3];
@@ -270,16 +285,16 @@ __global__ __launch_bounds__(kWsThreads, 1) void k_dqn_mlp_ws(const DqnNet net, 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     switch (wave) {  // the per-wave tile counts are compile-time (register arrays)
         case 0:
-            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, qb != 0, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
             break;
         case 1:
-            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            ws_wave<5, 4, 2>(net, loc, list, n_rows, q, ldq, qb != 0, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
             break;
         case 2:
-            ws_wave<5, 3, 2>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            ws_wave<5, 3, 2>(net, loc, list, n_rows, q, ldq, qb != 0, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
             break;
         default:
-            ws_wave<5, 3, 3>(net, loc, list, n_rows, q, ldq, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
+            ws_wave<5, 3, 3>(net, loc, list, n_rows, q, ldq, qb != 0, bufA, bufB, locs, l0s, bias1, bias2, bias3, wave, lane);
             break;
     }
 }
@@ -292,13 +307,13 @@ bool dqn_mlp_ws_fits(const DqnNet& net) {
 }
 
 hipError_t launch_dqn_mlp_ws(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
-                             int max_rows, float* q, int ldq, int n_cu, hipStream_t stream) {
+                             int max_rows, float* q, int ldq, int n_cu, bool qb, hipStream_t stream) {
     if (max_rows <= 0) return hipSuccess;
     const int tiles = (max_rows + kRows - 1) / kRows;
     if (ldq != 0 && (ldq < tiles * kRows || ldq % 4 != 0)) return hipErrorInvalidValue;
     const int blocks = min(tiles, n_cu);
     hipLaunchKernelGGL(k_dqn_mlp_ws, dim3((unsigned)blocks), dim3(kWsThreads), 0, stream, net, loc, list, count,
-                       max_rows, q, ldq);
+                       max_rows, q, ldq, (int)(qb && ldq != 0));
     return hipGetLastError();
 }
 

@@ -296,7 +296,7 @@ hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* li
 // weight-stationary forward (rt_dqn_ws.hip): one workgroup per CU, the 200-300-200 shape
 bool dqn_mlp_ws_fits(const DqnNet& net);
 hipError_t launch_dqn_mlp_ws(const DqnNet& net, const float* loc, const int32_t* list, const int32_t* count,
-                             int max_rows, float* q, int ldq, int n_cu, hipStream_t stream);
+                             int max_rows, float* q, int ldq, int n_cu, bool qb, hipStream_t stream);
 hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream);
 hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream);  // samples s0 .. s0 + n/n_pix - 1
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream);
@@ -368,7 +368,10 @@ struct SarsaMap {
     int32_t* qmax = nullptr;               // [n] first sector of largest Q (k_sarsa_apply)
     unsigned long long* stats = nullptr;   // [2] launch: sum of per-pixel int(mean path length), zero paths
 };
-constexpr int kKdStack = 32;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
+#ifndef RT_KD_STACK
+#define RT_KD_STACK 32
+#endif
+constexpr int kKdStack = RT_KD_STACK;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
 
 hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);

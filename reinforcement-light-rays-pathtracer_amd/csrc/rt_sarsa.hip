@@ -692,8 +692,11 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
 // k_sarsa_fold adds each pixel's chunks in chunk order and takes its path-length statistic.
 // The volume search still runs with every lane of the wave (the walks of the grid's
 // undecided queries, sarsa_resolve_walks).  csum: float4 per chunk {r, g, b, casts (bits)}.
+#ifndef RT_SARSA_WAVES
+#define RT_SARSA_WAVES 5  // waves per SIMD of the persistent render (its grid: that many workgroups per CU)
+#endif
 template <int RULE, int MF, int TD>
-__global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_render_pq(const RenderLaunch a,
+__global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) void k_sarsa_render_pq(const RenderLaunch a,
                                                                                         const SarsaMap m) {
     __shared__ int kd_stack[kKdStack * 256];
     int* const st = kd_stack_of(kd_stack);
@@ -980,7 +983,9 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
     if constexpr (RT_SARSA_PQ) {
         if (a.csum == nullptr || a.work == nullptr) return hipErrorInvalidValue;
         (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
-        const dim3 grid((unsigned)min(a.n_blocks * a.split, 5 * device_cu_count()));  // 5 workgroups per CU fit
+        // as many workgroups as fit: RT_SARSA_WAVES per CU (registers and the k-d stack's LDS)
+        const int per_cu = mf ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES;
+        const dim3 grid((unsigned)min(a.n_blocks * a.split, per_cu * device_cu_count()));
         if constexpr (RT_MF_SARSA) {
             if (mf) {
                 if (a.hit_rule == 0 && one)

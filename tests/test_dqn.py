@@ -551,3 +551,20 @@ def test_gpu_weight_stationary_forward_equals_streaming(rtmi_mod, gpu_ctx, kind)
             qs = net.forward(loc)
             assert qa.shape == (n, 144) and np.isfinite(qa).all()
             assert np.array_equal(qa.view(np.uint32), qs.view(np.uint32)), n
+
+
+@pytest.mark.gpu
+def test_gpu_weight_stationary_render_equals_streaming(rtmi_mod, gpu_ctx):
+    """Both forward kernels write the renderer's bf16 Q (k_dqn_mlp<.., QB>, k_dqn_mlp_ws): the
+    archway render is the same bit for bit whichever computes it."""
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "archway.obj"), "archway")
+    W, b = rtmi_mod.dqn.synthetic_weights(g.nn_vertices.size)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1024, height=1024, spp=2)
+    rect = (448, 448, 64, 64)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["archway"])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, W, b) as net:
+        img_s, casts_s = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+        net.set_mlp(net.MLP_STATIONARY)
+        img_w, casts_w = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
+        net.set_mlp(net.MLP_STREAM)
+    assert casts_s == casts_w and np.array_equal(img_s.view(np.uint32), img_w.view(np.uint32))
