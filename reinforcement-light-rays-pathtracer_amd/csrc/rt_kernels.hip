@@ -562,6 +562,9 @@ __global__ __launch_bounds__(256) void k_fold_chunks(const RenderLaunch a) {
 //   continuing: the hit point x, y, z, triangle;  ended: L.x, L.y, L.z, -1.
 constexpr int kPsFields = 4;
 
+#ifndef RT_PS_PRIM_BATCH
+#define RT_PS_PRIM_BATCH 4  // samples per candidate pass of phase P (1: one sample at a time)
+#endif
 #ifndef RT_PS_STEAL
 #define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
 #endif
@@ -632,25 +635,8 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #endif
     const float nts = a.t_scale;
     cfloat4* __restrict__ isect = as_const(a.scene.isect);
-    for (int k = 0; k < pc; ++k) {
-        const int s = chunk * pc + k;
-        float r1, r2;
-        draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
-        f3 d;
-        camera_ray<0>(a, px, py, r1, r2, &d);
-        const float nDx = -(d.x * nts), nDy = -(d.y * nts), nDz = -(d.z * nts);
-        Hit h;
-        h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
-        h.tri = -1;
-#pragma unroll
-        for (int g = 0; g < kRenderCullWords; ++g) {
-            uint64_t m = cm[g];
-            while (m != 0ull) {
-                const int b = __builtin_ctzll(m);
-                m &= m - 1ull;
-                exact_one_c<RULE>(isect, g * 64 + b, cam, nDx, nDy, nDz, h);
-            }
-        }
+    // parks sample k's primary result (the shading's pos = cam + t D, or the final value)
+    auto park = [&](int k, const f3& d, const Hit& h) {
         n_casts += valid ? 1u : 0u;
         // a continuing path parks its hit point (the same operations the bounce loop's
         // shading used to apply to (cam, t, d): D = d t_scale, pos = cam + t D)
@@ -673,7 +659,85 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         sl[1 * 64] = v1;
         sl[2 * 64] = v2;
         sl[3 * 64] = __int_as_float(code);
+    };
+#if RT_PS_PRIM_BATCH > 1
+    // The primary rays all start at the camera, so the cofactors of the exact test that
+    // involve only b = cam - v0 and the edges (s3, s4, s6, det_t) are the same for every
+    // sample of the wave: computed once per candidate for a batch of samples, each sample
+    // then runs the direction-dependent rest (exact_one_c's operations on the same
+    // operands in the same order: the same bits).  Samples of a batch fold the candidates
+    // in index order each, as before.
+    constexpr int PB = RT_PS_PRIM_BATCH;
+    for (int k0 = 0; k0 < pc; k0 += PB) {
+        f3 dd[PB];
+        float nx[PB], ny[PB], nz[PB];
+        Hit hh[PB];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) {
+            const int s = chunk * pc + min(k0 + j, pc - 1);
+            float r1, r2;
+            draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+            camera_ray<0>(a, px, py, r1, r2, &dd[j]);
+            nx[j] = -(dd[j].x * nts);
+            ny[j] = -(dd[j].y * nts);
+            nz[j] = -(dd[j].z * nts);
+            hh[j].t = (RULE == 0) ? FLT_MAX : 999999.0f;
+            hh[j].tri = -1;
+        }
+#pragma unroll
+        for (int g = 0; g < kRenderCullWords; ++g) {
+            uint64_t m = cm[g];
+            while (m != 0ull) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1ull;
+                const int i = g * 64 + b;
+                const float4 A = ldc(isect + i * kIsectF4 + 0);
+                const float4 E1 = ldc(isect + i * kIsectF4 + 1);
+                const float4 E2 = ldc(isect + i * kIsectF4 + 2);
+                const float bx = cam.x - A.x, by = cam.y - A.y, bz = cam.z - A.z;
+                const float s3 = by * E2.z - E2.y * bz;
+                const float s4 = by * E1.z - E1.y * bz;
+                const float det_t = (bx * A.w - E1.x * s3) + E2.x * s4;
+                const float s6 = E1.y * bz - by * E1.z;
+#pragma unroll
+                for (int j = 0; j < PB; ++j) {
+                    const float s1 = ny[j] * E2.z - E2.y * nz[j];
+                    const float s2 = ny[j] * E1.z - E1.y * nz[j];
+                    const float detA = (nx[j] * A.w - E1.x * s1) + E2.x * s2;
+                    const float s5 = ny[j] * bz - by * nz[j];
+                    const float det_u = (nx[j] * s3 - bx * s1) + E2.x * s5;
+                    const float det_v = (nx[j] * s6 - E1.x * s5) + bx * s2;
+                    exact_test<RULE>(detA, det_t, det_u, det_v, i, hh[j]);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < PB; ++j)
+            if (k0 + j < pc) park(k0 + j, dd[j], hh[j]);
     }
+#else
+    for (int k = 0; k < pc; ++k) {
+        const int s = chunk * pc + k;
+        float r1, r2;
+        draw2(pix, (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
+        f3 d;
+        camera_ray<0>(a, px, py, r1, r2, &d);
+        const float nDx = -(d.x * nts), nDy = -(d.y * nts), nDz = -(d.z * nts);
+        Hit h;
+        h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+        h.tri = -1;
+#pragma unroll
+        for (int g = 0; g < kRenderCullWords; ++g) {
+            uint64_t m = cm[g];
+            while (m != 0ull) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1ull;
+                exact_one_c<RULE>(isect, g * 64 + b, cam, nDx, nDy, nDz, h);
+            }
+        }
+        park(k, d, h);
+    }
+#endif
 
     // ---- phase S: bounces ----
 #if RT_PROF

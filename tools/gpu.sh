@@ -17,6 +17,11 @@
 #                            profiles/<tag>_<workload>_bench_pmc.json (bench.py's roofline)
 #   ab:<variant,variant,..>  tools/ab_render.py over build/variants/<v> (same image check)
 #   run:<name>:<limit>:<cmd> any command, output in gpurun_out/<tag>/<name>.log
+#   configs[:<w1,w2,..>]     for each profile workload (tools/bench_pmc_summary.py WORKLOADS; default:
+#                            the five BASELINE configs at their stated sizes): pmc, kt, wbench
+# A/B recipes: build the variants here (tools/build_variants.sh name "flags" ...), then
+#   ab:<v1,v2>                         Cornell frame, same image checked (tools/ab_render.py)
+#   run:x:600:'RTMI_LIB=.../variants/<v>/librtmi.so python3 tools/bench_sarsa.py' (or bench_dqn.py)
 # Outputs: gpurun_out/<tag>/ (gpurun copies only gpurun_out/ back); the summaries meant for
 # profiles/ go to gpurun_out/<tag>/profiles/.  Here, without a GPU:
 #   bash tools/gpu.sh <tag> collect      copies them into profiles/
@@ -65,7 +70,7 @@ for step in "$@"; do
       run "wbench_$arg" 400 $(bench_cmd "$arg" | sed 's/--cpu-seconds 0//') ;;
     kt)
       w=${arg:-cornell}
-      steps=20; [ "$w" = cornell ] && steps=40
+      steps=""; [ "$w" = cornell ] && steps=40  # (others: the profiled command's own frames)
       run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" $steps)
       mkdir -p "$out/profiles"
       cp "$out/kt_$w/kt_kernel_stats.csv" "$out/profiles/${tag}_${w}_kernel_stats.csv" ;;
@@ -83,6 +88,10 @@ for step in "$@"; do
       mkdir -p profiles
       for f in "$out"/profiles/*; do [ -e "$f" ] && cp -v "$f" profiles/; done
       for f in "$out"/smoke.log "$out"/tests.log "$out"/bench*.log "$out"/wbench*.log; do [ -e "$f" ] && cp "$f" "profiles/${tag}_$(basename "$f")"; done ;;
+    configs)
+      for w in $(echo "${arg:-cornell_c1,cornell,door_room_sarsa,archway_dqn,complex_light}" | tr ',' ' '); do
+        "$0" "$tag" "pmc:$w" "kt:$w" "wbench:$w" || exit $?
+      done ;;
     ab) run "ab" 400 python3 -u tools/ab_render.py $(echo "$arg" | tr ',' '\n' | sed 's#^#build/variants/#') --split 64 --rounds 7 ;;
     run)
       name=${arg%%:*}; rest=${arg#*:}; lim=${rest%%:*}; cmd=${rest#*:}
