@@ -311,7 +311,24 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         # the HBM leg of the same kernel: measured DRAM bytes per frame / its time
         line["hbm_gbs"] = round(line["traffic"] / t / 1e9, 1)
         line["hbm_frac"] = round(line["hbm_gbs"] / HBM_PEAK_GBS, 4)
+        if prof.get("fetch_scale") == 1:
+            line["traffic_note"] = ("FETCH_SIZE + WRITE_SIZE at the L2's fabric side, FETCH_SIZE not doubled "
+                                    "(gathers, not 16-B streams); Infinity-Cache hits included, so an upper "
+                                    "bound on DRAM bytes")
     line["kernels"] = kernel_table(prof if match else None, args, kt)
+    # what the counters say holds the kernel back: the busiest pipe, or latency when no pipe
+    # is near its roof and most wave cycles wait (s_waitcnt / barrier)
+    pipes = {"valu_issue": line.get("valu_issue_frac"), "hbm": line.get("hbm_frac"),
+             "matrix": line.get("mfma_busy_frac")}
+    pipes = {k: v for k, v in pipes.items() if v is not None}
+    wait = line.get("wave_cycles_waiting_frac")
+    if pipes:
+        top = max(pipes, key=pipes.get)
+        if wait is not None and wait > 0.4 and pipes[top] < 0.5:
+            line["limiter"] = (f"latency: {wait:.0%} of wave cycles waiting on memory / LDS, busiest pipe "
+                               f"{top} at {pipes[top]:.0%}")
+        else:
+            line["limiter"] = f"{top} at {pipes[top]:.0%}"
     if bound == "mfma":
         n_in = geom.nn_vertices.size
         dims = [n_in, 200, 300, 200, 144]
@@ -362,6 +379,11 @@ def kernel_table(prof, args, kt: dict) -> dict:
     return out
 
 
+def progress(msg: str) -> None:
+    """a stderr line per stage (long runs stay visibly alive; stdout keeps the one JSON line)"""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds):
     """The CPU restatement (oracle/, OpenMP over rows) on a bounded sample of a learned-sampler
     frame, best of 3 ("for configs 4-5, CPU time may be measured on a reduced
@@ -405,57 +427,70 @@ def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds):
                 f"bf16-emulating DQN forward at every bounce (the frame's own spp {params.spp}: per-sample "
                 f"cost is independent of it)")
     best, casts = None, 0
-    for _ in range(3):
+    for i in range(3):
         t0 = time.perf_counter()
         _, casts = run()
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
+        progress(f"cpu baseline run {i + 1}/3: {casts} ray casts in {dt:.2f} s")
     return {"value": round(casts / best / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"{what}; {casts} ray casts, best of 3: {best:.2f} s, OpenMP over rows"}
 
 
 def cpu_baseline(geom, params, cam_pos, seconds):
-    """Time the CPU restatement (oracle/, OpenMP) on a bounded strip of the same frame,
-    best of 3, and one thread on a 2-row strip."""
+    """Time the CPU restatement (oracle/, OpenMP over rows) on a bounded strip of the same frame,
+    best of 3, and one thread on a 2-row strip.  A frame whose rows cost
+    more than the budget is sampled at fewer spp (<= 16 per pixel: a sample's cost does not
+    depend on the frame's spp); the strip is then not the frame's own pixels (no parity strip)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
     oracle.set_threads(threads)
-    op = oracle.params_from(params)
     ocam = oracle.camera(cam_pos)
     w = params.width
-    rows, y0 = 4, params.height // 2 - 2
+    sp = params
+    if params.spp > 16:
+        sp = rtmi.default_params(params.preset, width=params.width, height=params.height, spp=16,
+                                 spp_split=min(params.spp_split, 16))
+    op = oracle.params_from(sp)
+    rows, y0 = max(4, min(threads, 16)), params.height // 2 - 2
     t0 = time.perf_counter()
     _, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
     rate = casts / max(time.perf_counter() - t0, 1e-9)
     per_row = casts / rows
+    if sp is not params and rate * seconds >= per_row * params.spp / sp.spp * params.height:
+        sp, op = params, oracle.params_from(params)  # the whole frame at its own spp fits the budget
+        per_row *= params.spp / 16
     rows = int(max(4, min(params.height, seconds * rate / max(per_row, 1.0))))
     if rows >= 0.6 * params.height:  # most of the frame anyway: take all of it (a full-frame parity check)
         rows = params.height
     y0 = max(0, params.height // 2 - rows // 2)
     best, strip = None, None
-    for _ in range(3):
+    for i in range(3):
         t0 = time.perf_counter()
         strip, casts = oracle.render(geom, ocam, op, (0, y0, w, rows))
         dt = time.perf_counter() - t0
         best = dt if best is None else min(best, dt)
+        progress(f"cpu baseline run {i + 1}/3: rows {y0}..{y0 + rows - 1} at {sp.spp} spp, {casts} ray casts in {dt:.2f} s")
     oracle.set_threads(1)
     y1 = params.height // 2 - 1
     t0 = time.perf_counter()
     _, casts1 = oracle.render(geom, ocam, op, (0, y1, w, 2))
     dt1 = time.perf_counter() - t0
     oracle.set_threads(threads)
+    own = sp is params
     return {
         "value": round(casts / best / 1e6, 3),
         "unit": "Mrays/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"rows {y0}..{y0 + rows - 1} of the {w}x{params.height}/{params.spp}-spp frame "
-                  f"({casts} ray casts, best of 3: {best:.2f} s, OpenMP over rows)",
+        "sample": f"rows {y0}..{y0 + rows - 1} of the {w}x{params.height} frame at {sp.spp} spp"
+                  + ("" if own else f" (the frame's own spp {params.spp}: per-sample cost is independent of it)")
+                  + f" ({casts} ray casts, best of 3: {best:.2f} s, OpenMP over rows)",
         "value_1thread": round(casts1 / max(dt1, 1e-9) / 1e6, 3),
-        "sample_1thread": f"rows {y1}..{y1 + 1} ({casts1} ray casts, {dt1:.2f} s, 1 thread)",
-    }, (y0, rows, strip, casts)
+        "sample_1thread": f"rows {y1}..{y1 + 1} at {sp.spp} spp ({casts1} ray casts, {dt1:.2f} s, 1 thread)",
+    }, ((y0, rows, strip, casts) if own else None)
 
 
 def parity_strip(ctx, scene, cam, params, image, strip_run):
@@ -563,6 +598,8 @@ def main():
     for i in range(args.warmup):
         pipe.gather_frame(pipe.render_frame(i))
     pipe.drain()
+    if rank == 0:
+        progress(f"{args.workload}: {args.warmup} warmup frame(s) done, timing {args.steps}")
     torch.cuda.synchronize()
     casts.zero_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -599,6 +636,7 @@ def main():
 
     frame = pipe.frame(args.steps - 1)
     if rank == 0:
+        progress(f"timed: {elapsed / args.steps * 1e3:.3f} ms per step")
         image = rtmi.tiles.assemble(frame.cpu().numpy(), params.width, params.height, TILE, world)
         line = {
             "metric": f"Mrays/sec ({WORKLOADS[args.workload][0]} {params.width}^2 {params.spp}spp ray casts)"
@@ -635,7 +673,7 @@ def main():
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
             if sampler == "uniform":
                 line["cpu_baseline"], strip_run = cpu_baseline(geom, params, cam_pos, args.cpu_seconds)
-                if "parity" in line:  # the baseline's strip is the same frame: check it too
+                if "parity" in line and strip_run is not None:  # the baseline's strip is the same frame: check it too
                     line["parity"]["cpu_strip"] = parity_strip(ctx, scene, cam, params, image, strip_run)
             else:
                 line["cpu_baseline"] = cpu_baseline_learned(sampler, geom, params, cam_pos, args.cpu_seconds)

@@ -354,6 +354,9 @@ struct SarsaMap {
     const int4* class_dim = nullptr;       // [n_class] cells per axis
     const float4* class_nrm = nullptr;     // [n_class] the class normal
     const uint32_t* cell_start = nullptr;  // [cells + 1] first grid_leaf of each cell
+    const uint2* cell_range = nullptr;     // [cells] {first, end} grid_leaf of each cell (one load)
+    const float4* tri_grid = nullptr;      // [n_surf][2] the surface's class grid: {org, first cell (bits)},
+                                           // {dims (int bits), class (int bits, -1: none)}
     const float4* grid_leaf = nullptr;     // [n] volume positions by (class, cell), w = volume (int bits)
     float grid_inv_cs = 0.f;               // 1 / cell size
     float grid_cs = 0.f;                   // cell size (cell centres: org + (i + 0.5) cs)
@@ -367,6 +370,7 @@ struct SarsaMap {
     int td_inframe = 0;
     int32_t* qmax = nullptr;               // [n] first sector of largest Q (k_sarsa_apply)
     unsigned long long* stats = nullptr;   // [2] launch: sum of per-pixel int(mean path length), zero paths
+    unsigned long long* prof = nullptr;    // [8] RT_SARSA_PROF builds: per-phase s_memtime cycles (rt_sarsa.hip)
 };
 #ifndef RT_KD_STACK
 #define RT_KD_STACK 32

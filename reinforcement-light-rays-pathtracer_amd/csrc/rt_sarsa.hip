@@ -27,6 +27,9 @@
 #ifndef RT_SARSA_NO_TD
 #define RT_SARSA_NO_TD 0
 #endif
+#ifndef RT_SARSA_PROF
+#define RT_SARSA_PROF 0  // 1: k_sarsa_render_pq sums per-phase s_memtime cycles into SarsaMap::prof (timing builds)
+#endif
 #ifndef RT_SARSA_NO_KD
 #define RT_SARSA_NO_KD 0
 #endif
@@ -105,12 +108,12 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
 // (sarsa_resolve_walks).
 constexpr int kNeedWalk = -2;  // sarsa_nearest_grid: only the KD walk decides this query
 
-__device__ int sarsa_nearest_grid(const SarsaMap& m, int cls, f3 pos, f3 nrm) {
-    if (RT_SARSA_NO_KD) return 0;
+#ifndef RT_SARSA_TRIREC
+#define RT_SARSA_TRIREC 1  // 0: class -> grid descriptor -> cell start / end as four dependent loads (A/B)
+#endif
+// G, D: the class grid's origin (w: first cell, bits) and cells per axis
+__device__ int sarsa_nearest_grid_gd(const SarsaMap& m, float4 G, int4 D, f3 pos) {
     {
-        if (cls < 0) return 0;
-        const float4 G = m.class_org[cls];
-        const int4 D = m.class_dim[cls];
         const float ic = m.grid_inv_cs;
         // padded cell of the query (rt_sarsa_host.cpp grid_cell): its list holds every
         // class volume of the 3x3x3 neighbourhood
@@ -118,7 +121,15 @@ __device__ int sarsa_nearest_grid(const SarsaMap& m, int cls, f3 pos, f3 nrm) {
         const int iy = (int)floorf(fminf(fmaxf((pos.y - G.y) * ic, 0.0f), (float)(D.y - 1)));
         const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, 0.0f), (float)(D.z - 1)));
         const uint32_t c = __float_as_uint(G.w) + (uint32_t)((iz * D.y + iy) * D.x + ix);
-        const uint32_t k0 = m.cell_start[c], e = m.cell_start[c + 1];
+        uint32_t k0, e;
+        if (RT_SARSA_TRIREC) {
+            const uint2 r = m.cell_range[c];
+            k0 = r.x;
+            e = r.y;
+        } else {
+            k0 = m.cell_start[c];
+            e = m.cell_start[c + 1];
+        }
         // The list is sorted by distance to the cell centre C: d(q, L) >= d(C, L) - d(q, C),
         // so once d(C, L) exceeds best + d(q, C) (with a 2^-12 margin: such a candidate's
         // float distance is strictly above the best, no tie either) no later one can win.
@@ -173,8 +184,27 @@ __device__ int sarsa_nearest_grid(const SarsaMap& m, int cls, f3 pos, f3 nrm) {
         if (m.grid_fallbacks != nullptr) atomicAdd(m.grid_fallbacks, 1ull);
         if (RT_SARSA_NO_FALLBACK) return bv >= 0 ? bv : 0;
     }
-    (void)nrm;
     return kNeedWalk;
+}
+
+// cls: normal class of the query (-1: no volume has its normal -- the KD walk keeps volume 0)
+__device__ int sarsa_nearest_grid(const SarsaMap& m, int cls, f3 pos, f3 nrm) {
+    (void)nrm;
+    if (RT_SARSA_NO_KD) return 0;
+    if (cls < 0) return 0;
+    return sarsa_nearest_grid_gd(m, m.class_org[cls], m.class_dim[cls], pos);
+}
+
+// the same for a hit on surface tri: its class's grid descriptor in one per-surface record
+// (two independent loads instead of the class, then its descriptor)
+__device__ int sarsa_nearest_grid_tri(const SarsaMap& m, int tri, f3 pos, f3 nrm) {
+    if (RT_SARSA_NO_KD) return 0;
+    if (!RT_SARSA_TRIREC) return sarsa_nearest_grid(m, m.tri_class[tri], pos, nrm);
+    const float4 G = m.tri_grid[2 * tri];
+    const float4 Df = m.tri_grid[2 * tri + 1];
+    const int4 D = make_int4(__float_as_int(Df.x), __float_as_int(Df.y), __float_as_int(Df.z), __float_as_int(Df.w));
+    if (D.w < 0) return 0;
+    return sarsa_nearest_grid_gd(m, G, D, pos);
 }
 
 #ifndef RT_SARSA_COOP_KD
@@ -302,9 +332,28 @@ __device__ int sarsa_class_of(const SarsaMap& m, f3 nrm) {
     return -1;
 }
 
-// sample_direction_from_radiance_distribution (radiance_volume.cu:191-244)
-__device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float ry, int* sector, f3* dir,
-                             float* pdf) {
+// The sampling volume's per-frame data, loaded as soon as the volume is known (sarsa_step):
+// its CDF row ends (one 64-B line) and its frame (N, T, B with the position)
+struct VolPre {
+    float4 t0, t1, t2, t3;
+    float4 N4, T4, B4;
+};
+__device__ __forceinline__ VolPre vol_load(const SarsaMap& m, int rv) {
+    VolPre v;
+    const float4* tp = m.cdf_top + (size_t)rv * 4;
+    v.t0 = tp[0];
+    v.t1 = tp[1];
+    v.t2 = tp[2];
+    v.t3 = tp[3];
+    v.N4 = m.vol_frame[rv * 3 + 0];
+    v.T4 = m.vol_frame[rv * 3 + 1];
+    v.B4 = m.vol_frame[rv * 3 + 2];
+    return v;
+}
+
+// sample_direction_from_radiance_distribution (radiance_volume.cu:191-244); vp: vol_load(m, rv)
+__device__ bool sarsa_sample(const SarsaMap& m, int rv, const VolPre& vp, float r, float rx, float ry, int* sector,
+                             f3* dir, float* pdf) {
     const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
     int found = -1;
     float mv = 0.0f, pv = 0.0f;
@@ -314,8 +363,7 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     // independent loads (the 12 row ends, then one 12-sector row) instead of 8
     // dependent probes; the rare equal / NaN cases run the search itself.
     bool exact = false;
-    const float4* tp = m.cdf_top + (size_t)rv * 4;  // one 64-B line: cdf[0] and the row ends
-    const float4 t0 = tp[0], t1 = tp[1], t2 = tp[2], t3 = tp[3];
+    const float4 t0 = vp.t0, t1 = vp.t1, t2 = vp.t2, t3 = vp.t3;  // one 64-B line: cdf[0] and the row ends
     const float c0 = t0.x;
     if (r <= c0) {
         found = 0;
@@ -377,7 +425,7 @@ __device__ bool sarsa_sample(const SarsaMap& m, int rv, float r, float rx, float
     const int sy = found - sx * kGridRes;
     *sector = found;
     *pdf = kRho * ((found == 0 ? mv : (mv - pv)) / kGridRhoS);
-    const float4 N4 = m.vol_frame[rv * 3 + 0], T4 = m.vol_frame[rv * 3 + 1], B4 = m.vol_frame[rv * 3 + 2];
+    const float4 N4 = vp.N4, T4 = vp.T4, B4 = vp.B4;
     *dir = grid_direction((float)sx + rx, (float)sy + ry, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                           make3(B4.x, B4.y, B4.z), make3(N4.w, T4.w, B4.w));
     return true;
@@ -396,7 +444,7 @@ __device__ __forceinline__ float live_load(const float* p) {
 // (TD = 1): the reference's scan of the live radiance grid at every sample (:251-257), the
 // CDF still the frame's (update_radiance_volume_distributions runs between frames).
 template <int TD>
-__device__ void sarsa_sample_max(const SarsaMap& m, int rv, float rx, float ry, int* sector, f3* dir,
+__device__ void sarsa_sample_max(const SarsaMap& m, int rv, const VolPre& vp, float rx, float ry, int* sector, f3* dir,
                                  float* pdf) {
     const float* __restrict__ cdf = m.cdf + (size_t)rv * kSarsaSectors;
     int mi;
@@ -420,7 +468,7 @@ __device__ void sarsa_sample_max(const SarsaMap& m, int rv, float rx, float ry, 
     const int sy = mi - sx * kGridRes;
     *sector = mi;
     *pdf = kRho * ((mv - last) / kGridRhoS);
-    const float4 N4 = m.vol_frame[rv * 3 + 0], T4 = m.vol_frame[rv * 3 + 1], B4 = m.vol_frame[rv * 3 + 2];
+    const float4 N4 = vp.N4, T4 = vp.T4, B4 = vp.B4;
     *dir = grid_direction((float)sx + rx, (float)sy + ry, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                           make3(B4.x, B4.y, B4.z), make3(N4.w, T4.w, B4.w));
 }
@@ -473,6 +521,11 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
                                            f3 pos, f3 nrm, int rv, bool td, uint32_t pix, int s, SarsaPath& P,
                                            unsigned& n_casts, f3* L_out) {
     const float4* __restrict__ shade = a.scene.shade;
+    // the volume this hit samples from, and its data loaded now: in flight with the TD
+    // target's irradiance load, the TD atomics and the Philox block
+    const int sv = (td || (P.depth == 0 && is_surf)) ? rv : P.cur_rv;
+    VolPre vp;
+    if (is_surf && sv >= 0) vp = vol_load(m, sv);
     if (td) {
         float target;
         if (h.tri < 0) {
@@ -514,9 +567,9 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
                        (sx * B4.z + c * nrm.z) + sz * T4.z);
             pdf = kRho;
         } else if (m.sample_max) {
-            sarsa_sample_max<TD>(m, P.cur_rv, u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
+            sarsa_sample_max<TD>(m, P.cur_rv, vp, u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
         } else {
-            ok = sarsa_sample(m, P.cur_rv, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
+            ok = sarsa_sample(m, P.cur_rv, vp, u01_oc(rn[0]), u01_oc(rn[1]), u01_oc(rn[2]), &P.cur_sector, &sd, &pdf);
         }
         if (!ok) {
             // no sector: the reference traces the zero direction it returns, which
@@ -616,7 +669,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         const bool td = active && depth > 0 && cur_rv >= 0 && cur_sector >= 0;
         int rv = -1;
         if (is_surf && (depth == 0 || td))
-            rv = m.use_grid ? sarsa_nearest_grid(m, m.tri_class[h.tri], pos, nrm) : kNeedWalk;
+            rv = m.use_grid ? sarsa_nearest_grid_tri(m, h.tri, pos, nrm) : kNeedWalk;
         if (m.use_grid)  // the grid's few undecided queries: walked by the whole wave
             sarsa_resolve_walks(m, pos, nrm, &rv, kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64), st, lane);
         else if (rv == kNeedWalk)
@@ -716,6 +769,9 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
     SarsaPath P{cam, make3(0.f, 0.f, 1.f), make3(1.f, 1.f, 1.f), 0, -1, -1, 0.0f};
     f3 acc = make3(0.f, 0.f, 0.f);
     unsigned n_casts = 0, n_zero = 0, casts0 = 0;
+#if RT_SARSA_PROF
+    uint64_t pr[6] = {0, 0, 0, 0, 0, 0};  // trace, grid search, walks, step (TD + sampling), trips, active lanes
+#endif
     auto camera = [&]() {
         float r1, r2;
         draw2(pix, a.sample_base + (uint32_t)s, 0u, a.seed_lo, a.seed_hi, &r1, &r2);
@@ -777,6 +833,10 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
             if (exhausted) break;
             continue;
         }
+#if RT_SARSA_PROF
+        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+        pr[5] += (uint64_t)__builtin_popcountll(__ballot(active));
+#endif
         Hit h;
         h.t = 0.0f;
         h.tri = -1;
@@ -787,6 +847,9 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
         } else if (active) {
             h = closest_hit_sel<RULE>(a.scene, a.use_filter, P.o, P.d, a.t_scale);
         }
+#if RT_SARSA_PROF
+        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
         if (active) ++n_casts;
         const bool is_surf = active && (h.tri >= 0) && (h.tri < n_surf);
         f3 pos = P.o;
@@ -800,14 +863,31 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
         const bool td = active && P.depth > 0 && P.cur_rv >= 0 && P.cur_sector >= 0;
         int rv = -1;
         if (is_surf && (P.depth == 0 || td))
-            rv = m.use_grid ? sarsa_nearest_grid(m, m.tri_class[h.tri], pos, nrm) : kNeedWalk;
+            rv = m.use_grid ? sarsa_nearest_grid_tri(m, h.tri, pos, nrm) : kNeedWalk;
+#if RT_SARSA_PROF
+        const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+#endif
         if (m.use_grid)
             sarsa_resolve_walks(m, pos, nrm, &rv, blk_ws, st, lane);
         else if (rv == kNeedWalk)
             rv = sarsa_nearest(m, pos, nrm, st);
+#if RT_SARSA_PROF
+        const uint64_t pt3 = __builtin_amdgcn_s_memtime();
+        f3 L;
+        const bool term = active && sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
+        const uint64_t pt4 = __builtin_amdgcn_s_memtime();
+        pr[0] += pt1 - pt0;
+        pr[1] += pt2 - pt1;
+        pr[2] += pt3 - pt2;
+        pr[3] += pt4 - pt3;
+        pr[4] += 1;
+        if (!active) continue;
+        if (term) {
+#else
         if (!active) continue;
         f3 L;
         if (sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L)) {
+#endif
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
@@ -829,6 +909,10 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
         const unsigned tot = wave_sum(n_casts);
         if (lane == 0) atomicAdd(a.casts, (unsigned long long)tot);
     }
+#if RT_SARSA_PROF
+    if (m.prof != nullptr && lane == 0)
+        for (int i = 0; i < 6; ++i) atomicAdd(m.prof + i, (unsigned long long)pr[i]);
+#endif
 }
 
 // the pixels of k_sarsa_render_pq's launch: the chunk sums in chunk order / spp, and the

@@ -342,6 +342,7 @@ bool build_nearest_grid(const std::vector<float>& pos, const std::vector<float>&
     return true;
 }
 
+
 }  // namespace
 
 struct rt_sarsa {
@@ -367,6 +368,7 @@ struct rt_sarsa {
         for (void* p : allocs) (void)hipFree(p);
         if (d_csum) (void)hipFree(d_csum);
         if (d_work) (void)hipFree(d_work);
+        if (m.prof) (void)hipFree(m.prof);
     }
     template <class T>
     hipError_t alloc(T** p, size_t count) {
@@ -429,7 +431,18 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
     a.csum = sa->d_csum;
     a.work = sa->d_work;
     RT_HIPE(hipMemsetAsync(sa->m.stats, 0, 2 * sizeof(unsigned long long), stream));
+    // RT_SARSA_PROF (with an RT_SARSA_PROF=1 kernel build): the render's per-phase cycles to stderr
+    static const bool prof = getenv("RT_SARSA_PROF") != nullptr;
+    if (prof && !sa->m.prof) RT_HIPE(hipMalloc(&sa->m.prof, 8 * sizeof(unsigned long long)));
+    if (prof) RT_HIPE(hipMemsetAsync(sa->m.prof, 0, 8 * sizeof(unsigned long long), stream));
     RT_HIPE(rt::launch_sarsa_render(a, sa->m, stream));
+    if (prof) {
+        unsigned long long v[8];
+        RT_HIPE(hipStreamSynchronize(stream));
+        RT_HIPE(hipMemcpy(v, sa->m.prof, sizeof(v), hipMemcpyDeviceToHost));
+        fprintf(stderr, "{\"sarsa_prof\": {\"trace\": %llu, \"grid\": %llu, \"walks\": %llu, \"step\": %llu, "
+                        "\"trips\": %llu, \"active_lanes\": %llu}}\n", v[0], v[1], v[2], v[3], v[4], v[5]);
+    }
     if (apply) RT_HIPE(rt::launch_sarsa_apply(sa->m, stream));
     sa->frames += 1;
     return RT_OK;
@@ -570,6 +583,9 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     int4* d_cdim = nullptr;
     uint32_t* d_cstart = nullptr;
     unsigned long long* d_fb = nullptr;
+    uint2* d_crange = nullptr;
+    float4* d_tgrid = nullptr;
+
     if (e == hipSuccess) e = sa->alloc(&d_fb, 1);
     unsigned long long* d_stats = nullptr;
     int32_t* d_qmax = nullptr;
@@ -582,7 +598,10 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         if (e == hipSuccess) e = sa->alloc(&d_cdim, grid.dim.size());
         if (e == hipSuccess) e = sa->alloc(&d_cstart, grid.start.size());
         if (e == hipSuccess) e = sa->alloc(&d_leaf, grid.leaf.size());
+        if (e == hipSuccess) e = sa->alloc(&d_crange, grid.start.size() - 1);
+        if (e == hipSuccess) e = sa->alloc(&d_tgrid, 2 * grid.tri_class.size());
     }
+
     auto up = [&](void* d, const void* h, size_t bytes) {
         if (e == hipSuccess && bytes) e = hipMemcpy(d, h, bytes, hipMemcpyHostToDevice);
     };
@@ -612,7 +631,23 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         up(d_cdim, grid.dim.data(), sizeof(int4) * grid.dim.size());
         up(d_cstart, grid.start.data(), sizeof(uint32_t) * grid.start.size());
         up(d_leaf, grid.leaf.data(), sizeof(float4) * grid.leaf.size());
+        std::vector<uint2> range(grid.start.size() - 1);
+        for (size_t c = 0; c + 1 < grid.start.size(); ++c) range[c] = make_uint2(grid.start[c], grid.start[c + 1]);
+        up(d_crange, range.data(), sizeof(uint2) * range.size());
+        // per surface: its class's grid descriptor (the kernel's one-step lookup)
+        std::vector<float4> tg(2 * grid.tri_class.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t j = 0; j < grid.tri_class.size(); ++j) {
+            const int k = grid.tri_class[j];
+            int4 d = make_int4(0, 0, 0, -1);
+            if (k >= 0) {
+                tg[2 * j] = grid.org[k];
+                d = make_int4(grid.dim[k].x, grid.dim[k].y, grid.dim[k].z, k);
+            }
+            memcpy(&tg[2 * j + 1], &d, sizeof(d));
+        }
+        up(d_tgrid, tg.data(), sizeof(float4) * tg.size());
     }
+
     if (e == hipSuccess) e = hipMemset(d_fb, 0, sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(d_stats, 0, 2 * sizeof(unsigned long long));
     if (e == hipSuccess) e = hipMemset(d_qmax, 0, sizeof(int32_t) * n);  // every Q equal: sector 0
@@ -652,6 +687,9 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         m.class_nrm = d_cnrm;
         m.cell_start = d_cstart;
         m.grid_leaf = d_leaf;
+        m.cell_range = d_crange;
+        m.tri_grid = d_tgrid;
+
         m.grid_inv_cs = grid.inv_cs;
         m.grid_cs = grid.cs;
         m.grid_h = grid.h;
