@@ -159,6 +159,8 @@ namespace rt {
 void release_dqn_workspace(const rt_ctx* ctx);
 int ctx_device(const rt_ctx* ctx) { return ctx->device; }
 const DeviceScene& scene_device(const rt_scene* s) { return s->dev; }
+// the device view a render launch takes (the BVH fields set when the scene's BVH path is on)
+DeviceScene scene_launch_view(const rt_scene* s) { return launch_scene(s); }
 void scene_host(const rt_scene* s, const float** tri, const float** normals, const float** albedo,
                 const float** emission, int* n_surf, int* n_light) {
     *tri = s->tri.data();

@@ -72,6 +72,8 @@ constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
 constexpr int kSampBlocks = 4;
 constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 9 Philox draws
 static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
+// the fused sampler maps a thread to a (ray, block): 64 rays on kSampBlocks waves
+constexpr bool kFusedFits = kTileM == 64 && kMlpThreads == 64 * kSampBlocks;
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
 
 __device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
@@ -372,13 +374,14 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
         }
         float* const srow = stage + r * kStageStride;
         // (1) Q*cos of the block's cells (one Philox draw per four cells, counter 1 + a/4), B_w
+        const PhiloxShared ph = philox_shared(pixid, sample, smp.ev, smp.k0, smp.k1);
         if (live) {
             const int c0 = w * kSampCells;
             float b = 0.0f;
 #pragma unroll 3
             for (int a = c0; a < c0 + kSampCells; a += 4) {
                 uint32_t o[4];
-                philox4x32_10(pixid, sample, smp.ev, 1u + (uint32_t)(a >> 2), smp.k0, smp.k1, o);
+                philox_from(ph, 1u + (uint32_t)(a >> 2), o);
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
                     const float qc = srow[a + h] * chiu_cos_cell(a + h, u16lo(o[h]), u16hi(o[h]));
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
         float* const hq = reinterpret_cast<float*>(hit + kRows * kSampBlocks);
         if (live) {
             uint32_t o[4];
-            philox4x32_10(pixid, sample, smp.ev, 0u, smp.k0, smp.k1, o);
+            philox_from(ph, 0u, o);
             const float rv = u01(o[0]);
             float bs[kSampBlocks];
             float total = 0.0f;
@@ -488,15 +491,14 @@ struct SampleOut {
 
 // the chosen cell's jittered direction (Philox counter 1 + 72) and the throughput update
 // cos / pdf, pdf = RHO * (qd / GRID_RHO) -- the end of importance_sample_direction
-__device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 N, f3 T, f3 B, f3 pos, uint32_t pix,
-                                                   uint32_t smp, uint32_t ev, uint32_t k0, uint32_t k1, f3* tp,
-                                                   bool update_tp) {
+__device__ __forceinline__ SampleOut sample_finish(int action, float qd_sel, f3 N, f3 T, f3 B, f3 pos,
+                                                   const PhiloxShared& ph, f3* tp, bool update_tp) {
     SampleOut res;
     res.action = action;
     res.dir = make3(0.0f, 0.0f, 0.0f);
     if (action >= 0) {
         uint32_t o[4];
-        philox4x32_10(pix, smp, ev, 1u + kDqnActions / 2, k0, k1, o);
+        philox_from(ph, 1u + kDqnActions / 2, o);
         const int gxi = action / kDqnGrid;
         const int gyi = action - gxi * kDqnGrid;
         res.dir = grid_direction((float)gxi + u01(o[0]), (float)gyi + u01(o[1]), N, T, B, pos);
@@ -532,8 +534,10 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
                                                    uint32_t pix, uint32_t smp, uint32_t ev,
                                                    uint32_t k0, uint32_t k1, f3* tp, bool update_tp) {
     static_assert(!(WB && QB), "the in-place Q*cos store needs the fp32 buffer");
+    // every draw of the ray shares (pixel, sample, event): rounds 1-3's shared part once
+    const PhiloxShared ph = philox_shared(pix, smp, ev, k0, k1);
     uint32_t o[4];
-    philox4x32_10(pix, smp, ev, 0u, k0, k1, o);
+    philox_from(ph, 0u, o);
     const float rv = u01(o[0]);
     // Q is read in groups of kQGroup cells (all loads of a group in flight at once:
     // one-at-a-time loads put an HBM round trip on every cell)
@@ -557,7 +561,7 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
 #pragma unroll
         for (int u4 = 0; u4 < kQGroup; u4 += 4) {
             uint32_t r[4];
-            philox4x32_10(pix, smp, ev, 1u + (uint32_t)((g + u4) >> 2), k0, k1, r);
+            philox_from(ph, 1u + (uint32_t)((g + u4) >> 2), r);
 #pragma unroll
             for (int h = 0; h < 4; ++h) qv[u4 + h] = qv[u4 + h] * chiu_cos_cell(g + u4 + h, u16lo(r[h]), u16hi(r[h]));
         }
@@ -605,13 +609,14 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
         }
         P = Pn;
     }
-    return sample_finish(res.action, qd_sel, N, T, B, pos, pix, smp, ev, k0, k1, tp, update_tp);
+    return sample_finish(res.action, qd_sel, N, T, B, pos, ph, tp, update_tp);
 }
 
 // trace_ray (pre_trained_pathtracer.cu:413-491): Ray(pos + dir*1e-5, dir), GPU hit rule.
 // Returns true if the ray continues (hit a surface).
 // MF > 0: the cast on the matrix-core filter (closest_hit_mf: every lane of the wave
 // calls, `active` false for a lane without a ray, which then returns false untouched).
+// MF < 0: the exact BVH (large scenes, closest_hit_bvh), wl = the lane's LDS stack column.
 template <int MF>
 __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bool active, float* wl, f3* loc_out,
                                           int* tri_out, f3* tp) {
@@ -621,6 +626,9 @@ __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bo
     if constexpr (MF > 0) {
         h = closest_hit_mf<1, false, MF>(a.scene, o, d, a.t_scale, active, wl);
         if (!active) return false;
+    } else if constexpr (MF < 0) {
+        if (!active) return false;
+        h = closest_hit_bvh<1, 256>(a.scene, o, d, a.t_scale, reinterpret_cast<int*>(wl));
     } else {
         if (!active) return false;
         h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
@@ -684,13 +692,22 @@ __device__ __forceinline__ f3 dqn_camera_dir(const DqnLaunch& a, float x, float 
     return d;
 }
 
+// the trace's LDS: MF > 0 the filter's per-wave scratch, MF < 0 the BVH stacks (a column per lane)
+__host__ __device__ constexpr int dqn_lds_floats(int mf) {
+    return mf > 0 ? 4 * kMfWaveFloats : (mf < 0 ? kBvhMaxDepth * 256 : 1);
+}
+template <int MF>
+__device__ __forceinline__ float* dqn_lane_ws(float* s) {
+    return MF < 0 ? s + threadIdx.x : s + ((int)threadIdx.x >> 6) * kMfWaveFloats;
+}
+
 // initialise_ray + the first trace_ray (bounce 0: no Q evaluation)
 #ifndef RT_MF_DQN_WAVES
 #define RT_MF_DQN_WAVES 4  // occupancy floor of the MF variants
 #endif
 template <int MF>
 __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camera(const DqnLaunch a) {
-    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
+    __shared__ float s_mfw[dqn_lds_floats(MF)];
     const int rid = blockIdx.x * 256 + threadIdx.x;
     bool keep = false;
     unsigned casts = 0;
@@ -712,7 +729,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camer
     }
     f3 loc;
     int tri = 0;
-    keep = dqn_trace<MF>(a, make3(a.cam_x, a.cam_y, a.cam_z), d, valid, s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats,
+    keep = dqn_trace<MF>(a, make3(a.cam_x, a.cam_y, a.cam_z), d, valid, dqn_lane_ws<MF>(s_mfw),
                          &loc, &tri, &tp);
     if (rid < a.rays.n) {
         if (keep) {
@@ -730,7 +747,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camer
 // FUSED: the cell was chosen by k_dqn_mlp<MT, true> (q[i] = its index bits, q[ldq + i] = qd)
 template <int MF, bool FUSED = false, bool QB = false>
 __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounce(const DqnLaunch a, int bounce) {
-    __shared__ float s_mfw[MF > 0 ? 4 * kMfWaveFloats : 1];
+    __shared__ float s_mfw[dqn_lds_floats(MF)];
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int n_act = a.rays.count[cur];
@@ -755,8 +772,9 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
         const float4 B4 = a.scene.shade[tri * kShadeF4 + 2];
         const SampleOut so =
             FUSED ? sample_finish(__float_as_int(a.rays.q[i]), a.rays.q[(size_t)a.rays.ldq + i], make3(N4.x, N4.y, N4.z),
-                                  make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
-                                  1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true)
+                                  make3(T4.x, T4.y, T4.z), make3(B4.x, B4.y, B4.z), pos,
+                                  philox_shared(pixid, (uint32_t)sample, 1u + (uint32_t)bounce, a.seed_lo, a.seed_hi),
+                                  &tp, true)
                   : sample_from_q<false, QB>(a.rays.q + i, (size_t)a.rays.ldq, make3(N4.x, N4.y, N4.z), make3(T4.x, T4.y, T4.z),
                                   make3(B4.x, B4.y, B4.z), pos, pixid, (uint32_t)sample,
                                   1u + (uint32_t)bounce, a.seed_lo, a.seed_hi, &tp, true);
@@ -771,7 +789,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
             tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
         }
     }
-    keep = dqn_trace<MF>(a, pos, dir, want, s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats, &loc, &ntri, &tp);
+    keep = dqn_trace<MF>(a, pos, dir, want, dqn_lane_ws<MF>(s_mfw), &loc, &ntri, &tp);
     if (i < n_act) {
         if (keep) {
             st3(a.rays.loc, rid, loc);
@@ -1048,10 +1066,13 @@ static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, cons
     }
     const int blocks = (max_rows + kTileM - 1) / kTileM;
     if (ldq != 0 && (ldq < blocks * kTileM || ldq % 4 != 0)) return hipErrorInvalidValue;
-    if (smp != nullptr)
-        hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net, loc,
-                           list, count, max_rows, q, ldq, *smp);
-    else if (qb && ldq != 0)
+    if (smp != nullptr) {
+        if constexpr (kFusedFits)
+            hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net,
+                               loc, list, count, max_rows, q, ldq, *smp);
+        else
+            return hipErrorInvalidValue;
+    } else if (qb && ldq != 0)
         hipLaunchKernelGGL((k_dqn_mlp<RT_MLP_MT, false, true>), dim3((unsigned)blocks), dim3(kMlpThreads), 0, stream, net,
                            loc, list, count, max_rows, q, ldq, MlpSample());
     else
@@ -1072,8 +1093,10 @@ hipError_t launch_dqn_frame_begin(const DqnLaunch& a, hipStream_t stream) {
 #define RT_MF_DQN 1  // 0: the casts on the fp32 filter (archway 512^2 x 16: 125.2 vs 120.9 ms, profiles/r3q)
 #endif
 // 64-triangle blocks of the matrix-core filter for this launch (0: the fp32 filter): the
-// image present and the camera inside its origin bound (as launch_render_t)
+// image present and the camera inside its origin bound (as launch_render_t); -1: the
+// scene's exact BVH (large scenes, the launch view carries it)
 static int dqn_mf(const DqnLaunch& a) {
+    if (a.scene.bvh_nodes != nullptr) return -1;
     const float cb = a.scene.mf_bound;
     const bool mf = RT_MF_DQN && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
@@ -1086,6 +1109,7 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
     switch (dqn_mf(a)) {
         case 1: hipLaunchKernelGGL(k_dqn_camera<1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
         case 4: hipLaunchKernelGGL(k_dqn_camera<4>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
+        case -1: hipLaunchKernelGGL(k_dqn_camera<-1>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
         default: hipLaunchKernelGGL(k_dqn_camera<0>, dim3(ray_blocks(a)), dim3(256), 0, stream, a); break;
     }
     return hipGetLastError();
@@ -1101,7 +1125,7 @@ hipError_t launch_dqn_camera(const DqnLaunch& a, hipStream_t stream) {
 hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream) {
     const int cur = (bounce - 1) & 1;
     // the fused sampler: the streaming forward (the weight-stationary A/B kernel writes Q)
-    const bool fused = RT_DQN_FUSED && !(a.net.mlp_mode == kMlpStationary && dqn_mlp_ws_fits(a.net)) &&
+    const bool fused = RT_DQN_FUSED && kFusedFits && !(a.net.mlp_mode == kMlpStationary && dqn_mlp_ws_fits(a.net)) &&
                        a.net.N[3] == kDqnActions && a.rays.ldq >= 2;
     MlpSample smp;
     smp.pix = a.rays.pix;
@@ -1121,6 +1145,7 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
         switch (dqn_mf(a)) {
             case 1: hipLaunchKernelGGL((k_dqn_bounce<1, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
             case 4: hipLaunchKernelGGL((k_dqn_bounce<4, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
+            case -1: hipLaunchKernelGGL((k_dqn_bounce<-1, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
             default: hipLaunchKernelGGL((k_dqn_bounce<0, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
         }
         return hipGetLastError();
@@ -1130,6 +1155,8 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
         case 3: hipLaunchKernelGGL((k_dqn_bounce<1, true>), grid, dim3(256), 0, stream, a, bounce); break;
         case 8: hipLaunchKernelGGL((k_dqn_bounce<4, false>), grid, dim3(256), 0, stream, a, bounce); break;
         case 9: hipLaunchKernelGGL((k_dqn_bounce<4, true>), grid, dim3(256), 0, stream, a, bounce); break;
+        case -2: hipLaunchKernelGGL((k_dqn_bounce<-1, false>), grid, dim3(256), 0, stream, a, bounce); break;
+        case -1: hipLaunchKernelGGL((k_dqn_bounce<-1, true>), grid, dim3(256), 0, stream, a, bounce); break;
         case 1: hipLaunchKernelGGL((k_dqn_bounce<0, true>), grid, dim3(256), 0, stream, a, bounce); break;
         default: hipLaunchKernelGGL((k_dqn_bounce<0, false>), grid, dim3(256), 0, stream, a, bounce); break;
     }

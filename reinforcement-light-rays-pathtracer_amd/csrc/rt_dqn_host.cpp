@@ -23,6 +23,7 @@ namespace rt {
 int set_error(int code, const char* msg);
 int ctx_device(const rt_ctx* ctx);
 const DeviceScene& scene_device(const rt_scene* s);
+DeviceScene scene_launch_view(const rt_scene* s);
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 }  // namespace rt
@@ -413,7 +414,7 @@ int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_came
     if (rc != RT_OK) return rc;
     rt::DqnLaunch a;
     memset(&a, 0, sizeof(a));
-    a.scene = rt::scene_device(scene);
+    a.scene = rt::scene_launch_view(scene);  // (large scenes: the exact BVH, dqn_trace<kMfBvh>)
     a.net = dqn->net;
     a.rays = ws->r;
     if (d_casts) a.rays.casts = reinterpret_cast<unsigned long long*>(d_casts);

@@ -124,6 +124,60 @@ RT_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+// Philox4x32-10 blocks that differ only in the last counter word c3 (the DQN sampler's 47
+// blocks of one ray: pixel, sample and event fixed, c3 = the draw): rounds 1-3 hold five
+// products and xors that do not depend on c3, computed once (philox_shared) instead of per
+// block; philox_from finishes a block -- the same words as philox4x32_10, bit for bit.
+struct PhiloxShared {
+    uint32_t r1_n0, r1_lo1, r1_x, r1_lo0;  // after round 1: (n0, lo1, n2 = r1_x ^ c3, lo0)
+    uint32_t r2_hi0, r2_lo0;               // round 2's product of the shared word n0
+    uint32_t k0, k1;                       // the key
+};
+RT_HD PhiloxShared philox_shared(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t k0, uint32_t k1) {
+    PhiloxShared s;
+    const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+    s.r1_n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    s.r1_lo1 = (uint32_t)p1;
+    s.r1_x = (uint32_t)(p0 >> 32) ^ k1;
+    s.r1_lo0 = (uint32_t)p0;
+    const uint64_t q0 = (uint64_t)0xD2511F53u * (uint64_t)s.r1_n0;
+    s.r2_hi0 = (uint32_t)(q0 >> 32);
+    s.r2_lo0 = (uint32_t)q0;
+    s.k0 = k0;
+    s.k1 = k1;
+    return s;
+}
+RT_HD void philox_from(const PhiloxShared& s, uint32_t c3, uint32_t out[4]) {
+    uint32_t k0 = s.k0 + 0x9E3779B9u, k1 = s.k1 + 0xBB67AE85u;
+    // round 2: (n0, lo1, n2, lo0) of round 1 with n2 = r1_x ^ c3
+    const uint32_t n2 = s.r1_x ^ c3;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)n2;
+    uint32_t c0 = (uint32_t)(p1 >> 32) ^ s.r1_lo1 ^ k0;
+    uint32_t c1 = (uint32_t)p1;
+    uint32_t c2 = s.r2_hi0 ^ s.r1_lo0 ^ k1;
+    uint32_t c3w = s.r2_lo0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+#pragma unroll
+    for (int r = 2; r < 10; ++r) {
+        const uint64_t q0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+        const uint64_t q1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+        const uint32_t n0 = (uint32_t)(q1 >> 32) ^ c1 ^ k0;
+        const uint32_t m2 = (uint32_t)(q0 >> 32) ^ c3w ^ k1;
+        c0 = n0;
+        c1 = (uint32_t)q1;
+        c2 = m2;
+        c3w = (uint32_t)q0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3w;
+}
+
 // 24-bit uniform in [0, 1)
 RT_HD float u01(uint32_t x) { return (float)(x >> 8) * 0x1p-24f; }
 // the two 16-bit uniforms of one Philox word, k/2^16 in [0, 1) (the DQN sampler's cell

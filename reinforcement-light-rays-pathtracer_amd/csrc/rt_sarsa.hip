@@ -748,7 +748,9 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
 #ifndef RT_SARSA_WAVES
 #define RT_SARSA_WAVES 5  // waves per SIMD of the persistent render (its grid: that many workgroups per CU)
 #endif
-template <int RULE, int MF, int TD>
+// BVH: scenes with the exact BVH (large models, rt_scene_set_accel): the casts through
+// closest_hit_bvh, its stack in the lane's k-d stack column (free until the volume search)
+template <int RULE, int MF, int TD, bool BVH = false>
 __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) void k_sarsa_render_pq(const RenderLaunch a,
                                                                                         const SarsaMap m) {
     __shared__ int kd_stack[kKdStack * 256];
@@ -840,7 +842,10 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
         Hit h;
         h.t = 0.0f;
         h.tri = -1;
-        if constexpr (MF > 0) {
+        if constexpr (BVH) {
+            static_assert(kKdStack >= kBvhMaxDepth, "the BVH stack fits the k-d stack column");
+            if (active) h = closest_hit_bvh<RULE, 64>(a.scene, P.o, P.d, a.t_scale, st);
+        } else if constexpr (MF > 0) {
             wave_lds_sync();
             h = closest_hit_mf<RULE, false, MF>(a.scene, P.o, P.d, a.t_scale, active, wl);
             wave_lds_sync();
@@ -1060,7 +1065,7 @@ namespace {
 template <int TD>
 hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipStream_t stream) {
     const float cb = a.scene.mf_bound;
-    const bool mf = RT_MF_SARSA && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
+    const bool mf = RT_MF_SARSA && a.scene.bvh_nodes == nullptr && a.use_filter && a.scene.mf_frag != nullptr && a.t_scale > 0.0f &&
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
                     fabsf(a.cam_z) <= cb;
     const bool one = a.scene.n_tri <= 64;
@@ -1082,7 +1087,12 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
                     hipLaunchKernelGGL((k_sarsa_render_pq<1, 4, TD>), grid, dim3(256), 0, stream, a, m);
             }
         }
-        if (!mf) {
+        if (a.scene.bvh_nodes != nullptr) {  // the exact BVH (large scenes)
+            if (a.hit_rule == 0)
+                hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD, true>), grid, dim3(256), 0, stream, a, m);
+            else
+                hipLaunchKernelGGL((k_sarsa_render_pq<1, 0, TD, true>), grid, dim3(256), 0, stream, a, m);
+        } else if (!mf) {
             if (a.hit_rule == 0)
                 hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD>), grid, dim3(256), 0, stream, a, m);
             else

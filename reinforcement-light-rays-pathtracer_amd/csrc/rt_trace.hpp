@@ -902,8 +902,8 @@ __device__ __forceinline__ float bvh_lam_hi(const BvhCand& c, const DeviceScene&
     return ((cut * t_scale + s.bvh_sig_a) / (1.0f - s.bvh_sig_b)) * 1.0000002f;
 }
 
-// stk: the lane's LDS stack, stride 256.
-template <int RULE>
+// stk: the lane's LDS stack (kBvhMaxDepth entries), STRIDE ints apart.
+template <int RULE, int STRIDE = 256>
 __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, int* stk) {
     const float nDx = -(d.x * t_scale), nDy = -(d.y * t_scale), nDz = -(d.z * t_scale);
     const float om = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
@@ -957,7 +957,7 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
             const bool h1 = slab(link + 1, lh, &e1);
             if (h0 && h1) {
                 const bool first0 = e0 <= e1;
-                stk[(sp++) * 256] = first0 ? link + 1 : link;
+                stk[(sp++) * STRIDE] = first0 ? link + 1 : link;
                 node = first0 ? link : link + 1;
                 continue;
             }
@@ -967,7 +967,7 @@ __device__ Hit closest_hit_bvh(const DeviceScene& s, f3 o, f3 d, float t_scale, 
             }
         }
         if (sp == 0) break;
-        node = stk[(--sp) * 256];
+        node = stk[(--sp) * STRIDE];
     }
     // grazing pairs (rt_bvh.cpp): the list of the ray's cube-map cell of directions, each
     // triangle tested for |d.N~| <= alpha B + beta and, with a window lambda, for its plane

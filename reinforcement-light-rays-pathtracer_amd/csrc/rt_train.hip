@@ -419,8 +419,9 @@ __global__ __launch_bounds__(256) void k_td_targets(const float* __restrict__ ne
     const float* q = next_q + (size_t)b * rt::kDqnActions;
     float best = q[0];
     uint32_t o[4];
+    const rt::PhiloxShared ph = rt::philox_shared(pix[b], sample, ev, k0, k1);  // 72 draws, one (pixel, sample, event)
     for (int a2 = 0; a2 < rt::kDqnActions; a2 += 2) {
-        rt::philox4x32_10(pix[b], sample, ev, 1u + (uint32_t)(a2 >> 1), k0, k1, o);
+        rt::philox_from(ph, 1u + (uint32_t)(a2 >> 1), o);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int a = a2 + h;

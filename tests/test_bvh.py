@@ -208,3 +208,41 @@ def test_bvh_small_scene_forced(rtmi_mod, gpu_ctx):
         img_b, casts_b = rtmi_mod.render(gpu_ctx, sc, cam, p)
     assert casts == casts_b
     assert np.array_equal(img.view(np.uint32), img_b.view(np.uint32))
+
+
+def test_bvh_sarsa_render_equals_scan(rtmi_mod, gpu_ctx):
+    """The SARSA sampler's trace on the BVH (k_sarsa_render_pq<.., BVH>) is the scan bit for bit:
+    two frames of the bunny in the Cornell box, the second sampling the map the first trained."""
+    g = bunny_cornell(rtmi_mod, rtmi_mod.RT_PRESET_GPU)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=8, spp_split=4)
+    out = {}
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        for accel in (None, rtmi_mod.ACCEL_SCAN):
+            if accel is not None:
+                sc.set_accel(accel)
+            with rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) as m:
+                out[accel] = [m.render(cam, p, 1) for _ in range(2)]
+    for (a, ca), (b, cb) in zip(out[None], out[rtmi_mod.ACCEL_SCAN]):
+        assert ca == cb
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    assert out[None][1][0].mean() > 0
+
+
+def test_bvh_dqn_render_equals_scan(rtmi_mod, gpu_ctx):
+    """The DQN sampler's casts on the BVH (dqn_trace<-1>) are the scan's bit for bit (synthetic
+    weights over the box's vertices as the network's inputs)."""
+    g = bunny_cornell(rtmi_mod, rtmi_mod.RT_PRESET_GPU)
+    box = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    nn = np.unique(box.tri.reshape(-1, 3), axis=0).astype(np.float32).ravel()
+    W, b = rtmi_mod.dqn.synthetic_weights(nn.size)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=4)
+    out = []
+    with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, nn, W, b) as net:
+        out.append(rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p))
+        sc.set_accel(rtmi_mod.ACCEL_SCAN)
+        out.append(rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p))
+    (a, ca), (b_, cb) = out
+    assert ca == cb and a.mean() > 0
+    assert np.array_equal(a.view(np.uint32), b_.view(np.uint32))
