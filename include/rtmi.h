@@ -171,9 +171,9 @@ int rt_intersect_method(rt_ctx* ctx, const rt_scene* scene, const float* orig, c
  * and a second BVH over the triangles' planes for the pairs a ray could graze (rt_bvh.cpp).  RT_ACCEL_AUTO (the
  * default) builds and uses it for scenes above RT_BVH_AUTO_MIN triangles; RT_ACCEL_SCAN
  * never uses it; RT_ACCEL_BVH builds it for any scene (A/B).  The default-sampler renders
- * (rt_render, rt_render_tiles_device) and rt_intersect / rt_intersect_device follow the mode;
- * the Expected-SARSA, DQN and Neural-Q kernels always run the (filtered) scan of every
- * triangle, whatever the mode. */
+ * (rt_render, rt_render_tiles_device), the Expected-SARSA, DQN and Neural-Q renders
+ * (their trace kernels take the BVH when the scene's mode turns it on) and rt_intersect /
+ * rt_intersect_device follow the mode. */
 #define RT_ACCEL_AUTO 0
 #define RT_ACCEL_SCAN 1
 #define RT_ACCEL_BVH 2

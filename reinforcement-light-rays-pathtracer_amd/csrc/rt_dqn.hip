@@ -932,8 +932,10 @@ __global__ __launch_bounds__(256) void k_nq_sample(const DqnLaunch a, const NqRa
 // miss: reward 0, terminal; light: reward = its luminance x 200, terminal; surface: the
 // new state, discount = the material's luminance.  Throughputs and path lengths change
 // only for paths still contributing (state 0).  The position before the trace is the
-// learning rule's S_t.
+// learning rule's S_t.  BVH: the scene's exact BVH (large scenes), a stack column per lane.
+template <bool BVH>
 __global__ __launch_bounds__(256) void k_nq_trace(const DqnLaunch a, const NqRays r, int bounce) {
+    __shared__ int s_stk[BVH ? kBvhMaxDepth * 256 : 1];
     const int i = blockIdx.x * 256 + threadIdx.x;
     unsigned casts = 0;
     if (i < r.n) {
@@ -941,7 +943,11 @@ __global__ __launch_bounds__(256) void k_nq_trace(const DqnLaunch a, const NqRay
         st3(r.prev, i, pos);
         const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
         const f3 d = normalize(dir);
-        const Hit h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
+        Hit h;
+        if constexpr (BVH)
+            h = closest_hit_bvh<1, 256>(a.scene, o, d, a.t_scale, s_stk + threadIdx.x);
+        else
+            h = closest_hit_sel<1>(a.scene, a.use_filter, o, d, a.t_scale);
         casts = 1;
         const uint32_t st = r.state[i];
         f3 tp = ld3(r.tp, i);
@@ -1196,7 +1202,10 @@ hipError_t launch_nq_sample(const DqnLaunch& a, const NqRays& r, float* q, float
     return hipGetLastError();
 }
 hipError_t launch_nq_trace(const DqnLaunch& a, const NqRays& r, int bounce, hipStream_t stream) {
-    hipLaunchKernelGGL(k_nq_trace, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, bounce);
+    if (a.scene.bvh_nodes != nullptr)
+        hipLaunchKernelGGL(k_nq_trace<true>, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, bounce);
+    else
+        hipLaunchKernelGGL(k_nq_trace<false>, dim3(nq_blocks(r)), dim3(256), 0, stream, a, r, bounce);
     return hipGetLastError();
 }
 hipError_t launch_nq_restart(const DqnLaunch& a, const NqRays& r, int sample, int bounce, hipStream_t stream) {

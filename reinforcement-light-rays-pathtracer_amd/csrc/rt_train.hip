@@ -43,6 +43,7 @@ namespace rt {
 int set_error(int code, const char* msg);
 int ctx_device(const rt_ctx* ctx);
 const DeviceScene& scene_device(const rt_scene* s);
+DeviceScene scene_launch_view(const rt_scene* s);
 void scene_host(const rt_scene* s, const float** tri, const float** normals, const float** albedo,
                 const float** emission, int* n_surf, int* n_light);
 }  // namespace rt
@@ -887,7 +888,7 @@ int rt_neuralq_render_frame(rt_ctx* ctx, rt_neuralq* q, const rt_camera* cam, co
     hipStream_t st = 0;
     rt::DqnLaunch a;
     memset(&a, 0, sizeof(a));
-    a.scene = rt::scene_device(q->scene);
+    a.scene = rt::scene_launch_view(q->scene);  // (large scenes: k_nq_trace<true> on the exact BVH)
     a.width = p->width;
     a.height = p->height;
     a.spp = p->spp;

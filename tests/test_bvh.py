@@ -246,3 +246,26 @@ def test_bvh_dqn_render_equals_scan(rtmi_mod, gpu_ctx):
     (a, ca), (b_, cb) = out
     assert ca == cb and a.mean() > 0
     assert np.array_equal(a.view(np.uint32), b_.view(np.uint32))
+
+
+def test_bvh_neuralq_frame_equals_scan(rtmi_mod, gpu_ctx):
+    """The Neural-Q trainer's casts on the BVH (k_nq_trace<true>) are the scan's: the same
+    frame, per-sample statistics and trained parameters, bit for bit."""
+    g = bunny_cornell(rtmi_mod, rtmi_mod.RT_PRESET_GPU)
+    box = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    nn = np.unique(box.tri.reshape(-1, 3), axis=0).astype(np.float32).ravel()
+    W, b = rtmi_mod.dqn.synthetic_weights(nn.size)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=32, height=24, spp=2)
+    out = []
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        for accel in (None, rtmi_mod.ACCEL_SCAN):
+            if accel is not None:
+                sc.set_accel(accel)
+            with rtmi_mod.dqn.DqnTrainer(gpu_ctx, nn, W, b) as tr, \
+                    rtmi_mod.dqn.NeuralQ(gpu_ctx, sc, tr, batch_size=256) as nq:
+                img, stats, casts = nq.render_frame(cam, p)
+                out.append((img, stats, casts, tr.params()))
+    (i1, s1, c1, (W1, _)), (i2, s2, c2, (W2, _)) = out
+    assert c1 == c2 and np.array_equal(i1, i2) and np.array_equal(s1, s2)
+    assert all(np.array_equal(x, y) for x, y in zip(W1, W2))

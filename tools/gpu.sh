@@ -73,7 +73,8 @@ for step in "$@"; do
       steps=""; [ "$w" = cornell ] && steps=40  # (others: the profiled command's own frames)
       run "kt_$w" 400 rocprofv3 --kernel-trace --stats -d "$out/kt_$w" -o kt --output-format csv -- $(bench_cmd "$w" $steps)
       mkdir -p "$out/profiles"
-      cp "$out/kt_$w/kt_kernel_stats.csv" "$out/profiles/${tag}_${w}_kernel_stats.csv" ;;
+      cp "$out/kt_$w/kt_kernel_stats.csv" "$out/profiles/${tag}_${w}_kernel_stats.csv"
+      rm -rf "$out/kt_$w" ;;  # (the traces of a 10k-launch frame exceed what gpurun copies back)
     pmc)
       w=${arg:-cornell}
       pmc_pass "$w" fetch FETCH_SIZE
@@ -83,7 +84,8 @@ for step in "$@"; do
       pmc_pass "$w" sq3 SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_BF16 SQ_INSTS_VALU_MFMA_F32 GRBM_GUI_ACTIVE
       run "pmc_summary_$w" 60 python3 tools/bench_pmc_summary.py "$out/pmc_$w" "$tag" "$w" "$out/profiles"
       # (the box's scratch tree: later bench / wbench steps of this call find the profile)
-      cp "$out"/profiles/*_bench_pmc.json profiles/ ;;
+      cp "$out"/profiles/*_bench_pmc.json profiles/
+      rm -rf "$out/pmc_$w" ;;  # raw counter CSVs: summarised above
     collect)
       mkdir -p profiles
       for f in "$out"/profiles/*; do [ -e "$f" ] && cp -v "$f" profiles/; done
