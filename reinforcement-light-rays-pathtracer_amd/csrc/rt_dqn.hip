@@ -59,11 +59,21 @@ constexpr int slots(int tiles) { return (tiles + kMlpWaves - 1) / kMlpWaves; }
 #define RT_MLP_RING_VGPRS 60  // VGPRs of the weight-fragment ring (60: 3 K steps of layer 1's 5 fragments)
 #endif
 constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
+#ifndef RT_MLP_A_DB
+#define RT_MLP_A_DB 1
+#endif
 #ifndef RT_MLP_PROLOGUE_GROUP
 #define RT_MLP_PROLOGUE_GROUP 1
 #endif
 constexpr int kStrideA = 336;
 constexpr int kStrideB = 272;
+#ifndef RT_MLP_INPLACE
+// 1: one activation buffer (stride 336) that every layer reads and then overwrites (a
+// barrier between the K loop and the epilogue; the accumulators hold the layer's outputs
+// meanwhile): 2 * 336 * 2 B per row instead of (336 + 272) * 2, so MT = 7 (112 rays, 75 KB)
+// still fits two workgroups per CU, and each weight fragment feeds 7 MFMAs instead of 4
+#define RT_MLP_INPLACE 0
+#endif
 __device__ __forceinline__ int swz(int row, int k, int stride) {
     return row * stride + (((k >> 3) ^ ((row >> 2) & 7)) << 3) + (k & 7);
 }
@@ -73,7 +83,7 @@ constexpr int kSampBlocks = 4;
 constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 9 Philox draws
 static_assert(kTileM * kStageStride * 4 <= kTileM * kStrideA * 2, "Q staging tile exceeds bufA");
 // the fused sampler maps a thread to a (ray, block): 64 rays on kSampBlocks waves
-constexpr bool kFusedFits = kTileM == 64 && kMlpThreads == 64 * kSampBlocks;
+constexpr bool kFusedFits = kTileM == 64 && kMlpThreads == 64 * kSampBlocks && !RT_MLP_INPLACE;
 constexpr float kGridRho = 1.0f / ((float)kDqnGrid * (float)kDqnGrid);  // GRID_RHO
 
 __device__ __forceinline__ unsigned wave_sum_u(unsigned v) {
@@ -143,7 +153,7 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 // unconditional: a conditional MFMA makes the compiler shuttle every accumulator
 // between AGPRs and VGPRs each K step) and are not stored.
 // ---------------------------------------------------------------------------
-template <int NT, bool LAST, int MT, int KS = 0>
+template <int NT, bool LAST, int MT, int KS = 0, bool INPLACE = false>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
                                           __bf16* out_lds, int out_stride) {
     const int lane = threadIdx.x & 63;
@@ -171,7 +181,10 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         // SIMD by its LDS anyway, so VGPRs up to 256 are free, and an L2 fragment load
         // (~1 us under load) needs several K steps of MFMAs (NT*MT*16 clk each) to hide.
         constexpr int R = (kMlpRingVgprs / (4 * NT)) < 2 ? 2 : (kMlpRingVgprs / (4 * NT));
-        bf16x8 bw[R][NT], a[2][MT];
+        // the activations of step k + 1 in flight during step k's MFMAs (RT_MLP_A_DB), or
+        // read at the top of their own step (MT * 4 fewer VGPRs: the wider tiles)
+        constexpr int AB = RT_MLP_A_DB ? 2 : 1;
+        bf16x8 bw[R][NT], a[AB][MT];
 #pragma unroll
         for (int s = 0; s < R - 1; ++s) {
             if (s < KS) {
@@ -196,20 +209,25 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
                 for (int j = 0; j < NT; ++j)
                     bw[(ks + R - 1) % R][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + (ks + R - 1) * 32 * 16);
             }
-            if (ks + 1 < KS) {
+            if (AB == 2 && ks + 1 < KS) {
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    a[(ks + 1) & 1][m] =
+                    a[(ks + 1) % AB][m] =
                         *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, (ks + 1) * 32 + kg, in_stride));
+            }
+            if (AB == 1 && ks > 0) {
+#pragma unroll
+                for (int m = 0; m < MT; ++m)
+                    a[0][m] = *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, ks * 32 + kg, in_stride));
             }
 #pragma unroll
             for (int j = 0; j < NT; ++j)
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % R][j], a[ks & 1][m], acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % R][j], a[ks % AB][m], acc[m][j], 0, 0, 0);
 #if RT_MLP_PROLOGUE_GROUP
             if (ks + R - 1 < KS) __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);  // VMEM reads
-            if (ks + 1 < KS) __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);      // LDS reads
+            if (AB == 2 ? ks + 1 < KS : ks > 0) __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);  // LDS reads
 #else
             __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);
             __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);
@@ -253,6 +271,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
     if (k0 < K) step(k0, b0);  // odd number of K steps
     }
+    if constexpr (INPLACE) __syncthreads();  // every wave has read the layer's input
     // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
     // (the weights are the MFMA's A operand, the activations its B operand, so a lane
     // holds 4 consecutive features of one ray: one 8-B (bf16) or 16-B (fp32) LDS store)
@@ -315,13 +334,13 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
 // q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
 // direction.  Q never leaves the chip.
 template <int MT, bool FUSED = false, bool QB = false>
-__global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
+__global__ __launch_bounds__(kMlpThreads, 2) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
                                                  float* __restrict__ q, int ldq, const MlpSample smp) {
     constexpr int kRows = MT * 16;
     __shared__ __attribute__((aligned(16))) __bf16 bufA[kRows * kStrideA];
-    __shared__ __attribute__((aligned(16))) __bf16 bufB[kRows * kStrideB];
+    __shared__ __attribute__((aligned(16))) __bf16 bufB[RT_MLP_INPLACE ? 8 : kRows * kStrideB];
     __shared__ float locs[kRows * 3];
     const int n_rows = (count != nullptr) ? min(*count, max_rows) : max_rows;
     const int row0 = blockIdx.x * kRows;
@@ -341,6 +360,24 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
         locs[row * 3 + 2] = z;
     }
     __syncthreads();
+#if RT_MLP_INPLACE
+    mlp_layer0<MT>(net, locs, bufA, kStrideA);
+    __syncthreads();
+    if (net.K[1] == 224 && net.K[2] == 320 && net.K[3] == 224) {  // the reference's 200-300-200 net
+        mlp_layer<slots(20), false, MT, 7, true>(net, 1, bufA, kStrideA, bufA, kStrideA);
+        __syncthreads();
+        mlp_layer<slots(14), false, MT, 10, true>(net, 2, bufA, kStrideA, bufA, kStrideA);
+        __syncthreads();
+        mlp_layer<slots(9), true, MT, 7, true>(net, 3, bufA, kStrideA, bufA, 0);
+    } else {
+        mlp_layer<slots(20), false, MT, 0, true>(net, 1, bufA, kStrideA, bufA, kStrideA);  // N <= 320
+        __syncthreads();
+        mlp_layer<slots(14), false, MT, 0, true>(net, 2, bufA, kStrideA, bufA, kStrideA);  // N <= 224
+        __syncthreads();
+        mlp_layer<slots(9), true, MT, 0, true>(net, 3, bufA, kStrideA, bufA, 0);           // N = 144
+    }
+    (void)bufB;
+#else
 #ifndef RT_MLP_SKIP_L0  // timing only: layer 0 not evaluated (wrong Q)
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
 #endif
@@ -358,8 +395,9 @@ __global__ __launch_bounds__(kMlpThreads) void k_dqn_mlp(const DqnNet net, const
         __syncthreads();
         mlp_layer<slots(9), true, MT>(net, 3, bufB, kStrideB, bufA, 0);           // N = 144
     }
+#endif
     __syncthreads();
-    if constexpr (FUSED) {
+    if constexpr (FUSED && kFusedFits) {
         static_assert(kRows == 64 && kMlpThreads == 64 * kSampBlocks, "the fused sampler maps a thread to a block");
         float* const stage = reinterpret_cast<float*>(bufA);  // [row][kStageStride]: Q -> Q*cos
         float* const bsum = reinterpret_cast<float*>(bufB);   // [row][block] B_w (bufB is free after layer 3)
@@ -1086,6 +1124,8 @@ static hipError_t launch_dqn_mlp_fused(const DqnNet& net, const float* loc, cons
                            list, count, max_rows, q, ldq, MlpSample());
     return hipGetLastError();
 }
+
+int dqn_mlp_tile_rows() { return kTileM; }
 
 static unsigned ray_blocks(const DqnLaunch& a) { return (unsigned)((a.rays.n + 255) / 256); }
 static unsigned pix_blocks(const DqnLaunch& a) { return (unsigned)((a.rays.n_pix + 255) / 256); }

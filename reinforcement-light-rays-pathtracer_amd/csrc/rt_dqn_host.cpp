@@ -357,6 +357,13 @@ int rt_dqn_sample(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float* q, c
 
 namespace {
 
+// the action-major Q buffer's leading dimension: the ray capacity rounded up to whole MLP
+// workgroup tiles (every launched row is written) and to 64
+int dqn_ldq(int n) {
+    const int t = rt::dqn_mlp_tile_rows();
+    return ((n + t - 1) / t * t + 63) / 64 * 64;
+}
+
 struct Workspace {
     rt::DqnRays r;
     std::vector<void*> allocs;
@@ -385,14 +392,14 @@ struct Workspace {
                   alloc(sizeof(uint32_t) * n, (void**)&r.pix) && alloc(sizeof(int32_t) * n, (void**)&r.list[0]) &&
                   alloc(sizeof(int32_t) * n, (void**)&r.list[1]) && alloc(sizeof(int32_t) * 4, (void**)&r.count) &&
                   alloc(sizeof(unsigned long long), (void**)&r.casts) &&
-                  alloc(sizeof(float) * rt::kDqnActions * (size_t)((n + 63) / 64 * 64), (void**)&r.q);
+                  alloc(sizeof(float) * rt::kDqnActions * (size_t)dqn_ldq(n), (void**)&r.q);
         if (!ok) {
             release();
             return err(RT_E_NOMEM, "DQN workspace allocation failed");
         }
         cap = n;
         r.n = n;
-        r.ldq = (n + 63) / 64 * 64;
+        r.ldq = dqn_ldq(n);
         return RT_OK;
     }
 };

@@ -238,7 +238,7 @@ struct DqnRays {
     int n = 0;              // rays of the current pass: n_pix * samples in flight
     int n_pix = 0;          // pixel slots (16x16 blocks x 256)
     int s0 = 0;             // sample of slot 0
-    int ldq = 0;            // leading dimension of q: ray capacity rounded up to the MLP tile (64)
+    int ldq = 0;            // leading dimension of q: ray capacity rounded up to whole MLP tiles and 64
 };
 
 struct DqnLaunch {
@@ -289,8 +289,10 @@ hipError_t launch_nq_restart(const DqnLaunch& a, const NqRays& r, int sample, in
 hipError_t launch_nq_end_sample(const DqnLaunch& a, const NqRays& r, hipStream_t stream);
 hipError_t launch_nq_image(const DqnLaunch& a, const NqRays& r, float* out, int spp, hipStream_t stream);
 
+// rays per k_dqn_mlp workgroup (an action-major q's ldq covers whole tiles)
+int dqn_mlp_tile_rows();
 // q layout: ldq == 0 -> [row][144] (the C ABI's); ldq > 0 -> action-major q[a * ldq + row],
-// ldq a multiple of 64 covering every launched row (the renderer's, coalesced per action)
+// ldq a multiple of 64 covering every launched row (whole MLP tiles; the renderer's, coalesced per action)
 hipError_t launch_dqn_mlp(const DqnNet& net, const float* loc, const int32_t* list,
                           const int32_t* count, int max_rows, float* q, int ldq, hipStream_t stream);
 // weight-stationary forward (rt_dqn_ws.hip): one workgroup per CU, the 200-300-200 shape
