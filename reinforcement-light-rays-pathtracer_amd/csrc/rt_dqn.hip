@@ -36,7 +36,7 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
 #ifndef RT_MLP_MT
-#define RT_MLP_MT 4  // 16-row M-tiles per MLP workgroup
+#define RT_MLP_MT 6  // 16-row M-tiles per MLP workgroup (96 rays; 4 with the two-buffer layout)
 #endif
 constexpr int kTileM = RT_MLP_MT * 16;  // rays per MLP workgroup
 #ifndef RT_MLP_WAVES
@@ -59,8 +59,16 @@ constexpr int slots(int tiles) { return (tiles + kMlpWaves - 1) / kMlpWaves; }
 #define RT_MLP_RING_VGPRS 60  // VGPRs of the weight-fragment ring (60: 3 K steps of layer 1's 5 fragments)
 #endif
 constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
+#ifndef RT_MLP_XPF
+// 1: each layer's first weight fragments prefetched during the previous layer (archway
+// 512^2 x 16 with MT = 4: 110.4 vs 111.2 ms; with MT = 6 it spills: 119.8 ms, profiles/r4p)
+#define RT_MLP_XPF 0
+#endif
 #ifndef RT_MLP_A_DB
-#define RT_MLP_A_DB 1
+#define RT_MLP_A_DB 0  // 1: the next K step's activations double-buffered in registers (MT = 4: 234 VGPRs)
+#endif
+#ifndef RT_MLP_SKIP_PAD
+#define RT_MLP_SKIP_PAD 0
 #endif
 #ifndef RT_MLP_PROLOGUE_GROUP
 #define RT_MLP_PROLOGUE_GROUP 1
@@ -72,7 +80,7 @@ constexpr int kStrideB = 272;
 // barrier between the K loop and the epilogue; the accumulators hold the layer's outputs
 // meanwhile): 2 * 336 * 2 B per row instead of (336 + 272) * 2, so MT = 7 (112 rays, 75 KB)
 // still fits two workgroups per CU, and each weight fragment feeds 7 MFMAs instead of 4
-#define RT_MLP_INPLACE 0
+#define RT_MLP_INPLACE 1  // archway 512^2 x 16: 107.4 (MT = 6) vs 110.5 ms (two buffers, MT = 4), profiles/r4o
 #endif
 __device__ __forceinline__ int swz(int row, int k, int stride) {
     return row * stride + (((k >> 3) ^ ((row >> 2) & 7)) << 3) + (k & 7);
@@ -153,9 +161,33 @@ __device__ __forceinline__ void mlp_layer0(const DqnNet& net, const float* __res
 // unconditional: a conditional MFMA makes the compiler shuttle every accumulator
 // between AGPRs and VGPRs each K step) and are not stored.
 // ---------------------------------------------------------------------------
-template <int NT, bool LAST, int MT, int KS = 0, bool INPLACE = false>
+// the weight-fragment ring depth of a layer with NT N-tile slots per wave
+constexpr int mlp_ring(int nt) { return (kMlpRingVgprs / (4 * nt)) < 2 ? 2 : (kMlpRingVgprs / (4 * nt)); }
+
+// wave's weight fragments of layer L, K steps 0 .. PS-1 (the layer's ring prologue), into
+// pre[s * NT + j]: issued ahead (the previous layer's tail, or layer 0 for layer 1) so a
+// layer starts with its first fragments in registers instead of an L2 round trip
+template <int NT, int PS>
+__device__ __forceinline__ void mlp_prefetch(const DqnNet& net, int L, bf16x8* pre) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int n_tiles = net.N[L] >> 4;
+    const uint16_t* __restrict__ W = net.W[L];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const uint16_t* wr = W + ((size_t)min(wave + kMlpWaves * j, n_tiles - 1) * (net.K[L] >> 5) * 64 + lane) * 8;
+#pragma unroll
+        for (int s = 0; s < PS; ++s) pre[s * NT + j] = *reinterpret_cast<const bf16x8*>(wr + s * 32 * 16);
+    }
+}
+
+// PRE_IN: the ring prologue (mlp_ring(NT) - 1 steps) arrives in pre_in (mlp_prefetch);
+// NTN > 0: the next layer's prologue (NTN slots, mlp_ring(NTN) - 1 steps) is issued into
+// pre_out once this layer's own weight loads are done (KS > 0 only)
+template <int NT, bool LAST, int MT, int KS = 0, bool INPLACE = false, bool PRE_IN = false, int NTN = 0>
 __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16* in_lds, int in_stride,
-                                          __bf16* out_lds, int out_stride) {
+                                          __bf16* out_lds, int out_stride, const bf16x8* pre_in = nullptr,
+                                          bf16x8* pre_out = nullptr) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int K = net.K[L];
@@ -180,7 +212,7 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         // copies).  R is set by the register budget: the kernel is held to two waves per
         // SIMD by its LDS anyway, so VGPRs up to 256 are free, and an L2 fragment load
         // (~1 us under load) needs several K steps of MFMAs (NT*MT*16 clk each) to hide.
-        constexpr int R = (kMlpRingVgprs / (4 * NT)) < 2 ? 2 : (kMlpRingVgprs / (4 * NT));
+        constexpr int R = mlp_ring(NT);
         // the activations of step k + 1 in flight during step k's MFMAs (RT_MLP_A_DB), or
         // read at the top of their own step (MT * 4 fewer VGPRs: the wider tiles)
         constexpr int AB = RT_MLP_A_DB ? 2 : 1;
@@ -189,7 +221,8 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         for (int s = 0; s < R - 1; ++s) {
             if (s < KS) {
 #pragma unroll
-                for (int j = 0; j < NT; ++j) bw[s][j] = *reinterpret_cast<const bf16x8*>(wrow[j] + s * 32 * 16);
+                for (int j = 0; j < NT; ++j)
+                    bw[s][j] = PRE_IN ? pre_in[s * NT + j] : *reinterpret_cast<const bf16x8*>(wrow[j] + s * 32 * 16);
             }
         }
 #pragma unroll
@@ -199,9 +232,12 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
         // the prologue's loads as their own groups: each step's groups below then claim
         // that step's own loads (without this the scheduler pairs step k's MFMAs with the
         // prologue's second step, and the ring is one step shallower than written)
-        __builtin_amdgcn_sched_group_barrier(0x020, (R - 1 < KS ? R - 1 : KS) * NT, 0);
+        if (!PRE_IN) __builtin_amdgcn_sched_group_barrier(0x020, (R - 1 < KS ? R - 1 : KS) * NT, 0);
         __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);
 #endif
+        constexpr int PN = NTN > 0 ? mlp_ring(NTN) - 1 : 0;  // next layer's prologue steps
+        const bool last_valid = __builtin_amdgcn_readfirstlane(wave) + kMlpWaves * (NT - 1) < n_tiles;
+        constexpr int KP = KS - R + 1 > 0 ? KS - R + 1 : 0;  // first step without own loads
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
             if (ks + R - 1 < KS) {
@@ -220,13 +256,19 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
                 for (int m = 0; m < MT; ++m)
                     a[0][m] = *reinterpret_cast<const bf16x8*>(in_lds + swz(m * 16 + r16, ks * 32 + kg, in_stride));
             }
+            if (PN > 0 && ks == KP) mlp_prefetch<(NTN > 0 ? NTN : 1), PN>(net, L + 1, pre_out);
 #pragma unroll
-            for (int j = 0; j < NT; ++j)
+            for (int j = 0; j < NT; ++j) {
+                // (RT_MLP_SKIP_PAD: the wave's last slot, past the layer's tiles for some waves,
+                // skipped by a wave-uniform branch instead of recomputing the last tile)
+                if (RT_MLP_SKIP_PAD && j == NT - 1 && !last_valid) continue;
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
                     acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % R][j], a[ks % AB][m], acc[m][j], 0, 0, 0);
+            }
 #if RT_MLP_PROLOGUE_GROUP
             if (ks + R - 1 < KS) __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);  // VMEM reads
+            if (PN > 0 && ks == KP) __builtin_amdgcn_sched_group_barrier(0x020, PN * (NTN > 0 ? NTN : 1), 0);
             if (AB == 2 ? ks + 1 < KS : ks > 0) __builtin_amdgcn_sched_group_barrier(0x100, MT, 0);  // LDS reads
 #else
             __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);
@@ -346,6 +388,12 @@ __global__ __launch_bounds__(kMlpThreads, 2) void k_dqn_mlp(const DqnNet net, co
     const int row0 = blockIdx.x * kRows;
     if (row0 >= n_rows) return;
     const int rows_valid = min(kRows, n_rows - row0);
+    // layer 1's first weight fragments in flight during the ray loads and layer 0
+    const bool ref_net = net.K[1] == 224 && net.K[2] == 320 && net.K[3] == 224;
+    bf16x8 p1[RT_MLP_XPF ? (mlp_ring(slots(20)) - 1) * slots(20) : 1];
+    if constexpr (RT_MLP_XPF != 0) {
+        if (ref_net) mlp_prefetch<slots(20), mlp_ring(slots(20)) - 1>(net, 1, p1);
+    }
     if (threadIdx.x < kRows) {
         const int row = threadIdx.x;
         float x = 0.0f, y = 0.0f, z = 0.0f;
@@ -363,12 +411,16 @@ __global__ __launch_bounds__(kMlpThreads, 2) void k_dqn_mlp(const DqnNet net, co
 #if RT_MLP_INPLACE
     mlp_layer0<MT>(net, locs, bufA, kStrideA);
     __syncthreads();
-    if (net.K[1] == 224 && net.K[2] == 320 && net.K[3] == 224) {  // the reference's 200-300-200 net
-        mlp_layer<slots(20), false, MT, 7, true>(net, 1, bufA, kStrideA, bufA, kStrideA);
+    if (ref_net) {  // the reference's 200-300-200 net
+        bf16x8 p2[RT_MLP_XPF ? (mlp_ring(slots(14)) - 1) * slots(14) : 1];
+        bf16x8 p3[RT_MLP_XPF ? (mlp_ring(slots(9)) - 1) * slots(9) : 1];
+        mlp_layer<slots(20), false, MT, 7, true, RT_MLP_XPF, RT_MLP_XPF ? slots(14) : 0>(net, 1, bufA, kStrideA, bufA,
+                                                                                      kStrideA, p1, p2);
         __syncthreads();
-        mlp_layer<slots(14), false, MT, 10, true>(net, 2, bufA, kStrideA, bufA, kStrideA);
+        mlp_layer<slots(14), false, MT, 10, true, RT_MLP_XPF, RT_MLP_XPF ? slots(9) : 0>(net, 2, bufA, kStrideA, bufA,
+                                                                                      kStrideA, p2, p3);
         __syncthreads();
-        mlp_layer<slots(9), true, MT, 7, true>(net, 3, bufA, kStrideA, bufA, 0);
+        mlp_layer<slots(9), true, MT, 7, true, RT_MLP_XPF>(net, 3, bufA, kStrideA, bufA, 0, p3);
     } else {
         mlp_layer<slots(20), false, MT, 0, true>(net, 1, bufA, kStrideA, bufA, kStrideA);  // N <= 320
         __syncthreads();
@@ -382,12 +434,16 @@ __global__ __launch_bounds__(kMlpThreads, 2) void k_dqn_mlp(const DqnNet net, co
     mlp_layer0<MT>(net, locs, bufB, kStrideB);
 #endif
     __syncthreads();
-    if (net.K[1] == 224 && net.K[2] == 320 && net.K[3] == 224) {  // the reference's 200-300-200 net
-        mlp_layer<slots(20), false, MT, 7>(net, 1, bufB, kStrideB, bufA, kStrideA);
+    if (ref_net) {  // the reference's 200-300-200 net
+        bf16x8 p2[RT_MLP_XPF ? (mlp_ring(slots(14)) - 1) * slots(14) : 1];
+        bf16x8 p3[RT_MLP_XPF ? (mlp_ring(slots(9)) - 1) * slots(9) : 1];
+        mlp_layer<slots(20), false, MT, 7, false, RT_MLP_XPF, RT_MLP_XPF ? slots(14) : 0>(net, 1, bufB, kStrideB, bufA,
+                                                                                       kStrideA, p1, p2);
         __syncthreads();
-        mlp_layer<slots(14), false, MT, 10>(net, 2, bufA, kStrideA, bufB, kStrideB);
+        mlp_layer<slots(14), false, MT, 10, false, RT_MLP_XPF, RT_MLP_XPF ? slots(9) : 0>(net, 2, bufA, kStrideA, bufB,
+                                                                                       kStrideB, p2, p3);
         __syncthreads();
-        mlp_layer<slots(9), true, MT, 7>(net, 3, bufB, kStrideB, bufA, 0);
+        mlp_layer<slots(9), true, MT, 7, false, RT_MLP_XPF>(net, 3, bufB, kStrideB, bufA, 0, p3);
     } else {
         mlp_layer<slots(20), false, MT>(net, 1, bufB, kStrideB, bufA, kStrideA);  // N <= 320
         __syncthreads();
