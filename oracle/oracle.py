@@ -264,7 +264,9 @@ def dqn_sample(tri_all, q, loc, tri, pix, sample, bounce, seed, tp):
     return q, tp, d, a
 
 
-def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False):
+def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False, q_bf16=True):
+    """orc_render_dqn; bf16: the kernel's arithmetic (bf16 forward, and with q_bf16 the
+    renderer's Q rounded to bf16 before the sampler, as k_dqn_mlp<.., QB> stores it)"""
     L = lib()
     L.orc_render_dqn.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_int, ctypes.c_int, ctypes.POINTER(_FP), ctypes.POINTER(_FP), _FP,
@@ -284,7 +286,7 @@ def render_dqn(geom, W, b, verts, cam, params, rect=None, bf16=False):
     casts = ctypes.c_uint64(0)
     L.orc_render_dqn(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp), get("light").shape[0],
                      W[0].shape[1], W[0].shape[0], W[1].shape[0], W[2].shape[0], _ptrs(W), _ptrs(b), _f(v),
-                     int(bf16), ctypes.byref(cam), ctypes.byref(params), x0, y0, w, h, _f(out),
+                     (1 if q_bf16 else 2) if bf16 else 0, ctypes.byref(cam), ctypes.byref(params), x0, y0, w, h, _f(out),
                      ctypes.byref(casts))
     return out, int(casts.value)
 

@@ -1011,8 +1011,10 @@ ORC_API int orc_render_dqn(const float *tri, const float *albedo, int n_surf, co
                         float locf[3] = {loc.x, loc.y, loc.z};
                         dqn_forward_one(&net, locf, bf16, q, scratch);
                         /* the kernel arithmetic (bf16 = 1) keeps the renderer's Q in bf16
-                         * between the forward and the sampler (k_dqn_mlp<.., QB>) */
-                        if (bf16)
+                         * between the forward and the sampler (k_dqn_mlp<.., QB>); bf16 = 2:
+                         * the bf16 forward with its fp32 Q (the statistical gate of that
+                         * rounding, tests/test_dqn.py) */
+                        if (bf16 == 1)
                             for (int a = 0; a < 144; a++) q[a] = bf16_round(q[a]);
                         const float *nn = sc.normal + (size_t)tri_i * 3;
                         v3 dir;

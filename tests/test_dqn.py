@@ -209,6 +209,29 @@ def test_config4_archway_dqn_matches_oracle(rtmi_mod, oracle_mod, gpu_ctx):
     assert rtmi_mod.metrics.mape_f(ref, img) <= noise, (rtmi_mod.metrics.mape_f(ref, img), noise)
 
 
+def test_oracle_bf16_q_rounding_gate(rtmi_mod, oracle_mod):
+    """Statistical gate of the renderer's bf16 Q (round 4: k_dqn_mlp<.., QB> stores Q in bf16
+    for the sampler; the restatement rounds the same way): the door_room frame with the
+    trained network, the same paths with Q rounded and with the fp32 Q the sampler took
+    before (CPU, no GPU).  Rounding can only move a CDF boundary by < 2^-9 of a cell's Q, so
+    the two renders differ where a draw falls in that sliver: the per-channel z of the paired
+    per-pixel differences stays below 3.5, and their MAPE stays below the seed-to-seed MAPE
+    of the unrounded render."""
+    g = door(rtmi_mod)
+    W, b = trained(rtmi_mod)
+    cam = oracle_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    rect = (56, 56, 16, 16)
+    p = oracle_mod.params_from(rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=8))
+    p7 = oracle_mod.params_from(rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=128, height=128, spp=8, seed=7))
+    rq, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, cam, p, rect, bf16=True, q_bf16=True)
+    rf, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, cam, p, rect, bf16=True, q_bf16=False)
+    alt, _ = oracle_mod.render_dqn(g, W, b, g.nn_vertices, cam, p7, rect, bf16=True, q_bf16=False)
+    assert rq.mean() > 0 and not np.array_equal(rq, rf)  # the rounding does change some paths
+    z = zscores(rq, rf)
+    assert np.all(z < 3.5), z
+    assert rtmi_mod.metrics.mape_f(rf, rq) <= rtmi_mod.metrics.mape_f(rf, alt)
+
+
 def test_oracle_wavefront_render_equals_per_path(rtmi_mod, oracle_mod):
     """orc_render_dqn_wave fed by the restatement's own bf16 forward is orc_render_dqn bit for
     bit: the wavefront order and the batched Q change nothing (CPU, no GPU)."""
