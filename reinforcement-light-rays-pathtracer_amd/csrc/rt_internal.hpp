@@ -357,6 +357,7 @@ struct SarsaMap {
     const float4* class_nrm = nullptr;     // [n_class] the class normal
     const uint32_t* cell_start = nullptr;  // [cells + 1] first grid_leaf of each cell
     const uint2* cell_range = nullptr;     // [cells] {first, end} grid_leaf of each cell (one load)
+    const float4* cell_head = nullptr;     // [cells][4] {first, end (bits)} + the cell's first 3 grid_leaf entries (one 64-B line)
     const float4* tri_grid = nullptr;      // [n_surf][2] the surface's class grid: {org, first cell (bits)},
                                            // {dims (int bits), class (int bits, -1: none)}
     const float4* grid_leaf = nullptr;     // [n] volume positions by (class, cell), w = volume (int bits)

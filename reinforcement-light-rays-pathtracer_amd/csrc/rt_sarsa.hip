@@ -108,6 +108,9 @@ __device__ int sarsa_nearest(const SarsaMap& m, f3 pos, f3 nrm, int* st) {
 // (sarsa_resolve_walks).
 constexpr int kNeedWalk = -2;  // sarsa_nearest_grid: only the KD walk decides this query
 
+#ifndef RT_SARSA_HEAD
+#define RT_SARSA_HEAD 1  // the cell's range and first three candidates as one 64-B record (0: range, then leaves)
+#endif
 #ifndef RT_SARSA_TRIREC
 #define RT_SARSA_TRIREC 1  // 0: class -> grid descriptor -> cell start / end as four dependent loads (A/B)
 #endif
@@ -122,6 +125,13 @@ __device__ int sarsa_nearest_grid_gd(const SarsaMap& m, float4 G, int4 D, f3 pos
         const int iz = (int)floorf(fminf(fmaxf((pos.z - G.z) * ic, 0.0f), (float)(D.z - 1)));
         const uint32_t c = __float_as_uint(G.w) + (uint32_t)((iz * D.y + iy) * D.x + ix);
         uint32_t k0, e;
+#if RT_SARSA_HEAD
+        const float4* hp = m.cell_head + (size_t)c * 4;
+        const float4 h0 = hp[0];
+        const float4 H[3] = {hp[1], hp[2], hp[3]};
+        k0 = __float_as_uint(h0.x);
+        e = __float_as_uint(h0.y);
+#else
         if (RT_SARSA_TRIREC) {
             const uint2 r = m.cell_range[c];
             k0 = r.x;
@@ -130,6 +140,7 @@ __device__ int sarsa_nearest_grid_gd(const SarsaMap& m, float4 G, int4 D, f3 pos
             k0 = m.cell_start[c];
             e = m.cell_start[c + 1];
         }
+#endif
         // The list is sorted by distance to the cell centre C: d(q, L) >= d(C, L) - d(q, C),
         // so once d(C, L) exceeds best + d(q, C) (with a 2^-12 margin: such a candidate's
         // float distance is strictly above the best, no tie either) no later one can win.
@@ -146,7 +157,29 @@ __device__ int sarsa_nearest_grid_gd(const SarsaMap& m, float4 G, int4 D, f3 pos
 #if RT_SARSA_FIRST_ONLY  // timing only: the first listed candidate (wrong volumes)
         if (k0 < e) return __float_as_int(m.grid_leaf[k0].w);
 #endif
-        for (uint32_t k = k0; k < e; k += 4) {  // 4 candidate loads in flight
+        uint32_t kb = k0;
+#if RT_SARSA_HEAD
+        // the cell record's own first three candidates (no break test before the first
+        // candidates: the limit is infinite there); the scan goes on from the fourth.  Where
+        // the scan's batches start does not change its answer: the break only skips
+        // candidates that can neither win nor tie.
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const float dx = H[u].x - pos.x, dy = H[u].y - pos.y, dz = H[u].z - pos.z;
+            const float s = (dx * dx + dy * dy) + dz * dz;  // len3's sum
+            if (k0 + (uint32_t)u < e) {
+                if (s < b1) {
+                    b2 = b1;
+                    b1 = s;
+                    bv = __float_as_int(H[u].w);
+                } else if (s < b2) {
+                    b2 = s;
+                }
+            }
+        }
+        kb = k0 + 3;
+#endif
+        for (uint32_t k = kb; k < e; k += 4) {  // 4 candidate loads in flight
 #if RT_SARSA_SCAN_STATS
             ++steps;
 #endif

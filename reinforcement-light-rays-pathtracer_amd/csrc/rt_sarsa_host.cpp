@@ -585,6 +585,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     unsigned long long* d_fb = nullptr;
     uint2* d_crange = nullptr;
     float4* d_tgrid = nullptr;
+    float4* d_chead = nullptr;
 
     if (e == hipSuccess) e = sa->alloc(&d_fb, 1);
     unsigned long long* d_stats = nullptr;
@@ -599,6 +600,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         if (e == hipSuccess) e = sa->alloc(&d_cstart, grid.start.size());
         if (e == hipSuccess) e = sa->alloc(&d_leaf, grid.leaf.size());
         if (e == hipSuccess) e = sa->alloc(&d_crange, grid.start.size() - 1);
+        if (e == hipSuccess) e = sa->alloc(&d_chead, 4 * (grid.start.size() - 1));
         if (e == hipSuccess) e = sa->alloc(&d_tgrid, 2 * grid.tri_class.size());
     }
 
@@ -634,6 +636,17 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         std::vector<uint2> range(grid.start.size() - 1);
         for (size_t c = 0; c + 1 < grid.start.size(); ++c) range[c] = make_uint2(grid.start[c], grid.start[c + 1]);
         up(d_crange, range.data(), sizeof(uint2) * range.size());
+        // per cell: its range and first three candidates in one 64-B record (the search's
+        // first load then already holds them: one dependent round trip less)
+        std::vector<float4> head(4 * range.size(), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t c = 0; c < range.size(); ++c) {
+            float fx, fy;
+            memcpy(&fx, &range[c].x, 4);
+            memcpy(&fy, &range[c].y, 4);
+            head[4 * c] = make_float4(fx, fy, 0.f, 0.f);
+            for (uint32_t u = 0; u < 3 && range[c].x + u < range[c].y; ++u) head[4 * c + 1 + u] = grid.leaf[range[c].x + u];
+        }
+        up(d_chead, head.data(), sizeof(float4) * head.size());
         // per surface: its class's grid descriptor (the kernel's one-step lookup)
         std::vector<float4> tg(2 * grid.tri_class.size(), make_float4(0.f, 0.f, 0.f, 0.f));
         for (size_t j = 0; j < grid.tri_class.size(); ++j) {
@@ -688,6 +701,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
         m.cell_start = d_cstart;
         m.grid_leaf = d_leaf;
         m.cell_range = d_crange;
+        m.cell_head = d_chead;
         m.tri_grid = d_tgrid;
 
         m.grid_inv_cs = grid.inv_cs;
