@@ -376,7 +376,10 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
 // q[ldq + i] = qd), 8 B instead of 576 B of Q per ray; k_dqn_bounce<MF, true> finishes the
 // direction.  Q never leaves the chip.
 template <int MT, bool FUSED = false, bool QB = false>
-__global__ __launch_bounds__(kMlpThreads, 2) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
+#ifndef RT_MLP_MIN_WAVES
+#define RT_MLP_MIN_WAVES 2  // waves per SIMD: the workgroups per CU that its LDS admits (3: MT = 4 in place)
+#endif
+__global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const DqnNet net, const float* __restrict__ loc,
                                                  const int32_t* __restrict__ list,
                                                  const int32_t* __restrict__ count, int max_rows,
                                                  float* __restrict__ q, int ldq, const MlpSample smp) {
