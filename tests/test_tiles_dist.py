@@ -173,3 +173,57 @@ def test_gloo_world2_sarsa_frame_refuses_in_frame_td():
         p.join(timeout=120)
     assert all(p.exitcode == 0 for p in procs)
     assert [q.get(timeout=5), q.get(timeout=5)] == [True, True]
+
+
+_RCCL_CHILD = r'''
+import os, sys
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, sys.argv[1])
+import rtmi
+dist.init_process_group("nccl", rank=0, world_size=1)  # RCCL on ROCm
+dev = torch.device("cuda:0")
+with rtmi.Context(0) as ctx, rtmi.Scene(ctx, rtmi.cornell_geometry(rtmi.RT_PRESET_GPU)) as sc, \
+        rtmi.sarsa.RadianceMap(ctx, sc, 1984) as rm:
+    # the TD accumulators librtmi owns, as the multi-rank SARSA frame hands them to RCCL
+    ts, tc = rtmi.dist.td_tensors(rm, dev)
+    ts.copy_(torch.arange(ts.numel(), dtype=torch.int64, device=dev) * 3 - 7)
+    tc.copy_(torch.arange(tc.numel(), dtype=torch.int32, device=dev) % 1000)
+    rs, rc = ts.clone(), tc.clone()
+    dist.all_reduce(ts, op=dist.ReduceOp.SUM)
+    dist.all_reduce(tc, op=dist.ReduceOp.SUM)
+    torch.cuda.synchronize()
+    assert torch.equal(ts, rs) and torch.equal(tc, rc)
+    # the tile gather, blocking and asynchronous (bench.py's double-buffered frames)
+    out = torch.randn((6, 32, 32, 3), device=dev)
+    g = [torch.empty_like(out)]
+    dist.gather(out, gather_list=g, dst=0)
+    w = dist.gather(out * 2, gather_list=g, dst=0, async_op=True)
+    w.wait()
+    torch.cuda.synchronize()
+    assert torch.equal(g[0], out * 2)
+    dist.barrier()
+print("RCCL OK", torch.cuda.nccl.version())
+dist.destroy_process_group()
+'''
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_collectives_on_librtmi_buffers(tmp_path):
+    """RCCL on the GPU (backend "nccl", one rank: the box has one GPU): all-reduce of the
+    SARSA TD accumulators librtmi owns (torch views through __cuda_array_interface__, as
+    rtmi.dist.sarsa_frame passes them) and the tile gather, blocking and asynchronous.  A
+    child process, so the test run keeps no process group."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "-c", _RCCL_CHILD, os.path.join(root, "reinforcement-light-rays-pathtracer_amd")],
+                       env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "RCCL OK" in r.stdout
