@@ -67,6 +67,21 @@ constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
 #ifndef RT_MLP_A_DB
 #define RT_MLP_A_DB 0  // 1: the next K step's activations double-buffered in registers (MT = 4: 234 VGPRs)
 #endif
+#ifndef RT_DQN_NT_LOAD
+#define RT_DQN_NT_LOAD 1  // the sampler's reads of the bf16 Q non-temporal (read once: archway 512^2 x 16 with the NT stores: 104.6 vs 106.4 ms, profiles/r4af)
+#endif
+#ifndef RT_MLP_NT_STORE
+#define RT_MLP_NT_STORE 1  // the renderer's bf16 Q stored non-temporally (106.4 vs 107.4 ms, profiles/r4af)
+#endif
+#ifndef RT_MLP_T_NOEPI  // timing-only knobs (wrong Q): the layers' epilogues, the ray loads, the Q stores
+#define RT_MLP_T_NOEPI 0
+#endif
+#ifndef RT_MLP_T_NOLOC
+#define RT_MLP_T_NOLOC 0
+#endif
+#ifndef RT_MLP_T_NOSTORE
+#define RT_MLP_T_NOSTORE 0
+#endif
 #ifndef RT_MLP_SKIP_PAD
 #define RT_MLP_SKIP_PAD 0
 #endif
@@ -315,6 +330,9 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
     if constexpr (INPLACE) __syncthreads();  // every wave has read the layer's input
     // epilogue: bias + ReLU (fc_layer.cu:40-72, dynet::rectify)
+#if RT_MLP_T_NOEPI  // timing only: no epilogue (wrong Q)
+    if (acc[0][0][0] != 12345.0f) return;
+#endif
     // (the weights are the MFMA's A operand, the activations its B operand, so a lane
     // holds 4 consecutive features of one ray: one 8-B (bf16) or 16-B (fp32) LDS store)
 #pragma unroll
@@ -400,7 +418,7 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
     if (threadIdx.x < kRows) {
         const int row = threadIdx.x;
         float x = 0.0f, y = 0.0f, z = 0.0f;
-        if (row < rows_valid) {
+        if (row < rows_valid && !RT_MLP_T_NOLOC) {  // (RT_MLP_T_NOLOC: timing only, positions 0)
             const int rid = (list != nullptr) ? list[row0 + row] : (row0 + row);
             x = loc[(size_t)rid * 3 + 0];
             y = loc[(size_t)rid * 3 + 1];
@@ -549,6 +567,9 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
     // 16-B stores: row-major rows are one contiguous run, action-major columns runs
     // of kRows rows (ldq covers every launched row, so padding rows may be written).
     const float* stage = reinterpret_cast<const float*>(bufA);
+#if RT_MLP_T_NOSTORE  // timing only: Q not written
+    if (stage[threadIdx.x] != 12345.0f) return;
+#endif
     if (ldq == 0) {
         float* dst = q + (size_t)row0 * kDqnActions;
         for (int t = threadIdx.x; t < rows_valid * (kDqnActions / 4); t += kMlpThreads) {
@@ -569,7 +590,14 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
                 const mlp_f32x2 v = {sp[k * kStageStride], sp[k * kStageStride + 1]};
                 w[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, mlp_bf16x2));
             }
+#if RT_MLP_NT_STORE
+            // streamed past the caches: the weights the other workgroups re-read stay in L2
+            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+            const u32x4v wv = {w[0], w[1], w[2], w[3]};
+            __builtin_nontemporal_store(wv, reinterpret_cast<u32x4v*>(q2 + (size_t)j * ldq + row0 + r));
+#else
             *reinterpret_cast<uint4*>(q2 + (size_t)j * ldq + row0 + r) = make_uint4(w[0], w[1], w[2], w[3]);
+#endif
         }
     } else {
         for (int t = threadIdx.x; t < kDqnActions * (kRows / 4); t += kMlpThreads) {
@@ -646,7 +674,12 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
             const uint32_t* q2 = reinterpret_cast<const uint32_t*>(q);
 #pragma unroll
             for (int u = 0; u < kQGroup; u += 2) {
+#if RT_DQN_NT_LOAD
+                const uint32_t w = stored ? q2[(size_t)((g + u) >> 1) * qs]
+                                          : __builtin_nontemporal_load(q2 + (size_t)((g + u) >> 1) * qs);
+#else
                 const uint32_t w = q2[(size_t)((g + u) >> 1) * qs];
+#endif
                 qv[u] = __uint_as_float(w << 16);
                 qv[u + 1] = __uint_as_float(w & 0xffff0000u);
             }
@@ -746,13 +779,27 @@ __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bo
     return true;
 }
 
+#ifndef RT_DQN_NT_STATE
+#define RT_DQN_NT_STATE 0  // 1: the per-ray state (position, throughput) loaded and stored non-temporally (A/B)
+#endif
 __device__ __forceinline__ f3 ld3(const float* p, int i) {
+#if RT_DQN_NT_STATE
+    return make3(__builtin_nontemporal_load(p + (size_t)i * 3), __builtin_nontemporal_load(p + (size_t)i * 3 + 1),
+                 __builtin_nontemporal_load(p + (size_t)i * 3 + 2));
+#else
     return make3(p[(size_t)i * 3], p[(size_t)i * 3 + 1], p[(size_t)i * 3 + 2]);
+#endif
 }
 __device__ __forceinline__ void st3(float* p, int i, f3 v) {
+#if RT_DQN_NT_STATE
+    __builtin_nontemporal_store(v.x, p + (size_t)i * 3);
+    __builtin_nontemporal_store(v.y, p + (size_t)i * 3 + 1);
+    __builtin_nontemporal_store(v.z, p + (size_t)i * 3 + 2);
+#else
     p[(size_t)i * 3] = v.x;
     p[(size_t)i * 3 + 1] = v.y;
     p[(size_t)i * 3 + 2] = v.z;
+#endif
 }
 
 // ray id -> pixel of the tile list
