@@ -143,8 +143,10 @@ PMC_GLOB = os.path.join(ROOT, "profiles", "*_bench_pmc.json")
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=None, help="timed frames (default: 20 for cornell, else 10)")
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed frames first (default: 10 for cornell -- the clock ramps over the first "
+                         "~40 ms of a 4-ms frame stream -- else 1)")
     ap.add_argument("--workload", default="cornell", choices=sorted(WORKLOADS))
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
@@ -153,7 +155,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target duration of one CPU-baseline run (best of 3; 0 disables)")
     ap.add_argument("--no-parity", action="store_true")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.steps is None:
+        args.steps = 20 if args.workload == "cornell" else 10
+    if args.warmup is None:
+        args.warmup = 10 if args.workload == "cornell" else 1
+    return args
 
 
 def lib_sha256() -> str:
