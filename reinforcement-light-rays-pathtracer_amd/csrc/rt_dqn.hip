@@ -7,7 +7,7 @@
 // NN_Builders/dq_network.cu + fc_layer.cu (4 ReLU affine layers).
 //
 // MI355X mapping:
-//  * k_dqn_mlp — the dense contraction.  One workgroup = 64 active rays (M),
+//  * k_dqn_mlp — the dense contraction.  One workgroup = 96 active rays (M = MT * 16),
 //    4 waves; each wave owns every M-tile and a quarter of the N-tiles, so each
 //    weight byte is fetched once per workgroup (from L2; 0.4-0.7 MB per net).
 //    v_mfma_f32_16x16x32_bf16 with fp32 accumulation; bias + ReLU fused in the
@@ -385,7 +385,7 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
     return chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
 }
 
-// One workgroup = MT*16 rays (LDS: MT=4 -> 77 KB, two workgroups per CU).
+// One workgroup = MT*16 rays (LDS: MT = 6 in place -> 66 KB, two workgroups per CU).
 // FUSED: instead of writing Q out, the workgroup runs importance_sample_direction's
 // selection (nn_rendering_helpers.cu:391-489) on its LDS tile in sample_from_q's blocked
 // order, one thread per (ray, block of 36 cells): Q*cos and the block sums, then the total,
