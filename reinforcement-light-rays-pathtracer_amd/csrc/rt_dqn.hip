@@ -73,6 +73,9 @@ constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
 #ifndef RT_MLP_NT_STORE
 #define RT_MLP_NT_STORE 1  // the renderer's bf16 Q stored non-temporally (106.4 vs 107.4 ms, profiles/r4af)
 #endif
+#ifndef RT_MLP_EPI2
+#define RT_MLP_EPI2 1  // packed epilogue (bias pairs, ReLU on bf16 pairs; archway 1024^2 x 16: 409.7 vs 417.0 ms, profiles/r4ao)
+#endif
 #ifndef RT_MLP_T_NOEPI  // timing-only knobs (wrong Q): the layers' epilogues, the ray loads, the Q stores
 #define RT_MLP_T_NOEPI 0
 #endif
@@ -88,6 +91,8 @@ constexpr int kMlpRingVgprs = RT_MLP_RING_VGPRS;
 #ifndef RT_MLP_PROLOGUE_GROUP
 #define RT_MLP_PROLOGUE_GROUP 1
 #endif
+typedef float mlp_f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 mlp_bf16x2 __attribute__((ext_vector_type(2)));
 constexpr int kStrideA = 336;
 constexpr int kStrideB = 272;
 #ifndef RT_MLP_INPLACE
@@ -101,6 +106,9 @@ __device__ __forceinline__ int swz(int row, int k, int stride) {
     return row * stride + (((k >> 3) ^ ((row >> 2) & 7)) << 3) + (k & 7);
 }
 constexpr int kStageStride = kDqnActions + 1;  // fp32 Q staging rows (in bufA)
+// bf16 Q staging (RT_MLP_EPI2, the renderer's QB forward): [72 cell pairs][kQPairStride rows]
+// dwords; 2 * 104 = 16 mod 64 banks, so a wave's pair-row writes hit 64 distinct banks
+constexpr int kQPairStride = kTileM <= 104 ? 104 : kTileM + 8;
 // the sampler's fixed sum order: kSampBlocks blocks of kSampCells cells (sample_from_q)
 constexpr int kSampBlocks = 4;
 constexpr int kSampCells = kDqnActions / kSampBlocks;  // 36 = 9 Philox draws
@@ -216,10 +224,14 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     for (int j = 0; j < NT; ++j)
         wrow[j] = W + ((size_t)min(wave + kMlpWaves * j, n_tiles - 1) * (K >> 5) * 64 + lane) * 8;
     f32x4 acc[MT][NT];
+    // (RT_MLP_EPI2 with K known: the first K step's MFMAs take C = 0 as an inline constant,
+    // no zeroing moves)
+    if (!(RT_MLP_EPI2 && KS > 0)) {
 #pragma unroll
-    for (int m = 0; m < MT; ++m)
+        for (int m = 0; m < MT; ++m)
 #pragma unroll
-        for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < NT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if constexpr (KS > 0) {
         // K known at compile time (the reference's 200-300-200 shape): the weight
         // fragments of steps k+1 .. k+R-1 and the activations of step k+1 are in flight
@@ -279,7 +291,9 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
                 if (RT_MLP_SKIP_PAD && j == NT - 1 && !last_valid) continue;
 #pragma unroll
                 for (int m = 0; m < MT; ++m)
-                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bw[ks % R][j], a[ks % AB][m], acc[m][j], 0, 0, 0);
+                    acc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                        bw[ks % R][j], a[ks % AB][m], (RT_MLP_EPI2 && ks == 0) ? f32x4{0.f, 0.f, 0.f, 0.f} : acc[m][j],
+                        0, 0, 0);
             }
 #if RT_MLP_PROLOGUE_GROUP
             if (ks + R - 1 < KS) __builtin_amdgcn_sched_group_barrier(0x020, NT, 0);  // VMEM reads
@@ -345,6 +359,33 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
 #pragma unroll
         for (int m = 0; m < MT; ++m) {
             const int row = m * 16 + r16;
+#if RT_MLP_EPI2
+            if (!LAST || out_stride != 0) {
+                // bias in packed adds (the same IEEE sums), then RNE to bf16 and the ReLU on the
+                // bf16 pairs as a signed 16-bit max with 0: RN is monotone with RN(0) = 0, so
+                // max(RN(v), 0) = RN(max(v, 0)) for every finite v (a negative bf16 is a
+                // negative int16; -0 becomes +0 as the fp32 ReLU gives)
+                const mlp_f32x2 s01 = mlp_f32x2{acc[m][j][0], acc[m][j][1]} + mlp_f32x2{bb[0], bb[1]};
+                const mlp_f32x2 s23 = mlp_f32x2{acc[m][j][2], acc[m][j][3]} + mlp_f32x2{bb[2], bb[3]};
+                typedef short mlp_i16x2 __attribute__((ext_vector_type(2)));
+                const mlp_i16x2 z = {0, 0};
+                mlp_i16x2 h01 = __builtin_bit_cast(mlp_i16x2, __builtin_convertvector(s01, mlp_bf16x2));
+                mlp_i16x2 h23 = __builtin_bit_cast(mlp_i16x2, __builtin_convertvector(s23, mlp_bf16x2));
+                h01 = h01 > z ? h01 : z;
+                h23 = h23 > z ? h23 : z;
+                if (LAST) {  // the renderer's bf16 Q: cell pairs staged action-major, [pair][row]
+                    uint32_t* const st2 = reinterpret_cast<uint32_t*>(out_lds);
+                    st2[(col >> 1) * out_stride + row] = __builtin_bit_cast(uint32_t, h01);
+                    st2[((col >> 1) + 1) * out_stride + row] = __builtin_bit_cast(uint32_t, h23);
+                    continue;
+                }
+                uint2 w;
+                w.x = __builtin_bit_cast(uint32_t, h01);
+                w.y = __builtin_bit_cast(uint32_t, h23);
+                *reinterpret_cast<uint2*>(out_lds + swz(row, col, out_stride)) = w;
+                continue;
+            }
+#endif
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -368,8 +409,6 @@ __device__ __forceinline__ void mlp_layer(const DqnNet& net, int L, const __bf16
     }
 }
 
-typedef float mlp_f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 mlp_bf16x2 __attribute__((ext_vector_type(2)));
 
 // The fused Q.cos sampler's per-ray inputs (k_dqn_mlp<MT, true>): the rays' pixel keys and
 // sample (ray id = slot * n_pix + pixel slot, as k_dqn_bounce), the Philox event and key.
@@ -441,13 +480,14 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
         mlp_layer<slots(14), false, MT, 10, true, RT_MLP_XPF, RT_MLP_XPF ? slots(9) : 0>(net, 2, bufA, kStrideA, bufA,
                                                                                       kStrideA, p2, p3);
         __syncthreads();
-        mlp_layer<slots(9), true, MT, 7, true, RT_MLP_XPF>(net, 3, bufA, kStrideA, bufA, 0, p3);
+        mlp_layer<slots(9), true, MT, 7, true, RT_MLP_XPF>(net, 3, bufA, kStrideA, bufA, (RT_MLP_EPI2 && QB) ? kQPairStride : 0,
+                                                          p3);
     } else {
         mlp_layer<slots(20), false, MT, 0, true>(net, 1, bufA, kStrideA, bufA, kStrideA);  // N <= 320
         __syncthreads();
         mlp_layer<slots(14), false, MT, 0, true>(net, 2, bufA, kStrideA, bufA, kStrideA);  // N <= 224
         __syncthreads();
-        mlp_layer<slots(9), true, MT, 0, true>(net, 3, bufA, kStrideA, bufA, 0);           // N = 144
+        mlp_layer<slots(9), true, MT, 0, true>(net, 3, bufA, kStrideA, bufA, (RT_MLP_EPI2 && QB) ? kQPairStride : 0);
     }
     (void)bufB;
 #else
@@ -581,6 +621,23 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
         // the renderer's Q in bf16 (RNE), cells 2j and 2j + 1 of a ray in one dword (low,
         // high): q2[j * ldq + ray], 16-B runs of four rays -- half the bytes of the fp32 tile
         uint32_t* const q2 = reinterpret_cast<uint32_t*>(q);
+#if RT_MLP_EPI2 && RT_MLP_INPLACE
+        static_assert(kRows <= kQPairStride && (kDqnActions / 2) * kQPairStride * 4 <= kRows * kStrideA * 2,
+                      "the bf16 Q staging fits bufA");
+        const uint32_t* const st2 = reinterpret_cast<const uint32_t*>(bufA);
+        for (int t = threadIdx.x; t < (kDqnActions / 2) * (kRows / 4); t += kMlpThreads) {
+            const int j = t / (kRows / 4), r = (t - j * (kRows / 4)) * 4;
+            const uint4 v = *reinterpret_cast<const uint4*>(st2 + j * kQPairStride + r);
+#if RT_MLP_NT_STORE
+            typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+            const u32x4v wv = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(wv, reinterpret_cast<u32x4v*>(q2 + (size_t)j * ldq + row0 + r));
+#else
+            *reinterpret_cast<uint4*>(q2 + (size_t)j * ldq + row0 + r) = v;
+#endif
+        }
+        if (true) return;
+#endif
         for (int t = threadIdx.x; t < (kDqnActions / 2) * (kRows / 4); t += kMlpThreads) {
             const int j = t / (kRows / 4), r = (t - j * (kRows / 4)) * 4;
             const float* sp = stage + r * kStageStride + 2 * j;
