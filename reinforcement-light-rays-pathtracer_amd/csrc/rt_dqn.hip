@@ -423,6 +423,14 @@ __device__ __forceinline__ float chiu_cos_cell(int a, float r1, float r2) {
     const int gyi = a - gxi * kDqnGrid;
     return chiu_cos((float)gxi + r1, (float)gyi + r2);  // cos of the jittered cell direction
 }
+// the same for the cell's two 16-bit jitters in one Philox word (u16lo / u16hi): the grid
+// coordinate cell + k 2^-16 as one fma -- both terms and their sum exact, so the same
+// float as u16lo's product then the add (the build does not contract them itself)
+__device__ __forceinline__ float chiu_cos_cell_w(int a, uint32_t w) {
+    const int gxi = a / kDqnGrid;
+    const int gyi = a - gxi * kDqnGrid;
+    return chiu_cos(fmaf((float)(w & 0xffffu), 0x1p-16f, (float)gxi), fmaf((float)(w >> 16), 0x1p-16f, (float)gyi));
+}
 
 // One workgroup = MT*16 rays (LDS: MT = 6 in place -> 66 KB, two workgroups per CU).
 // FUSED: instead of writing Q out, the workgroup runs importance_sample_direction's
@@ -539,7 +547,7 @@ __global__ __launch_bounds__(kMlpThreads, RT_MLP_MIN_WAVES) void k_dqn_mlp(const
                 philox_from(ph, 1u + (uint32_t)(a >> 2), o);
 #pragma unroll
                 for (int h = 0; h < 4; ++h) {
-                    const float qc = srow[a + h] * chiu_cos_cell(a + h, u16lo(o[h]), u16hi(o[h]));
+                    const float qc = srow[a + h] * chiu_cos_cell_w(a + h, o[h]);
                     srow[a + h] = qc;
                     b = b + qc;
                 }
@@ -750,7 +758,7 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
             uint32_t r[4];
             philox_from(ph, 1u + (uint32_t)((g + u4) >> 2), r);
 #pragma unroll
-            for (int h = 0; h < 4; ++h) qv[u4 + h] = qv[u4 + h] * chiu_cos_cell(g + u4 + h, u16lo(r[h]), u16hi(r[h]));
+            for (int h = 0; h < 4; ++h) qv[u4 + h] = qv[u4 + h] * chiu_cos_cell_w(g + u4 + h, r[h]);
         }
     };
     float bs[kSampBlocks];
