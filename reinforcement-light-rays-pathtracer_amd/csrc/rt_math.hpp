@@ -109,13 +109,11 @@ RT_HD f3 cross(f3 x, f3 y) {
 #define RT_XOR3 1
 #endif
 // a ^ b ^ c: one v_bitop3_b32 on gfx950 (the compiler emits two v_xor_b32 for it)
-RT_HD uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__) && RT_XOR3
-    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#define RT_XOR3F(a, b, c) __builtin_amdgcn_bitop3_b32((a), (b), (c), 0x96)
 #else
-    return a ^ b ^ c;
+#define RT_XOR3F(a, b, c) ((a) ^ (b) ^ (c))
 #endif
-}
 
 // Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11).  Counter
 // (pixel, sample, event, 0), key (seed_lo, seed_hi): DESIGN.md §3.
@@ -127,8 +125,8 @@ RT_HD void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
         uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
         uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
         uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
-        uint32_t n0 = xor3(hi1, c1, k0);
-        uint32_t n2 = xor3(hi0, c3, k1);
+        uint32_t n0 = RT_XOR3F(hi1, c1, k0);
+        uint32_t n2 = RT_XOR3F(hi0, c3, k1);
         c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
         k0 += 0x9E3779B9u;
         k1 += 0xBB67AE85u;
@@ -149,7 +147,7 @@ RT_HD PhiloxShared philox_shared(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t
     PhiloxShared s;
     const uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
-    s.r1_n0 = xor3((uint32_t)(p1 >> 32), c1, k0);
+    s.r1_n0 = RT_XOR3F((uint32_t)(p1 >> 32), c1, k0);
     s.r1_lo1 = (uint32_t)p1;
     s.r1_x = (uint32_t)(p0 >> 32) ^ k1;
     s.r1_lo0 = (uint32_t)p0;
@@ -165,9 +163,9 @@ RT_HD void philox_from(const PhiloxShared& s, uint32_t c3, uint32_t out[4]) {
     // round 2: (n0, lo1, n2, lo0) of round 1 with n2 = r1_x ^ c3
     const uint32_t n2 = s.r1_x ^ c3;
     const uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)n2;
-    uint32_t c0 = xor3((uint32_t)(p1 >> 32), s.r1_lo1, k0);
+    uint32_t c0 = RT_XOR3F((uint32_t)(p1 >> 32), s.r1_lo1, k0);
     uint32_t c1 = (uint32_t)p1;
-    uint32_t c2 = xor3(s.r2_hi0, s.r1_lo0, k1);
+    uint32_t c2 = RT_XOR3F(s.r2_hi0, s.r1_lo0, k1);
     uint32_t c3w = s.r2_lo0;
     k0 += 0x9E3779B9u;
     k1 += 0xBB67AE85u;
@@ -175,8 +173,8 @@ RT_HD void philox_from(const PhiloxShared& s, uint32_t c3, uint32_t out[4]) {
     for (int r = 2; r < 10; ++r) {
         const uint64_t q0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
         const uint64_t q1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
-        const uint32_t n0 = xor3((uint32_t)(q1 >> 32), c1, k0);
-        const uint32_t m2 = xor3((uint32_t)(q0 >> 32), c3w, k1);
+        const uint32_t n0 = RT_XOR3F((uint32_t)(q1 >> 32), c1, k0);
+        const uint32_t m2 = RT_XOR3F((uint32_t)(q0 >> 32), c3w, k1);
         c0 = n0;
         c1 = (uint32_t)q1;
         c2 = m2;

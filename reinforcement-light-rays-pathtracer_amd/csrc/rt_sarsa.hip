@@ -17,6 +17,12 @@
 // seed: bit-identical Q-table and image on any GPU count, and against oracle/.
 #include <float.h>
 
+// Philox's xor3 as v_bitop3 (rt_math.hpp RT_XOR3) pays in the DQN sampler (47 blocks a ray: 401.5 ->
+// 391.5 ms, profiles/r4ar); here (0.6% on Cornell, 0.3% on SARSA) the two-xor form is kept, the
+// code the committed rocprofv3 profiles measured
+#ifndef RT_XOR3
+#define RT_XOR3 0
+#endif
 #include "rt_trace.hpp"
 
 // A/B knobs (timing / statistics builds only; all but SCAN_STATS change results):
