@@ -1529,7 +1529,11 @@ static void td_add(orc_sarsa *m, int rv, int sector, float target) {
 }
 
 /* path_trace_reinforcement_iterative with the frame-synchronous TD */
-static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t smp, v3 o, v3 d, uint64_t *casts) {
+/* *null_ray (may be NULL): set when the path ends by tracing the zero direction of a failed
+ * CDF search, whose radiance is NaN in the reference ((BRDF * 0) / pdf 0,
+ * reinforcement_path_tracing.cu:101-108): it is not a zero-contribution path there */
+static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t smp, v3 o, v3 d, uint64_t *casts,
+                      int *null_ray) {
     orc_scene sc;
     sc.n_surf = m->n_surf; sc.n_light = m->n_light; sc.tri = m->tri; sc.albedo = m->albedo;
     sc.emission = m->emission; sc.light_group = m->light_group; sc.normal = m->normal;
@@ -1588,6 +1592,7 @@ static v3 sarsa_trace(orc_sarsa *m, const orc_params *p, uint32_t pix, uint32_t 
             m->stat_cdf += 1u;
             if (i + 1 >= p->max_bounces) return mk(0.0f, 0.0f, 0.0f);
             (*casts)++; /* the zero direction is traced and misses */
+            if (null_ray) *null_ray = 1;
             return mk(tp.x * p->env_light, tp.y * p->env_light, tp.z * p->env_light);
         }
         if (cur_rv >= 0 && !m->sample_max) {
@@ -1695,7 +1700,7 @@ ORC_API int orc_sarsa_td_rect(orc_sarsa *m, const orc_camera *cam, const orc_par
                 draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
                 v3 o, d;
                 camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
-                (void)sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
+                (void)sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts, NULL);
             }
             total += casts;
         }
@@ -1738,11 +1743,13 @@ static uint64_t sarsa_frame_rect(orc_sarsa *m, const orc_camera *cam, const orc_
                     draw2(p->seed, pix, base + (uint32_t)s, 0u, &r1, &r2);
                     v3 o, d;
                     camera_ray(cam, &pg, cy, sy, cx, sx, px, py, r1, r2, &o, &d);
-                    v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts);
+                    int null_ray = 0;
+                    v3 L = sarsa_trace(m, p, pix, base + (uint32_t)s, o, d, &casts, &null_ray);
                     part.x = part.x + L.x; part.y = part.y + L.y; part.z = part.z + L.z;
                     /* path_trace_reinforcement (reinforcement_path_tracing.cu:28-41): a
-                     * zero-contribution path; its path length is its ray casts */
-                    if ((L.x + L.y + L.z) / 3.f < 0.0001f) zero++;
+                     * zero-contribution path (a NaN one, null_ray, is not); its path length is
+                     * its ray casts */
+                    if (!null_ray && (L.x + L.y + L.z) / 3.f < 0.0001f) zero++;
                 }
                 if (c == 0) acc = part;
                 else { acc.x = acc.x + part.x; acc.y = acc.y + part.y; acc.z = acc.z + part.z; }

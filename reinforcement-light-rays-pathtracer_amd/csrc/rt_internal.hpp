@@ -382,6 +382,7 @@ constexpr int kKdStack = RT_KD_STACK;  // traversal stack entries per lane (LDS)
 
 hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);
+bool sarsa_prof_compiled();  // rt_sarsa.hip was built with RT_SARSA_PROF=1 (per-phase cycle counters)
 hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream);  // CDF + argmax from Q
 hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float* nrm, int n, int32_t* out,
                                 hipStream_t stream);

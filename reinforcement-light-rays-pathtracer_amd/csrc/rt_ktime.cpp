@@ -65,6 +65,9 @@ KernelTimer::KernelTimer(int k, hipStream_t s) : stream(s) {
         }
     }
     if (a == nullptr && (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess)) {
+        // the first event may exist when the second failed: do not leak it
+        if (a != nullptr) (void)hipEventDestroy(a);
+        a = b = nullptr;
         std::lock_guard<std::mutex> lk(g_mu);
         ++g_errors;
         return;

@@ -17,12 +17,6 @@
 // seed: bit-identical Q-table and image on any GPU count, and against oracle/.
 #include <float.h>
 
-// Philox's xor3 as v_bitop3 (rt_math.hpp RT_XOR3) pays in the DQN sampler (47 blocks a ray: 401.5 ->
-// 391.5 ms, profiles/r4ar); here (0.6% on Cornell, 0.3% on SARSA) the two-xor form is kept, the
-// code the committed rocprofv3 profiles measured
-#ifndef RT_XOR3
-#define RT_XOR3 0
-#endif
 #include "rt_trace.hpp"
 
 // A/B knobs (timing / statistics builds only; all but SCAN_STATS change results):
@@ -491,6 +485,8 @@ __device__ void sarsa_sample_max(const SarsaMap& m, int rv, const VolPre& vp, fl
         const float* q = m.Q + (size_t)rv * kSarsaSectors;
         mi = 0;
         float mq = live_load(q);
+        // from k = 0, as the reference's scan (radiance_volume.cu:251-257 reads grid[0] twice):
+        // in this racy mode the second read of q[0] may see another lane's update
         for (int k = 0; k < kSarsaSectors; ++k) {
             const float v = live_load(q + k);
             if (mq < v) {
@@ -549,6 +545,7 @@ struct SarsaPath {
     f3 o, d, tp;
     int depth, cur_rv, cur_sector;
     float cur_brdf;
+    bool null_ray;  // set by sarsa_step: the path ended by tracing the zero direction
 };
 
 // One cast of path_trace_reinforcement_iterative after its closest hit h and the volume
@@ -617,6 +614,9 @@ __device__ __forceinline__ bool sarsa_step(const RenderLaunch& a, const SarsaMap
             if (P.depth + 1 < a.max_bounces) {
                 ++n_casts;
                 L = make3(P.tp.x * a.env_light, P.tp.y * a.env_light, P.tp.z * a.env_light);
+                // the reference's throughput is (BRDF * 0) / pdf 0 = NaN here: its radiance is
+                // NaN, which its zero-contribution test (NaN < threshold) does not count
+                P.null_ray = true;
             }
         } else {
             const float4 brdf = shade[h.tri * kShadeF4 + 3];
@@ -714,7 +714,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
         else if (rv == kNeedWalk)
             rv = sarsa_nearest(m, pos, nrm, st);
         if (!active) continue;
-        SarsaPath P{o, d, tp, depth, cur_rv, cur_sector, cur_brdf};
+        SarsaPath P{o, d, tp, depth, cur_rv, cur_sector, cur_brdf, false};
         f3 L;
         const bool terminal = sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
         o = P.o;
@@ -729,7 +729,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
             // a zero-contribution light path (reinforcement_path_tracing.cu:36-40)
-            n_zero += ((L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
+            n_zero += (!P.null_ray && (L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
             ++s;
             depth = 0;
             cur_rv = -1;
@@ -807,7 +807,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
     long long item = 0;
     int s = 0, s_end = 0, px = 0, py = 0;
     uint32_t pix = 0;
-    SarsaPath P{cam, make3(0.f, 0.f, 1.f), make3(1.f, 1.f, 1.f), 0, -1, -1, 0.0f};
+    SarsaPath P{cam, make3(0.f, 0.f, 1.f), make3(1.f, 1.f, 1.f), 0, -1, -1, 0.0f, false};
     f3 acc = make3(0.f, 0.f, 0.f);
     unsigned n_casts = 0, n_zero = 0, casts0 = 0;
 #if RT_SARSA_PROF
@@ -822,6 +822,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
         P.depth = 0;
         P.cur_rv = -1;
         P.cur_sector = -1;
+        P.null_ray = false;
     };
     for (;;) {
         if (!exhausted) {
@@ -935,7 +936,7 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) 
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
             acc.z = acc.z + L.z;
-            n_zero += ((L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
+            n_zero += (!P.null_ray && (L.x + L.y + L.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
             ++s;
             if (s < s_end) {
                 camera();
@@ -1176,6 +1177,8 @@ hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream) {
     hipLaunchKernelGGL(k_sarsa_rebuild, dim3((unsigned)((m.n_vol + 255) / 256)), dim3(256), 0, stream, m);
     return hipGetLastError();
 }
+
+bool sarsa_prof_compiled() { return RT_SARSA_PROF != 0; }
 
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream) {
     if (m.n_vol <= 0) return hipSuccess;

@@ -431,8 +431,15 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
     a.csum = sa->d_csum;
     a.work = sa->d_work;
     RT_HIPE(hipMemsetAsync(sa->m.stats, 0, 2 * sizeof(unsigned long long), stream));
-    // RT_SARSA_PROF (with an RT_SARSA_PROF=1 kernel build): the render's per-phase cycles to stderr
-    static const bool prof = getenv("RT_SARSA_PROF") != nullptr;
+    // RT_SARSA_PROF (with an RT_SARSA_PROF=1 kernel build): the render's per-phase cycles to stderr.
+    // On a default build the counters are never written: warn once, and do not synchronise.
+    static const bool prof_env = getenv("RT_SARSA_PROF") != nullptr;
+    static const bool prof = prof_env && rt::sarsa_prof_compiled();
+    static bool warned = false;
+    if (prof_env && !prof && !warned) {
+        warned = true;
+        fprintf(stderr, "rtmi: RT_SARSA_PROF is set, but rt_sarsa.hip was built without -DRT_SARSA_PROF=1: ignored\n");
+    }
     if (prof && !sa->m.prof) RT_HIPE(hipMalloc(&sa->m.prof, 8 * sizeof(unsigned long long)));
     if (prof) RT_HIPE(hipMemsetAsync(sa->m.prof, 0, 8 * sizeof(unsigned long long), stream));
     RT_HIPE(rt::launch_sarsa_render(a, sa->m, stream));

@@ -80,7 +80,11 @@ def cornell_geometry(variant: int = _lib.RT_PRESET_CPU) -> Geometry:
     em = np.zeros((nl.value, 3), np.float32)
     grp = np.zeros((nl.value,), np.int32)
     check(L.rt_cornell_geometry(variant, _fp(tri), _fp(alb), _fp(lv), _fp(em), _ip(grp)))
-    return Geometry(tri, alb, lv, em, grp)
+    # the GPU engine's Scene::vertices (the network's input, 38 x 9 = 342 floats): each
+    # surface's v0, v1, v2 as stored, then each light's (GPU/scenes/cornell_box_scene.cu:190-199,
+    # 231-240); the CPU engine has no network
+    nnv = np.concatenate([tri, lv], axis=0).ravel().copy() if variant == _lib.RT_PRESET_GPU else None
+    return Geometry(tri, alb, lv, em, grp, nnv)
 
 
 def obj_geometry(path: str, kind: str | int = "generic") -> Geometry:

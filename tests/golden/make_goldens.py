@@ -14,6 +14,9 @@ Fixtures (all data, no reference source):
                          accept tests, as disassembled
   cornell_ref_stats.json block means of Images/cornell/*.png (statistical
                          reference renders of the GPU engine, 720x720)
+  scenes_ref_stats.json  block means of the OBJ scenes' reference renders, and of the
+                         pretrained renderer's NN renders and the SARSA renders
+  nn_ref_stats.json      the Neural-Q training logs of the shipped networks
   sarsa_ref_stats.json   the reference's Expected-SARSA training statistics
                          (Radiance_Map_Data/sarsa_*.txt, written per frame by
                          GPU/main.cu:321-339: average path length, 0.0,
@@ -92,6 +95,7 @@ def main(ref):
     except ImportError:
         pass
     scene_image_stats(ref)
+    nn_training_stats(ref)
 
 
 def scene_image_stats(ref):
@@ -108,7 +112,18 @@ def scene_image_stats(ref):
     # its reference.png was made with other settings)
     files = [(s, f"Images/{s}/reference.png") for s in ("door_room", "archway", "complex_light")]
     files += [("door_room_default_128spp", "Images/door_room/default_128spp_50avg.png"),
-              ("door_room_sarsa_128spp", "Images/door_room/sarsa_128_spp_avg_pl_5_max_pl_80.png")]
+              ("door_room_sarsa_128spp", "Images/door_room/sarsa_128_spp_avg_pl_5_max_pl_80.png"),
+              # the pretrained renderer's own renders (PretrainedPathtracer, 128 spp) with the
+              # networks Radiance_Map_Data/door_room_12_12.model and cornell_12_12.model
+              ("door_room_nn_128spp", "Images/door_room/nn_128spp_32avg.png"),
+              ("cornell_nn_128spp", "Images/cornell/nn_128spp_avg.png"),
+              ("cornell_default_128spp", "Images/cornell/default_128spp_6avg.png"),
+              # Expected-SARSA renders of the other scenes (128 spp)
+              ("cornell_sarsa_128spp", "Images/cornell/sarsa_128spp_3avg_44Mb.png"),
+              ("archway_sarsa_128spp", "Images/archway/sarsa_128spp_3avg_272Mb.png"),
+              ("complex_light_sarsa_128spp", "Images/complex_light/sarsa_128spp_5avg_300Mb.png"),
+              ("archway_default_128spp", "Images/archway/default_128spp_60avg.png"),
+              ("complex_light_default_128spp", "Images/complex_light/default_128spp_58avg.png")]
     for key, rel in files:
         p = os.path.join(ref, rel)
         if not os.path.exists(p):
@@ -120,6 +135,26 @@ def scene_image_stats(ref):
         stats[key] = {"file": rel, "shape": [h, w], "block": b, "means": blocks.round(4).tolist()}
     with open(os.path.join(HERE, "scenes_ref_stats.json"), "w") as f:
         json.dump(stats, f)
+
+
+def nn_training_stats(ref):
+    """nn_ref_stats.json: the Neural-Q training logs that produced the shipped networks
+    (Radiance_Map_Data/*_stats*.txt / cornell_no_decay.txt, one line per training frame written by
+    NeuralQPathtracer: average path length, loss, zero-contribution paths): all rows and the mean
+    of the last 10."""
+    out = {}
+    for key, fname, model in (("door_room_12_12", "door_room_12_12_stats.txt", "door_room_12_12.model"),
+                              ("cornell_12_12", "cornell_stats_12_12.txt", "cornell_12_12.model"),
+                              ("cornell_no_decay", "cornell_no_decay.txt", "cornell_no_decay.model")):
+        rows = [[float(x) for x in line.split()] for line in open(os.path.join(ref, "Radiance_Map_Data", fname))
+                if line.strip()]
+        tail = rows[-10:]
+        out[key] = {"file": "Radiance_Map_Data/" + fname, "model": "Radiance_Map_Data/" + model,
+                    "avg_path_length": [r[0] for r in rows], "loss": [r[1] for r in rows],
+                    "zero_contribution_paths": [r[2] for r in rows],
+                    "last10_mean_path_length": round(sum(r[0] for r in tail) / len(tail), 4)}
+    with open(os.path.join(HERE, "nn_ref_stats.json"), "w") as f:
+        json.dump(out, f)
 
 
 if __name__ == "__main__":

@@ -591,3 +591,64 @@ def test_gpu_weight_stationary_render_equals_streaming(rtmi_mod, gpu_ctx):
         img_w, casts_w = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p, rect)
         net.set_mlp(net.MLP_STREAM)
     assert casts_s == casts_w and np.array_equal(img_s.view(np.uint32), img_w.view(np.uint32))
+
+
+# ------------------------------------------ reference NN renders (GPU) ----------
+
+def _block_means8(rtmi_mod, img):
+    rgb8 = rtmi_mod.metrics.argb_to_rgb8(rtmi_mod.pack_argb(img)).astype(np.float64)
+    return rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3))
+
+
+def _transposed(W):
+    """each weight matrix read in the other order: its column-major bytes taken row-major (the
+    DyNet order error the gate must see)"""
+    return [np.ascontiguousarray(w.ravel(order="F").reshape(w.shape)) for w in W]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,model,key,casts_band", [
+    # nn_128spp_32avg.png: "32avg" is the pretrained renderer's logged average path length,
+    # int(sum of the last sample's ray_bounces / pixels), ray_bounces = casts - 1
+    # (pre_trained_pathtracer.cu:366-375, :409, :453-464)
+    ("door_room", "door_room_12_12.model", "door_room_nn_128spp", (32.0, 34.0)),
+    ("cornell", "cornell_12_12.model", "cornell_nn_128spp", None),
+])
+def test_gpu_dqn_render_matches_reference_nn_render(rtmi_mod, gpu_ctx, scene, model, key, casts_band):
+    """The pretrained renderer (PretrainedPathtracer::render_frame, pre_trained_pathtracer.cu:188-491)
+    with the reference's own trained networks, against the renders the reference made with them
+    (Images/door_room/nn_128spp_32avg.png, Images/cornell/nn_128spp_avg.png; 45x45 block means of
+    the 8-bit images in tests/golden/scenes_ref_stats.json), at the reference's 720x720, 128 spp,
+    GPU-engine preset.  A learned sampler gives zero probability to cells whose Q is 0, so its
+    render is biased in a pattern of its own: the NN renders differ from the default renders of
+    the same scenes by 1.26 (door room) and 1.82 (Cornell) of 255 in block mean, and ours
+    reproduces the reference's NN render to 0.36 / 0.36 (profiles/r5a_nn_pin.json).  That pins the
+    DyNet reader, the weight order, the layer-0 fold, the bf16 forward and the Q.cos sampler end
+    to end against the reference's output.  Negative control: the same parameters read in the
+    wrong matrix order render at 31 / 23 of 255 from it, with the door room's paths back at the
+    uniform sampler's 51 casts."""
+    import json
+    from conftest import GOLDEN
+    ref = np.array(json.load(open(os.path.join(GOLDEN, "scenes_ref_stats.json")))[key]["means"])
+    if scene == "cornell":
+        g = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    else:
+        g = rtmi_mod.obj_geometry(os.path.join(MODELS, f"{scene}.obj"), scene)
+    W, b = rtmi_mod.dqn.split_layers(rtmi_mod.dqn.read_dynet(os.path.join(MODELS, model)))
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=128)
+    res = {}
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        for kind, WW in (("trained", W), ("transposed", _transposed(W))):
+            with rtmi_mod.dqn.Dqn(gpu_ctx, g.nn_vertices, WW, b) as net:
+                img, casts = rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p)
+            d = np.abs(_block_means8(rtmi_mod, img) - ref)
+            res[kind] = (float(d.mean()), float(d.max()), casts / (720 * 720 * 128))
+    mean_d, max_d, cps = res["trained"]
+    assert mean_d <= 0.7 and max_d <= 4.0, res
+    if casts_band is not None:
+        assert casts_band[0] <= cps <= casts_band[1], res  # measured 33.78: 32.78 bounces
+    tmean, _, tcps = res["transposed"]
+    assert tmean >= 10.0, res
+    if casts_band is not None:
+        assert tcps > casts_band[1] + 10.0, res

@@ -678,3 +678,96 @@ def test_gpu_in_frame_mode_refuses_td_exchange(rtmi_mod, gpu_ctx):
             assert rf.td_device()[2] == rf.n_volumes * 144
         finally:
             rf.close()
+
+
+# The reference's training runs, recovered from their own logs (tests/golden/sarsa_ref_stats.json,
+# written per frame by GPU/main.cu:321-339): 720 x 720, ONE sample per pixel (the zero-contribution
+# count is a count of samples: 463,054 of 518,400 in Cornell's frame 0), GPU-engine preset.  Per
+# scene, the TD rule whose trajectory the logs follow (profiles/r5b_sarsa_pin.json, 4 seeds, both
+# rules): archway and complex_light_room follow the reference's own in-frame rule (zero counts
+# within 0.1-3.5 % over frames 1-7), Cornell the frame-synchronous one (within 0.6 %; its in-frame
+# runs sit 4-13 % above: the race outcome depends on the reference GPU's concurrency, which a
+# 24,000-volume box on 256 CUs does not reproduce).  door_room: frame 0 only -- from frame 1 the
+# logged run learns faster than either rule with every door-room variant of object_importer.cu
+# (DESIGN.md §6), so its settings are not recoverable from the repository.
+TRAJECTORY = {"cornell": "frame", "archway": "inframe", "complex_light_room": "inframe", "door_room": None}  # None: frame 0 only
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene", SCENES)
+def test_gpu_learning_trajectory_matches_reference_logs(rtmi_mod, gpu_ctx, scene):
+    """Frames 0-7 of Expected SARSA against the reference's logged statistics: the average path
+    length it logs (floor over pixels of the per-pixel floor, ±1 for a floor near an integer) and
+    the zero-contribution samples (a path whose radiance is NaN in the reference -- the zero
+    direction of a failed CDF search, (BRDF * 0) / pdf 0 -- is not one: NaN < threshold is false).
+    Frame 0 (the initial CDF: both rules alike) within 1 %, frames 1-7 within 5 %."""
+    ref = json.load(open(os.path.join(GOLDEN, "sarsa_ref_stats.json")))[scene]
+    mode = TRAJECTORY[scene]
+    frames = 8 if mode is not None else 1
+    S = rtmi_mod.sarsa
+    W = H = 720
+    g = geometry(rtmi_mod, scene)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        rm = S.RadianceMap(gpu_ctx, sc, 1984)
+        try:
+            if mode == "inframe":
+                rm.set_td_mode(S.TD_INFRAME)
+            p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=W, height=H, spp=1, spp_split=1)
+            cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+            logged, zero = [], []
+            for _ in range(frames):
+                rm.render(cam, p, 1)
+                paths, z = rm.frame_stats()
+                logged.append(paths // (W * H))
+                zero.append(z)
+        finally:
+            rm.close()
+    rl = [int(x) for x in ref["avg_path_length"][:frames]]
+    rz = ref["zero_contribution_paths"][:frames]
+    assert logged[0] == rl[0], (logged, rl)
+    assert abs(zero[0] - rz[0]) <= 0.01 * rz[0], (zero, rz)
+    for f in range(1, frames):
+        assert abs(logged[f] - rl[f]) <= 1, (f, logged, rl)
+        assert abs(zero[f] - rz[f]) <= 0.05 * rz[f], (f, zero, rz)
+    if frames > 1:
+        assert logged[-1] < logged[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,frames,key,name_len", [
+    ("cornell", 100, "cornell_sarsa_128spp", 3),            # sarsa_128spp_3avg_44Mb.png
+    ("complex_light_room", 142, "complex_light_sarsa_128spp", 5),  # sarsa_128spp_5avg_300Mb.png
+    ("door_room", 100, "door_room_sarsa_128spp", None),     # sarsa_128_spp_avg_pl_5_max_pl_80.png
+])
+def test_gpu_sarsa_render_matches_reference_sarsa_render(rtmi_mod, gpu_ctx, scene, frames, key, name_len):
+    """The reference's Expected-SARSA renders (Images/<scene>/sarsa_128spp_*.png, 720x720, 128 spp,
+    block means in tests/golden/scenes_ref_stats.json) against ours after the logged number of
+    1-spp training frames (sarsa_ref_stats.json: 100 rows, complex_light_room 142) in the scene's
+    TD rule (TRAJECTORY; door_room: the frame-synchronous one).  Measured (profiles/r5c_sarsa_final.json):
+    block mean |d| 0.42 / 0.41 / 0.91 of 255; the logged path length of the 128-spp frame 3 and 5 where
+    the file names give 3avg and 5avg.  The archway's SARSA render is not a target: it is 6% darker
+    than the reference's own default render of the same scene (109.7 vs 116.3 of 255), which an
+    unbiased importance sampler cannot be, so it was made with settings the repository does not
+    record."""
+    ref = np.array(json.load(open(os.path.join(GOLDEN, "scenes_ref_stats.json")))[key]["means"])
+    S = rtmi_mod.sarsa
+    g = geometry(rtmi_mod, scene)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        rm = S.RadianceMap(gpu_ctx, sc, 1984)
+        try:
+            if TRAJECTORY[scene] == "inframe":
+                rm.set_td_mode(S.TD_INFRAME)
+            p1 = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=1, spp_split=1)
+            for _ in range(frames):
+                rm.render(cam, p1, 1)
+            p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=128, spp_split=8)
+            img, _ = rm.render(cam, p, 1)
+            paths, _ = rm.frame_stats()
+        finally:
+            rm.close()
+    rgb8 = rtmi_mod.metrics.argb_to_rgb8(rtmi_mod.pack_argb(img)).astype(np.float64)
+    d = np.abs(rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3)) - ref)
+    assert d.mean() <= 1.2 and d.max() <= 12.0, (d.mean(), d.max())
+    if name_len is not None:
+        assert abs(paths // (720 * 720) - name_len) <= 1, paths // (720 * 720)
