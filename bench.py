@@ -254,10 +254,11 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
     * VALU-bound kernels (k_render_ps, k_render, k_sarsa_render): frac = VALU
       wave-instructions / (time x 1024 SIMDs x one wave-instruction per 2 cycles at 2.4 GHz).
       Their triangle records are scalar-cache resident; HBM traffic is the frame (profile).
-    * The DQN forward k_dqn_mlp (a dense contraction): frac = the reference's algorithmic
-      flops (2 sum(in x out) per ray per NN bounce; rays = the frame's
-      bounce casts, one forward each) / time / the 2.5 PF dense bf16 peak; the executed bf16
-      MFMA flops and the matrix pipe's busy fraction beside it.
+    * The DQN forward k_dqn_mlp (a dense contraction): frac = the bf16 MFMA flops the kernel
+      executes (SQ_INSTS_VALU_MFMA_BF16 x 16384 per v_mfma_f32_16x16x32_bf16, from the profile)
+      / time / the 2.5 PF dense bf16 peak, the matrix pipe's busy fraction beside it; the
+      reference's algorithmic flops (2 sum(in x out) per ray per NN bounce, SURVEY.md §8(d), with
+      the 918-wide layer 0 the kernel folds to a 3-wide affine map) as a named extra.
     Informational for the scan kernels: the reference's brute-force flops (71 per
     ray-triangle test) per second and the north star's HBM-algorithmic ratio (36 B per
     triangle per cast as if streamed: not a bound on these kernels)."""
@@ -341,10 +342,13 @@ def roofline(args, geom, params, casts_per_frame: float, kt: dict):
         dims = [n_in, 200, 300, 200, 144]
         flop_ray = 2 * sum(dims[i] * dims[i + 1] for i in range(4))
         rows = casts_per_frame - params.width * params.height * params.spp  # bounce casts = forwards
-        line["algorithmic_flops_per_ray"] = flop_ray
+        line["reference_flops_per_ray"] = flop_ray
         line["forwards_per_step"] = int(rows)
-        line["achieved"] = round(rows * flop_ray / t / 1e12, 1)
-        line["frac"] = round(line["achieved"] / MFMA_BF16_PEAK_TFLOPS, 4)
+        line["reference_algorithmic_tflops"] = round(rows * flop_ray / t / 1e12, 1)
+        line["reference_algorithmic_frac"] = round(line["reference_algorithmic_tflops"] / MFMA_BF16_PEAK_TFLOPS, 4)
+        # the roofline proper: what the matrix cores executed (None without a matching profile)
+        line["achieved"] = line.get("executed_bf16_tflops")
+        line["frac"] = line.get("executed_frac")
     else:
         if line.get("hbm_frac") is not None and line["frac"] is not None and line["hbm_frac"] > line["frac"]:
             # more of the HBM roof than of the VALU issue roof is in use: HBM bounds it
@@ -391,12 +395,13 @@ def progress(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds):
+def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds, q_state=None, frame_index=0):
     """The CPU restatement (oracle/, OpenMP over rows) on a bounded sample of a learned-sampler
     frame, best of 3 ("for configs 4-5, CPU time may be measured on a reduced
     SPP"; a sample's cost does not depend on the frame's spp).
-    sarsa: rows of frame 0 of the 512^2 door_room frame (the restatement's Expected SARSA: the
-      KD search, the CDF sampling, the TD accumulation), 16 spp per pixel;
+    sarsa: rows of the 512^2 door_room frame (the restatement's Expected SARSA: the KD search,
+      the CDF sampling, the TD accumulation), 16 spp per pixel, from the Q-table the GPU map
+      held at the first timed frame (q_state: the same frame index as the GPU's timed frames);
     dqn: a 64^2 window at the frame's centre with the bf16-emulating forward of the same
       synthetic weights at every bounce (oracle.render_dqn), spp from the time budget."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -408,6 +413,8 @@ def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds):
     W, H = params.width, params.height
     if sampler == "sarsa":
         m = oracle.Sarsa(geom, int(params.seed))
+        if q_state is not None:
+            m.load_q(q_state)
         sp = rtmi.default_params(params.preset, width=W, height=H, spp=16, spp_split=1)
         op = oracle.params_from(sp)
         rows = max(16, threads)
@@ -417,7 +424,9 @@ def cpu_baseline_learned(sampler, geom, params, cam_pos, seconds):
         rows = int(max(rows, min(H, seconds * rate / max(casts / rows, 1.0))))
         rect = (0, max(0, H // 2 - rows // 2), W, rows)
         run = lambda: m.render_rect(ocam, op, rect)  # noqa: E731
-        what = (f"rows {rect[1]}..{rect[1] + rows - 1} of frame 0 of the {W}x{H} Expected-SARSA frame at 16 spp "
+        state = (f"frame {frame_index} (the Q-table of the GPU map at the first timed frame, loaded into the "
+                 f"restatement)" if q_state is not None else "frame 0")
+        what = (f"rows {rect[1]}..{rect[1] + rows - 1} of {state} of the {W}x{H} Expected-SARSA frame at 16 spp "
                 f"per pixel (the frame's own spp {params.spp}: per-sample cost is independent of it)")
     else:
         Ws, bs = rtmi.dqn.synthetic_weights(geom.nn_vertices.size)
@@ -605,6 +614,9 @@ def main():
     for i in range(args.warmup):
         pipe.gather_frame(pipe.render_frame(i))
     pipe.drain()
+    q_state = None
+    if sampler == "sarsa" and rank == 0 and args.cpu_seconds > 0 and world == 1:
+        q_state = rmap.read()[0]  # (before the timed region) the CPU baseline's starting Q-table
     if rank == 0:
         progress(f"{args.workload}: {args.warmup} warmup frame(s) done, timing {args.steps}")
     torch.cuda.synchronize()
@@ -675,6 +687,9 @@ def main():
             "frame_ms": round(frame_ms, 4),
             "roofline": roofline(args, geom, params, rank_casts / args.steps, kt),
         }
+        if sampler == "sarsa":  # a learning run: which of its frames the line times
+            line["config"]["frames_warmup"] = [0, args.warmup - 1] if args.warmup else []
+            line["config"]["frames_timed"] = [args.warmup, args.warmup + args.steps - 1]
         if sampler == "uniform" and not args.no_parity and params.width % TILE == 0 and params.height % TILE == 0:
             line["parity"] = parity_tiles(ctx, scene, geom, params, cam, cam_pos, image)
         if args.cpu_seconds > 0 and world == 1:  # the CPU baseline is an N=1 figure
@@ -683,7 +698,8 @@ def main():
                 if "parity" in line and strip_run is not None:  # the baseline's strip is the same frame: check it too
                     line["parity"]["cpu_strip"] = parity_strip(ctx, scene, cam, params, image, strip_run)
             else:
-                line["cpu_baseline"] = cpu_baseline_learned(sampler, geom, params, cam_pos, args.cpu_seconds)
+                line["cpu_baseline"] = cpu_baseline_learned(sampler, geom, params, cam_pos, args.cpu_seconds,
+                                                            q_state, args.warmup)
         print(json.dumps(line), flush=True)
 
     for o in extra:

@@ -560,20 +560,18 @@ __global__ __launch_bounds__(256) void k_fold_chunks(const RenderLaunch a) {
 //
 // LDS: per wave and sample slot k, four 64-lane rows (lane-contiguous: conflict-free):
 //   continuing: the hit point x, y, z, triangle;  ended: L.x, L.y, L.z, -1.
-#ifndef RT_PS_STEAL
-#define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
-#endif
-#ifndef RT_PS_LIGHT_SPLIT
-#define RT_PS_LIGHT_SPLIT 1  // 0: terminal casts run the full closest hit (A/B builds)
-#endif
-// fields per slot: the hit point, its code (triangle; with the light split also the first
-// bounce's triangle << 16) and, with the light split, the first bounce's cos theta
-constexpr int kPsFields = (RT_PS_LIGHT_SPLIT && RT_PS_STEAL) ? 5 : 4;
-constexpr int kPsSplitLights = 8;  // the light split runs when the scene has at most this many light triangles
+constexpr int kPsFields = 4;
 
 #ifndef RT_PS_PRIM_BATCH
 #define RT_PS_PRIM_BATCH 4  // samples per candidate pass of phase P (1: one sample at a time)
 #endif
+#ifndef RT_PS_STEAL
+#define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
+#endif
+#ifndef RT_PS_LIGHT_SPLIT
+#define RT_PS_LIGHT_SPLIT 1  // 0: terminal casts always run the full closest hit (A/B builds)
+#endif
+constexpr int kPsSplitLights = 8;  // the light pre-test runs when the scene has at most this many light triangles
 // floats of LDS per wave: the sample slots, then (RT_PS_STEAL) the wave's queue of
 // continuing samples, one u16 (k << 6 | lane) per slot
 __host__ __device__ constexpr int ps_wave_floats(int pc) {
@@ -751,7 +749,6 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     pt[0] += t_s - t0;
 #endif
     f3 acc = make3(0.0f, 0.0f, 0.0f);
-    const bool use_mf_c = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
     int k = 0;          // next slot
     int cur = 0;        // sample of the live path
     int depth = 0;      // surface bounces of the live path so far
@@ -779,58 +776,18 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     float* own = slots;   // slot of the live path's sample (any lane's)
     uint32_t lpix = pix;  // its pixel (RNG key)
     bool live = false;
-    // Light split (RT_PS_LIGHT_SPLIT).  A terminal cast (the one at depth max_bounces) adds
-    // light only if its closest hit is a light triangle; a surface or a miss there gives 0.
-    // No light triangle passing the exact test without the t window means the closest hit
-    // cannot be a light: the value is 0 whatever the surfaces are, so only the (few) rays
-    // that pass a light's test need the whole closest hit.  Phase S then runs in stages,
-    // each a queue of slots in the wave's queue array:
-    //   0  non-terminal casts (full closest hit); a path whose next cast is terminal parks
-    //      its hit point, triangles and first cos theta in its slot for stage 1;
-    //   1  terminal casts against the light triangles only (exact_tv, the full test's own
-    //      operations): no pass -> value 0; a pass -> queued for stage 2;
-    //   2  those casts again (same Philox draw, same ray), full closest hit, folded.
-    // Entries of the next stage are written at positions below q_next (one per entry already
-    // taken), so one array serves all stages.  The image and the ray casts (counted in stage
-    // 0 and 1) are k_render's bit for bit.
-    const bool split = RT_PS_LIGHT_SPLIT && use_mf_c && a.max_bounces >= 1 &&
-                       (a.scene.n_tri - n_surf) <= kPsSplitLights;
-    int stage = (split && a.max_bounces == 1) ? 1 : 0;  // wave-uniform
-    int q_w = 0;          // wave-uniform: entries of the next stage written so far
-    uint32_t own_e = 0;   // the live path's queue entry
-    bool pending = false;  // the lane's path waits for the next stage (own_e to append)
     auto claim = [&]() {  // wave-level: lanes without a path take the next queued samples
-        if (RT_PS_LIGHT_SPLIT) {
-            const uint64_t pm = __ballot(pending);
-            if (pm != 0ull) {
-                if (pending)
-                    queue[q_w + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u))] =
-                        (uint16_t)own_e;
-                q_w += __builtin_popcountll(pm);
-                pending = false;
-            }
-        }
         const uint64_t need = __ballot(!live);
         if (need == 0ull || q_next >= q_total) return;
         const int j = q_next + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
         if (!live && j < q_total) {
             const uint32_t e = queue[j];
-            own_e = e;
             const int ol = (int)(e & 63u), kk = (int)(e >> 6);
             own = wslots + kk * kPsFields * 64 + ol;
             pos = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
-            const int code = __float_as_int(own[3 * 64]);
-            if (RT_PS_LIGHT_SPLIT && stage > 0) {
-                hit_tri = code & 0xffff;
-                depth = a.max_bounces - 1;
-                f_tri0 = code >> 16;  // (depth 0: set by the shading below)
-                f_cos0 = own[4 * 64];
-            } else {
-                hit_tri = code;
-                depth = 0;
-            }
+            hit_tri = __float_as_int(own[3 * 64]);
+            depth = 0;
             const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the lane's pixel
             lpix = (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
             cur = (ol & (a.split - 1)) * pc + kk;
@@ -866,22 +823,65 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     bool live = valid && fetch();
 #endif
     // the bounce casts on the matrix cores when the scene has the image (wave-uniform)
-    const bool use_mf = use_mf_c;
+    const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
+    // the next direction from the surface hit (pos, hit_tri) at bounce depth dep: cos theta
+    // and the ray (o = pos + eps sd, d = normalize(sd)), sampled with the path's Philox draw
+    auto shade_hit = [&](int dep, float* cos_out, f3* o_out, f3* d_out) {
+        const float4 N = shade[hit_tri * kShadeF4 + 0];
+        const float4 T = shade[hit_tri * kShadeF4 + 1];
+        const float4 B = shade[hit_tri * kShadeF4 + 2];
+        float r1, r2;
+#if RT_PS_STEAL
+        draw2(lpix, (uint32_t)cur, 1u + (uint32_t)dep, a.seed_lo, a.seed_hi, &r1, &r2);
+#else
+        draw2(pix, (uint32_t)cur, 1u + (uint32_t)dep, a.seed_lo, a.seed_hi, &r1, &r2);
+#endif
+        float cos_theta, sin_theta;
+        if (SAMPLER == 0) {
+            cos_theta = r1;
+            sin_theta = sqrtf(1.0f - r1 * r1);
+        } else {
+            cos_theta = sqrtf(r1);
+            sin_theta = sqrtf(1.0f - r1);
+        }
+        float sphi, cphi;
+        sincos_turn(r2, &sphi, &cphi);
+        const float sx = sin_theta * cphi, sz = sin_theta * sphi;
+        const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
+                            (sx * B.y + cos_theta * N.y) + sz * T.y,
+                            (sx * B.z + cos_theta * N.z) + sz * T.z);
+        *cos_out = cos_theta;
+        *o_out = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
+        *d_out = normalize(sd);
+    };
+    // Light pre-test (RT_PS_LIGHT_SPLIT).  The terminal cast of a path (the one at depth
+    // max_bounces) adds light only if its closest hit is a light triangle; a surface or a miss
+    // there gives 0.  If no light triangle passes the exact test without its t window
+    // (exact_tv: the full test's own operations), the closest hit cannot be a light, and the
+    // cast's value is 0 whatever the surfaces are.  So when a cast leaves a path whose next
+    // cast is terminal, the lane samples that next ray at once and tests only the light
+    // triangles: no pass -> the path ends with 0 (the terminal cast counted); a pass (a few
+    // percent of rays) -> the path stays live and the next trip traces the same ray (same
+    // Philox draw) in full.  Terminal casts thus stop taking slots of the matrix-core trips:
+    // the image and the ray casts are k_render's bit for bit.
+    const bool split = RT_PS_LIGHT_SPLIT && use_mf && a.max_bounces >= 1 &&
+                       (a.scene.n_tri - n_surf) <= kPsSplitLights;
+    // the pre-test of the terminal ray from (pos, hit_tri) at depth dep = max_bounces - 1
+    auto light_pass = [&](int dep) -> bool {
+        float c;
+        f3 lo, ld;
+        shade_hit(dep, &c, &lo, &ld);
+        const float nDx = -(ld.x * a.t_scale), nDy = -(ld.y * a.t_scale), nDz = -(ld.z * a.t_scale);
+        bool pass = false;
+        for (int j = n_surf; j < a.scene.n_tri; ++j)
+            pass |= exact_tv<RULE>(ms.isect, j, lo, nDx, nDy, nDz) != __builtin_inff();
+        return pass;
+    };
     for (;;) {
 #if RT_PS_STEAL
         claim();
-        if (__ballot(live) == 0ull) {
-            if (!split || stage == 2) break;
-            // the stage is done: the next one takes the entries written during it
-            ++stage;
-            q_total = q_w;
-            q_next = 0;
-            q_w = 0;
-            continue;
-        }
-#else
-        if (__ballot(live) == 0ull) break;
 #endif
+        if (__ballot(live) == 0ull) break;
         if (!use_mf && !live) continue;
 #if RT_PROF
         const uint64_t ta = __builtin_amdgcn_s_memtime();
@@ -891,60 +891,14 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         float s_cos = 0.0f;
         if (live) {
             // shade the live path's surface hit (depth < max_bounces by construction)
-            const float4 N = shade[hit_tri * kShadeF4 + 0];
-            const float4 T = shade[hit_tri * kShadeF4 + 1];
-            const float4 B = shade[hit_tri * kShadeF4 + 2];
-            float r1, r2;
-#if RT_PS_STEAL
-            draw2(lpix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
-#else
-            draw2(pix, (uint32_t)cur, 1u + (uint32_t)depth, a.seed_lo, a.seed_hi, &r1, &r2);
-#endif
-            float cos_theta, sin_theta;
-            if (SAMPLER == 0) {
-                cos_theta = r1;
-                sin_theta = sqrtf(1.0f - r1 * r1);
-            } else {
-                cos_theta = sqrtf(r1);
-                sin_theta = sqrtf(1.0f - r1);
-            }
-            float sphi, cphi;
-            sincos_turn(r2, &sphi, &cphi);
-            const float sx = sin_theta * cphi, sz = sin_theta * sphi;
-            const f3 sd = make3((sx * B.x + cos_theta * N.x) + sz * T.x,
-                                (sx * B.y + cos_theta * N.y) + sz * T.y,
-                                (sx * B.z + cos_theta * N.z) + sz * T.z);
             s_tri = hit_tri;
-            s_cos = cos_theta;
+            shade_hit(depth, &s_cos, &o, &d);
             if (depth == 0) {
                 f_tri0 = s_tri;
                 f_cos0 = s_cos;
             }
-            o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
-            d = normalize(sd);
             ++depth;
         }
-#if RT_PS_STEAL
-        if (RT_PS_LIGHT_SPLIT && stage == 1) {
-            // the terminal cast against the light triangles (surfaces first, lights last)
-            if (live) {
-                ++n_casts;
-                const float nDx = -(d.x * a.t_scale), nDy = -(d.y * a.t_scale), nDz = -(d.z * a.t_scale);
-                bool pass = false;
-                for (int j = n_surf; j < a.scene.n_tri; ++j)
-                    pass |= exact_tv<RULE>(ms.isect, j, o, nDx, nDy, nDz) != __builtin_inff();
-                if (pass) {
-                    pending = true;  // stage 2 traces it again in full
-                } else {
-                    own[0 * 64] = 0.0f;  // a surface or a miss at depth max_bounces: 0
-                    own[1 * 64] = 0.0f;
-                    own[2 * 64] = 0.0f;
-                }
-                live = false;
-            }
-            continue;
-        }
-#endif
         // every lane of the wave takes part in the matrix-core filter; a lane without a
         // live path casts its stale (finite) ray with no candidates
 #if RT_PROF
@@ -967,11 +921,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         pt[3] += tc - tm;
 #endif
         if (!live) continue;
-#if RT_PS_STEAL
-        if (stage != 2) ++n_casts;  // (stage 2 repeats a cast that stage 1 counted)
-#else
         ++n_casts;
-#endif
 
         bool terminal = true;
         f3 L = make3(0.0f, 0.0f, 0.0f);
@@ -1007,18 +957,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             terminal = false;  // shade the hit on the next trip
             pos = make3(o.x + h.t * (d.x * a.t_scale), o.y + h.t * (d.y * a.t_scale), o.z + h.t * (d.z * a.t_scale));
             hit_tri = h.tri;
-#if RT_PS_STEAL
-            if (split && depth + 1 == a.max_bounces) {
-                // the next cast is terminal: park the path for stage 1
-                own[0 * 64] = pos.x;
-                own[1 * 64] = pos.y;
-                own[2 * 64] = pos.z;
-                own[3 * 64] = __int_as_float(hit_tri | (f_tri0 << 16));
-                own[4 * 64] = f_cos0;
-                pending = true;
-                live = false;
+            if (split && depth + 1 == a.max_bounces && !light_pass(depth)) {
+                ++n_casts;  // the terminal cast: no light triangle can be its hit
+                terminal = true;
             }
-#endif
         }
         if (terminal) {
 #if RT_PS_STEAL
