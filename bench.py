@@ -562,6 +562,8 @@ def make_workload(args, ctx):
         geom = rtmi.obj_geometry(os.path.join(MODELS, scene_kind + ".obj"), scene_kind)
         cam_pos = rtmi.CAMERAS[scene_kind]
     params = rtmi.default_params(preset, width=W, height=H, spp=spp, spp_split=split)
+    if args.workload == "cornell" and (W, H, spp) == (256, 256, 4):
+        cfg = 1  # BASELINE config 1: the reference's CPU-runnable Cornell case
     return scene_kind, sampler, cfg, geom, cam_pos, params
 
 
