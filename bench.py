@@ -155,6 +155,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target duration of one CPU-baseline run (best of 3; 0 disables)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--emulate-ranks", type=int, default=0,
+                    help="P > 1: on one GPU, run each of the P ranks' tile sets through the timed loop in turn "
+                         "(host work included; a device copy stands in for the gather) and predict the P-GPU step")
     args = ap.parse_args()
     if args.steps is None:
         args.steps = 20 if args.workload == "cornell" else 10
@@ -567,8 +570,162 @@ def make_workload(args, ctx):
     return scene_kind, sampler, cfg, geom, cam_pos, params
 
 
+class _LocalGather:
+    """Stand-in for the RCCL gather in a one-GPU emulation of rank r of P: the rank's tile
+    buffer is copied into its slot of a [P, k, T, T, 3] buffer on a second stream, ordered
+    after the render the way the collective is (the next render into the buffer waits for it)."""
+
+    def __init__(self, world: int, shape, device, rank: int):
+        self.stream = torch.cuda.Stream(device)
+        self.buf = torch.empty((world,) + tuple(shape), dtype=torch.float32, device=device)
+        self.rank = rank
+        self.done = [None, None]
+
+    def gather(self, out: torch.Tensor, b: int) -> None:
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(out.device))
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ev)
+            self.buf[self.rank].copy_(out, non_blocking=True)
+            self.done[b] = torch.cuda.Event()
+            self.done[b].record(self.stream)
+
+    def wait(self, b: int) -> None:
+        if self.done[b] is not None:
+            torch.cuda.current_stream().wait_event(self.done[b])
+            self.done[b] = None
+
+
+def emulate(args) -> None:
+    """--emulate-ranks P: the P-GPU step predicted on one GPU.  For every rank r of P, its tile
+    set (rtmi.tiles.rank_tiles: the tiles it renders at world size P) runs through the same timed
+    loop as a real rank -- warmup, then `steps` frames, each: wait for the buffer's previous
+    gather, record events, render (the ctypes call and its launches), queue the gather -- with a
+    device copy on a second stream standing in for the RCCL gather to rank 0.  The P-GPU step is
+    the slowest rank's host-inclusive step time; the one-GPU step is the same loop over all tiles.
+    Expected SARSA adds its real exchange: the TD sums' all-reduce, whose payload is reported with
+    a ring-all-reduce model over one xGMI link (it cannot run on one GPU)."""
+    P = args.emulate_ranks
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    ctx = rtmi.Context(0)
+    scene_kind, sampler, cfg, geom, cam_pos, params = make_workload(args, ctx)
+    scene = rtmi.Scene(ctx, geom)
+    cam = rtmi.camera(cam_pos)
+    stream = torch.cuda.current_stream(dev)
+    casts = torch.zeros(1, dtype=torch.int64, device=dev)
+    extra = []
+    rmap = None
+    if sampler == "sarsa":
+        rmap = rtmi.sarsa.RadianceMap(ctx, scene, 1984)
+        extra.append(rmap)
+    elif sampler == "dqn":
+        Ws, bs = rtmi.dqn.synthetic_weights(geom.nn_vertices.size)
+        net = rtmi.dqn.Dqn(ctx, geom.nn_vertices, Ws, bs)
+        extra.append(net)
+
+    def make_render(tiles, n_real, world):
+        if sampler == "sarsa":
+            def render(out):
+                # every timed frame (one GPU and each rank alike) reads the map as the shared
+                # warmup left it and leaves its TD sums unapplied, as a rank's frame leaves them
+                # for the exchange: the ranks' frames are the same frame of the same learning run
+                rmap.render_tiles_device(cam, params, tiles[:n_real], TILE, out.data_ptr(), casts.data_ptr(),
+                                         apply=False, stream=stream.cuda_stream)
+        elif sampler == "dqn":
+            def render(out):
+                rtmi.dqn.render_tiles_device(ctx, scene, net, cam, params, tiles, TILE, out.data_ptr(),
+                                             casts.data_ptr(), stream.cuda_stream)
+        else:
+            def render(out):
+                rtmi.render_tiles_device(ctx, scene, cam, params, tiles, TILE, out.data_ptr(), casts.data_ptr(),
+                                         stream.cuda_stream)
+        return render
+
+    if sampler == "sarsa":  # the learning run's warmup frames, once, on the whole frame
+        wt = rtmi.tiles.rank_tiles(params.width, params.height, TILE, 0, 1)
+        wo = torch.zeros((wt.shape[0], TILE, TILE, 3), dtype=torch.float32, device=dev)
+        for _ in range(args.warmup):
+            rmap.render_tiles_device(cam, params, wt, TILE, wo.data_ptr(), casts.data_ptr(), apply=True,
+                                     stream=stream.cuda_stream)
+        torch.cuda.synchronize()
+
+    def run(world, rank):
+        tiles = rtmi.tiles.rank_tiles(params.width, params.height, TILE, rank, world)
+        n_real = rtmi.tiles.rank_tile_count(params.width, params.height, TILE, rank, world)
+        shape = (tiles.shape[0], TILE, TILE, 3)
+        render = make_render(tiles, n_real, world)
+        outs = [torch.zeros(shape, dtype=torch.float32, device=dev) for _ in range(2)]
+        g = _LocalGather(world, shape, dev, rank)
+        for i in range(args.warmup):
+            g.wait(i % 2)
+            render(outs[i % 2])
+            g.gather(outs[i % 2], i % 2)
+        torch.cuda.synchronize()
+        casts.zero_()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            b = i % 2
+            g.wait(b)
+            ev[i][0].record(stream)
+            render(outs[b])
+            ev[i][1].record(stream)
+            g.gather(outs[b], b)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        kern = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        return {"rank": rank, "tiles": int(n_real), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "frame_ms": round(kern, 4), "host_ms_over_device": round(elapsed / args.steps * 1e3 - kern, 4),
+                "ray_casts_per_step": int(casts.item()) // args.steps}
+
+    progress(f"{args.workload}: one GPU, all tiles")
+    one = run(1, 0)
+    ranks = []
+    for r in range(P):
+        ranks.append(run(P, r))
+        progress(f"rank {r} of {P}: {ranks[-1]['ms_per_step']} ms per step")
+    t_p = max(x["ms_per_step"] for x in ranks)
+    line = {"mode": "emulated_ranks", "workload": args.workload, "baseline_config": cfg, "emulated_world": P,
+            "width": params.width, "height": params.height, "spp": params.spp, "steps": args.steps,
+            "warmup": args.warmup, "one_gpu": one, "ranks": ranks,
+            "predicted_step_ms": t_p,
+            "predicted_speedup": round(one["ms_per_step"] / t_p, 3),
+            "predicted_speedup_device_only": round(one["frame_ms"] / max(x["frame_ms"] for x in ranks), 3),
+            "gather_bytes_per_rank": int(rtmi.tiles.rank_tiles(params.width, params.height, TILE, 0, P).shape[0]
+                                         * TILE * TILE * 12)}
+    if sampler == "sarsa":
+        # the frame's update (k_sarsa_apply over the whole map) runs on every rank after the
+        # exchange, at any P: timed here on its own, added to both sides
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rmap.apply(stream.cuda_stream)
+        torch.cuda.synchronize()
+        apply_ms = (time.perf_counter() - t0) / args.steps * 1e3
+        n = rmap.n_volumes * 144
+        payload = n * (8 + 4)  # int64 sums + int32 counts
+        ring = 2.0 * (P - 1) / P * payload / 153e9 * 1e3  # ms over one 153 GB/s xGMI link
+        line["apply_ms"] = round(apply_ms, 4)
+        line["td_allreduce_bytes"] = payload
+        line["td_allreduce_ms_model"] = round(ring, 3)
+        one_step = one["ms_per_step"] + apply_ms
+        p_step = t_p + ring + apply_ms
+        line["one_gpu_step_ms_with_apply"] = round(one_step, 4)
+        line["predicted_step_ms_with_apply_and_allreduce_model"] = round(p_step, 4)
+        line["predicted_speedup_with_apply_and_allreduce_model"] = round(one_step / p_step, 3)
+    print(json.dumps(line), flush=True)
+    for o in extra:
+        o.close()
+    scene.close()
+    ctx.close()
+
+
 def main():
     args = parse()
+    if args.emulate_ranks > 1:
+        return emulate(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:  # (rank_launch refuses this before any GPU work; kept for imports of main)
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
