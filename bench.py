@@ -107,7 +107,10 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 (MI355X_MICROARCH.md; no sparsity)
 WORKLOADS = {
     # name: (scene, preset, sampler, width, height, spp, spp_split, BASELINE config)
     "cornell": ("cornell", rtmi.RT_PRESET_CPU, "uniform", 512, 512, 256, 64, 2),
-    "door_room_sarsa": ("door_room", rtmi.RT_PRESET_GPU, "sarsa", 512, 512, 256, 8, 3),
+    # (config 3: spp_split 64 -- 4-sample work items balance the persistent queue's lanes: frames
+    # 1-10 91.9 vs 102.6 ms at split 8 on one GPU, and each rank's launch at P = 8, where split 8
+    # leaves about one item per lane: 6.5x vs 4.8x predicted, profiles/r5h/)
+    "door_room_sarsa": ("door_room", rtmi.RT_PRESET_GPU, "sarsa", 512, 512, 256, 64, 3),
     "archway_dqn": ("archway", rtmi.RT_PRESET_GPU, "dqn", 1024, 1024, 512, 1, 4),
     # (config 5: spp_split 32 -- 2-sample chunks end each rank's launch of the P = 8 split
     # sooner: 121.6 vs 131.3 ms per rank set at 64 spp, profiles/r3ag/; one GPU unchanged)
