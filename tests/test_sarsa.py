@@ -298,12 +298,13 @@ def test_gpu_render_grid_equals_kd(rtmi_mod, gpu_ctx, scene):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("scene,split,hit_rule", [("door_room", 1, 1), ("door_room", 4, 1), ("cornell", 2, 1),
-                                                   ("archway", 1, 0)])
-def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, split, hit_rule):
+@pytest.mark.parametrize("scene,split,hit_rule,spp", [("door_room", 1, 1, 8), ("door_room", 4, 1, 8),
+                                                       ("cornell", 2, 1, 8), ("archway", 1, 0, 8),
+                                                       ("door_room", 64, 1, 256)])  # the bench's split
+def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, split, hit_rule, spp):
     g, sc, rm, om = _both(rtmi_mod, oracle_mod, gpu_ctx, scene)
     try:
-        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=40, spp=8, spp_split=split,
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=40, spp=spp, spp_split=split,
                                     hit_rule=hit_rule)
         cam = rtmi_mod.camera(rtmi_mod.CAMERAS[scene])
         for frames in (1, 2):

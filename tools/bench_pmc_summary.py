@@ -65,7 +65,7 @@ WORKLOADS = {
 }
 
 # bench.py's per-workload frame defaults (width, height, spp, spp_split)
-BENCH_FRAMES = {"cornell": (512, 512, 256, 64), "door_room_sarsa": (512, 512, 256, 8),
+BENCH_FRAMES = {"cornell": (512, 512, 256, 64), "door_room_sarsa": (512, 512, 256, 64),
                 "archway_dqn": (1024, 1024, 512, 1), "complex_light": (2048, 2048, 1024, 32)}
 
 
