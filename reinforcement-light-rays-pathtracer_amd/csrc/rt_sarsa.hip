@@ -790,7 +790,10 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
 // BVH: scenes with the exact BVH (large models, rt_scene_set_accel): the casts through
 // closest_hit_bvh, its stack in the lane's k-d stack column (free until the volume search)
 template <int RULE, int MF, int TD, bool BVH = false>
-__global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES) void k_sarsa_render_pq(const RenderLaunch a,
+#ifndef RT_SARSA_BVH_WAVES
+#define RT_SARSA_BVH_WAVES 4  // the BVH variant's traversal state: 128 VGPRs, no spills (96 at 5 waves spilled)
+#endif
+__global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES)) void k_sarsa_render_pq(const RenderLaunch a,
                                                                                         const SarsaMap m) {
     __shared__ int kd_stack[kKdStack * 256];
     int* const st = kd_stack_of(kd_stack);
@@ -1113,7 +1116,7 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
         if (a.csum == nullptr || a.work == nullptr) return hipErrorInvalidValue;
         (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
         // as many workgroups as fit: RT_SARSA_WAVES per CU (registers and the k-d stack's LDS)
-        const int per_cu = mf ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES;
+        const int per_cu = a.scene.bvh_nodes != nullptr ? RT_SARSA_BVH_WAVES : (mf ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES);
         const dim3 grid((unsigned)min(a.n_blocks * a.split, per_cu * device_cu_count()));
         if constexpr (RT_MF_SARSA) {
             if (mf) {

@@ -210,36 +210,59 @@ def test_bvh_small_scene_forced(rtmi_mod, gpu_ctx):
     assert np.array_equal(img.view(np.uint32), img_b.view(np.uint32))
 
 
-def test_bvh_sarsa_render_equals_scan(rtmi_mod, gpu_ctx):
+@pytest.mark.parametrize("hit_rule,td_mode", [(1, "frame"), (0, "frame"), (1, "inframe")])
+def test_bvh_sarsa_render_equals_scan(rtmi_mod, gpu_ctx, hit_rule, td_mode):
     """The SARSA sampler's trace on the BVH (k_sarsa_render_pq<.., BVH>) is the scan bit for bit:
-    two frames of the bunny in the Cornell box, the second sampling the map the first trained."""
+    two frames of the bunny in the Cornell box, the second sampling the map the first trained;
+    both hit rules, and the in-frame TD rule (k_sarsa_render_pq<.., TD = 1, BVH>) on a launch
+    with one active lane (a 1 x 1 image, one chunk), whose events then run in sample order."""
     g = bunny_cornell(rtmi_mod, rtmi_mod.RT_PRESET_GPU)
     cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
-    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=8, spp_split=4)
+    if td_mode == "frame":
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=8, spp_split=4,
+                                    hit_rule=hit_rule)
+    else:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=1, height=1, spp=64, spp_split=1,
+                                    hit_rule=hit_rule)
     out = {}
     with rtmi_mod.Scene(gpu_ctx, g) as sc:
         for accel in (None, rtmi_mod.ACCEL_SCAN):
             if accel is not None:
                 sc.set_accel(accel)
             with rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) as m:
-                out[accel] = [m.render(cam, p, 1) for _ in range(2)]
+                if td_mode == "inframe":
+                    m.set_td_mode(rtmi_mod.sarsa.TD_INFRAME)
+                out[accel] = [m.render(cam, p, 1) for _ in range(2)] + [m.read()]
+        Q, Qs = out[None].pop(), out[rtmi_mod.ACCEL_SCAN].pop()
+    for a, b in zip(Q, Qs):
+        assert np.array_equal(a, b)
     for (a, ca), (b, cb) in zip(out[None], out[rtmi_mod.ACCEL_SCAN]):
         assert ca == cb
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
-    assert out[None][1][0].mean() > 0
+    if td_mode == "frame":
+        assert out[None][1][0].mean() > 0
 
 
-def test_bvh_dqn_render_equals_scan(rtmi_mod, gpu_ctx):
+@pytest.mark.parametrize("hit_rule", [1, 0])
+def test_bvh_dqn_render_equals_scan(rtmi_mod, gpu_ctx, hit_rule):
     """The DQN sampler's casts on the BVH (dqn_trace<-1>) are the scan's bit for bit (synthetic
-    weights over the box's vertices as the network's inputs)."""
+    weights over the box's vertices as the network's inputs).  The DQN renderer implements the
+    GPU engine (pre_trained_pathtracer.cu): the CPU object's hit rule is refused, BVH or scan."""
     g = bunny_cornell(rtmi_mod, rtmi_mod.RT_PRESET_GPU)
     box = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
     nn = np.unique(box.tri.reshape(-1, 3), axis=0).astype(np.float32).ravel()
     W, b = rtmi_mod.dqn.synthetic_weights(nn.size)
     cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
-    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=4)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=96, spp=4, hit_rule=hit_rule)
     out = []
     with rtmi_mod.Scene(gpu_ctx, g) as sc, rtmi_mod.dqn.Dqn(gpu_ctx, nn, W, b) as net:
+        if hit_rule == 0:
+            for accel in (None, rtmi_mod.ACCEL_SCAN):
+                if accel is not None:
+                    sc.set_accel(accel)
+                with pytest.raises(rtmi_mod.RtError):
+                    rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p)
+            return
         out.append(rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p))
         sc.set_accel(rtmi_mod.ACCEL_SCAN)
         out.append(rtmi_mod.dqn.render(gpu_ctx, sc, net, cam, p))
