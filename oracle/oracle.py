@@ -124,6 +124,21 @@ def intersect(tri, n_surf, n_light, light_group, orig, direction, t_scale, hit_r
     return out_t, out_h
 
 
+def pass_masks(tri, orig, direction, t_scale, hit_rule):
+    """[n_rays][ceil(n_tri / 64)] uint64: bit i = triangle i passes the exact test (no
+    closest-hit window) -- what a candidate filter must keep (orc_pass_masks)."""
+    t_all = np.ascontiguousarray(tri, np.float32).reshape(-1, 9)
+    o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
+    n, nt = o.shape[0], t_all.shape[0]
+    out = np.zeros((n, (nt + 63) // 64), np.uint64)
+    L = lib()
+    L.orc_pass_masks.argtypes = [_FP, ctypes.c_int, _FP, _FP, ctypes.c_int, ctypes.c_float, ctypes.c_int,
+                                 ctypes.c_void_p]
+    L.orc_pass_masks(_f(t_all), nt, _f(o), _f(d), n, t_scale, hit_rule, out.ctypes.data_as(ctypes.c_void_p))
+    return out
+
+
 def primary_hits(tri, n_surf, n_light, cam, params, rect, s0, s1):
     """Triangle index (-1 = miss) hit by the camera ray of every pixel of rect = (x, y, w, h)
     and sample in [s0, s1): array (h, w, s1 - s0)."""

@@ -372,6 +372,45 @@ ORC_API void orc_intersect(const float *tri, int n_surf, int n_light, const int3
     free(sc.normal);
 }
 
+/* The pass set of the geometric test per triangle, without the closest-hit window: bit i
+ * of masks[r * words + i / 64] = triangle i passes Triangle::intersects' test for ray r
+ * (the detA, t, u, v conditions of closest_hit above, CPU/rays/ray.cpp:14-28 and Appendix A
+ * of SURVEY.md for rule 0; GPU/rays/ray.cu:63-64 for rule 1).  A candidate filter must keep
+ * every such triangle (tests of the kernels' culls and candidate tables). */
+ORC_API void orc_pass_masks(const float *tri, int n_tri, const float *orig, const float *dir, int n,
+                            float t_scale, int hit_rule, uint64_t *masks) {
+    const int words = (n_tri + 63) / 64;
+    #pragma omp parallel for schedule(static)
+    for (int r = 0; r < n; r++) {
+        v3 o = mk(orig[r * 3], orig[r * 3 + 1], orig[r * 3 + 2]);
+        v3 d = mk(dir[r * 3], dir[r * 3 + 1], dir[r * 3 + 2]);
+        v3 nD = mk(-(d.x * t_scale), -(d.y * t_scale), -(d.z * t_scale));
+        uint64_t *m = masks + (size_t)r * words;
+        for (int w = 0; w < words; w++) m[w] = 0;
+        for (int i = 0; i < n_tri; i++) {
+            v3 v0 = vtx(tri, i, 0), v1 = vtx(tri, i, 1), v2 = vtx(tri, i, 2);
+            v3 e1 = mk(v1.x - v0.x, v1.y - v0.y, v1.z - v0.z);
+            v3 e2 = mk(v2.x - v0.x, v2.y - v0.y, v2.z - v0.z);
+            v3 b = mk(o.x - v0.x, o.y - v0.y, o.z - v0.z);
+            float detA = det3(nD, e1, e2);
+            if (!(detA != 0.0f)) continue;
+            float t, u, v;
+            if (hit_rule == 0) {
+                float inv = 1.0f / detA;
+                t = det3(b, e1, e2) * inv;
+                u = det3(nD, b, e2) * inv;
+                v = det3(nD, e1, b) * inv;
+            } else {
+                t = det3(b, e1, e2) / detA;
+                u = det3(nD, b, e2) / detA;
+                v = det3(nD, e1, b) / detA;
+            }
+            if (t >= 0.0f && u >= 0.0f && v >= 0.0f && (u + v) <= 1.0f && (hit_rule != 0 || t > 1e-5f))
+                m[i / 64] |= 1ull << (i % 64);
+        }
+    }
+}
+
 /* ------------------------------------------------------------------ */
 /* sampling                                                            */
 /* ------------------------------------------------------------------ */

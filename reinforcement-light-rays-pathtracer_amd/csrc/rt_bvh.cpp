@@ -31,33 +31,27 @@
 #include <string>
 #include <vector>
 
+#include "rt_bounds.hpp"
 #include "rt_internal.hpp"
 
 namespace rt {
 
 namespace {
 
-constexpr double kU = 1.0 / 16777216.0;   // 2^-24
-constexpr double kC = 1.0 / 524288.0;     // 2^-19: 2x the 16u of both evaluations
+using bnd::Bounds;
+using bnd::bounds_for;
+using bnd::down;
+using bnd::kC;
+using bnd::kU;
+using bnd::up;
 constexpr double kK = kBvhK;
 constexpr int kLeafMax = 4;
 constexpr int kBins = 16;
 
-float down(double x) {
-    float f = (float)x;
-    return ((double)f <= x) ? f : nextafterf(f, -INFINITY);
-}
-float up(double x) {
-    float f = (float)x;
-    return ((double)f >= x) ? f : nextafterf(f, INFINITY);
-}
-
-struct TriInfo {
+// build_filter's sums (bnd::TriAlg) and the padded box of one triangle
+struct TriInfo : bnd::TriAlg {
     double lo[3], hi[3];  // padded box
     double c[3];          // centroid of the padded box
-    double N[3], w0, nlen;
-    double M, n1, n2;     // build_filter's sums
-    double vmax;
 };
 
 struct Box {
@@ -74,20 +68,6 @@ struct Box {
         return 2.0 * (x * y + y * z + z * x);
     }
 };
-
-// error bounds of one triangle for origins within B (build_filter's structure)
-struct Bounds {
-    double eA, EW, ET;
-};
-Bounds bounds_for(const TriInfo& t, double B) {
-    const double dinf = (double)kMfDirBound;
-    const double F = ldexp(1.0, -90);
-    Bounds b;
-    b.eA = kC * dinf * t.M + F;
-    b.EW = 2.0 * (kC * 2.0 * dinf * B * t.n2 + kC * 2.0 * dinf * B * t.n1 + b.eA) + F;
-    b.ET = kC * (B + t.vmax) * t.M + 2.0 * 1e-5 * (double)kFiltMaxTScale * b.eA + F;
-    return b;
-}
 
 // threshold of the kernel's |d.N~| test (N~ the float normal): K EW + eA + evaluation slack
 float graze_threshold(const TriInfo& t, const Bounds& b) {
@@ -221,14 +201,8 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         const float4 P0 = isect[(size_t)i * 3], P1 = isect[(size_t)i * 3 + 1], P2 = isect[(size_t)i * 3 + 2];
         const double v0[3] = {P0.x, P0.y, P0.z}, a[3] = {P1.x, P1.y, P1.z}, b[3] = {P2.x, P2.y, P2.z};
         TriInfo& t = ti[(size_t)i];
-        t.M = t.n1 = t.n2 = t.vmax = 0.0;
+        static_cast<bnd::TriAlg&>(t) = bnd::tri_alg(P0, P1, P2);
         for (int k = 0; k < 3; ++k) {
-            const int j = (k + 1) % 3, l = (k + 2) % 3;
-            t.N[k] = a[j] * b[l] - a[l] * b[j];
-            t.M += fabs(a[j] * b[l]) + fabs(a[l] * b[j]);
-            t.n1 += fabs(a[k]);
-            t.n2 += fabs(b[k]);
-            t.vmax = std::max(t.vmax, fabs(v0[k]));
             const double x0 = v0[k], x1 = v0[k] + a[k], x2 = v0[k] + b[k];
             const double lo = std::min(x0, std::min(x1, x2)), hi = std::max(x0, std::max(x1, x2));
             const double pad = 2.0 / kK * (hi - lo) + mu;
@@ -236,8 +210,6 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
             t.hi[k] = hi + pad;
             t.c[k] = 0.5 * (t.lo[k] + t.hi[k]);
         }
-        t.w0 = v0[0] * t.N[0] + v0[1] * t.N[1] + v0[2] * t.N[2];
-        t.nlen = sqrt(t.N[0] * t.N[0] + t.N[1] * t.N[1] + t.N[2] * t.N[2]);
         if (!(t.M < ldexp(1.0, 36)) || !(obound < ldexp(1.0, 20))) return false;
     }
     // t-window slack over the regular pairs, for origins within obound (camera included)
@@ -328,16 +300,6 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
         }
         const int G = kBvhDirGrid;
         const int cells = 6 * G * G;
-        auto cell_dir = [&](int f, double u, double v, double* out) {  // face f: axis f/2, sign
-            const int ax = f >> 1;
-            const double sg = (f & 1) ? -1.0 : 1.0;
-            double p[3];
-            p[ax] = sg;
-            p[(ax + 1) % 3] = u;
-            p[(ax + 2) % 3] = v;
-            const double l = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
-            for (int k = 0; k < 3; ++k) out[k] = p[k] / l;
-        };
         const double BL[2] = {B_s, obound};
         for (int set = 0; set < 2; ++set) {
             std::vector<int32_t>& start = set ? h.dstart_cam : h.dstart;
@@ -348,17 +310,8 @@ bool bvh_build(const float4* isect, int n, BvhHost* out) {
                 const int f = c / (G * G), iu = (c / G) % G, iv = c % G;
                 const double u0 = -1.0 + 2.0 * iu / G, u1 = -1.0 + 2.0 * (iu + 1) / G;
                 const double v0 = -1.0 + 2.0 * iv / G, v1 = -1.0 + 2.0 * (iv + 1) / G;
-                double dc[3], q[3];
-                cell_dir(f, 0.5 * (u0 + u1), 0.5 * (v0 + v1), dc);
-                double chord = 0.0;
-                const double us[2] = {u0, u1}, vs[2] = {v0, v1};
-                for (int ku = 0; ku < 2; ++ku)
-                    for (int kv = 0; kv < 2; ++kv) {
-                        cell_dir(f, us[ku], vs[kv], q);
-                        chord = std::max(chord, sqrt((q[0] - dc[0]) * (q[0] - dc[0]) + (q[1] - dc[1]) * (q[1] - dc[1]) +
-                                                     (q[2] - dc[2]) * (q[2] - dc[2])));
-                    }
-                chord = chord * (1.0 + 1e-6) + 1e-6;  // + the kernel's rounding of the cell choice
+                double dc[3];
+                const double chord = bnd::cell_chord(f, u0, u1, v0, v1, dc);
                 for (int i = 0; i < n; ++i) {
                     const double* nn3 = &un[(size_t)i * 3];
                     const double dn = fabs(dc[0] * nn3[0] + dc[1] * nn3[1] + dc[2] * nn3[2]);

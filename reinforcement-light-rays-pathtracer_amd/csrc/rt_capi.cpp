@@ -79,6 +79,9 @@ struct rt_scene {
     rt::BvhHost bvh;
     float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, grec
     int32_t* d_dir[3] = {nullptr, nullptr, nullptr};           // starts (2 sets), list, camera list
+    // bounce-ray candidate table (rt_ctab.cpp): built on the first CPU-preset render that can
+    // use it (scene_ensure_ctab), its device arrays in dev.ctab*
+    bool ctab_tried = false;
 };
 
 namespace {
@@ -285,6 +288,57 @@ int check_params(const rt_params* p) {
     if (p->spp % split != 0) return fail(RT_E_INVALID, "spp_split %d does not divide spp %d", split, p->spp);
     if ((int64_t)p->width * (int64_t)p->height > (int64_t)1 << 31)
         return fail(RT_E_INVALID, "image too large");
+    return RT_OK;
+}
+
+
+void isect_record(const float* v, float4* out);
+
+// The bounce-ray candidate table of a scene (rt_ctab.cpp), built and uploaded once, on the
+// first render that can use it: the CPU engine's hit rule, t_scale >= kCtabTsMin, a scene of at
+// most 64 triangles with the matrix-core image (whose origin bound it shares).  A lazily
+// built cache of the scene (hence the const_cast); RT_CTAB=0 leaves the bounce casts on the
+// image's masks (A/B builds).  A scene the table cannot be built for keeps the image.
+int scene_ensure_ctab(const rt_scene* scene, const rt_params* p) {
+    rt_scene* sc = const_cast<rt_scene*>(scene);
+    if (sc->ctab_tried || p->preset != RT_PRESET_CPU || p->hit_rule != RT_HIT_RULE_CPU || !(p->t_scale >= rt::kCtabTsMin))
+        return RT_OK;
+    sc->ctab_tried = true;
+    static const bool ctab_on = getenv("RT_CTAB") == nullptr || atoi(getenv("RT_CTAB")) != 0;
+    const int n = sc->dev.n_tri, n_surf = sc->dev.n_surf;
+    if (!ctab_on || sc->dev.mf_frag == nullptr || n > 64 || n_surf <= 0) return RT_OK;
+    std::vector<float4> isect((size_t)n * rt::kIsectF4);
+    for (int i = 0; i < n; ++i) isect_record(sc->tri.data() + (size_t)i * 9, &isect[(size_t)i * 3]);
+    rt::CtabHost ct;
+    if (!rt::ctab_build(isect.data(), n, n_surf, (double)sc->dev.mf_bound, rt::kCtabTsMin, &ct)) return RT_OK;
+    int rc = set_device(sc->ctx);
+    if (rc != RT_OK) return rc;
+    unsigned long long *dm = nullptr, *dg = nullptr, *dc = nullptr;
+    float4* dt = nullptr;
+    hipError_t e = hipMalloc(&dm, sizeof(uint64_t) * ct.masks.size());
+    if (e == hipSuccess) e = hipMalloc(&dg, sizeof(uint64_t) * ct.graze.size());
+    if (e == hipSuccess) e = hipMalloc(&dc, sizeof(uint64_t) * ct.cop.size());
+    if (e == hipSuccess) e = hipMalloc(&dt, sizeof(float4) * ct.tri.size());
+    if (e == hipSuccess) e = hipMemcpy(dm, ct.masks.data(), sizeof(uint64_t) * ct.masks.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dg, ct.graze.data(), sizeof(uint64_t) * ct.graze.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dc, ct.cop.data(), sizeof(uint64_t) * ct.cop.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dt, ct.tri.data(), sizeof(float4) * ct.tri.size(), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (dm) (void)hipFree(dm);
+        if (dg) (void)hipFree(dg);
+        if (dc) (void)hipFree(dc);
+        if (dt) (void)hipFree(dt);
+        return fail(RT_E_HIP, "candidate table upload failed: %s", hipGetErrorString(e));
+    }
+    sc->dev.ctab = dm;
+    sc->dev.ctab_graze = dg;
+    sc->dev.ctab_cop = dc;
+    sc->dev.ctab_tri = dt;
+    sc->dev.ctab_h = ct.h_run;
+    sc->dev.ctab_ts_min = ct.ts_min;
+    sc->dev.ctab_cop_th = ct.cop_th;
+    sc->dev.ctab_bins = rt::kCtabBins;
+    sc->dev.ctab_graze_n = rt::kCtabGraze;
     return RT_OK;
 }
 
@@ -735,6 +789,10 @@ int rt_scene_destroy(rt_scene* scene) {
     (void)hipFree(scene->dev.code_gpu);
     if (scene->dev.filt) (void)hipFree(scene->dev.filt);
     if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
+    if (scene->dev.ctab) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab));
+    if (scene->dev.ctab_graze) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab_graze));
+    if (scene->dev.ctab_tri) (void)hipFree(const_cast<float4*>(scene->dev.ctab_tri));
+    if (scene->dev.ctab_cop) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab_cop));
     scene_free_bvh(scene);
     delete scene;
     return RT_OK;
@@ -751,6 +809,33 @@ int rt_scene_set_accel(rt_scene* scene, int mode) {
         if (rc != RT_OK) return fail(rc, "BVH build failed (scene outside the filter's ranges?)");
     }
     scene->accel = mode;
+    return RT_OK;
+}
+
+int rt_ctab_candidates(const float* tri_v, int n, int n_surf, const int32_t* surf, const float* orig, const float* dir,
+                       int n_rays, uint64_t* masks, int64_t* stats) {
+    if (!tri_v || n <= 0 || n > 64 || n_surf <= 0 || n_surf > n) return fail(RT_E_INVALID, "need 1 to 64 triangles");
+    if (n_rays < 0 || (n_rays > 0 && (!surf || !orig || !dir || !masks))) return fail(RT_E_INVALID, "missing ray arrays");
+    std::vector<float4> isect((size_t)n * rt::kIsectF4);
+    double vmax = 0.0;
+    for (int i = 0; i < n; ++i) isect_record(tri_v + (size_t)i * 9, &isect[(size_t)i * 3]);
+    for (int k = 0; k < n * 9; ++k) vmax = fmax(vmax, fabs((double)tri_v[k]));
+    // the scene's origin bound, as rt_scene_create gives the matrix-core image and the table
+    const double mf_bound = (double)round_up(vmax * (1.0 + ldexp(1.0, -10)) + ldexp(1.0, -10));
+    rt::CtabHost h;
+    if (!rt::ctab_build(isect.data(), n, n_surf, mf_bound, rt::kCtabTsMin, &h))
+        return fail(RT_E_UNSUPPORTED, "candidate table build failed");
+    for (int r = 0; r < n_rays; ++r) masks[r] = rt::ctab_lookup(h, surf[r], orig + (size_t)r * 3, dir + (size_t)r * 3);
+    if (stats) {
+        int64_t bits = 0;
+        for (uint64_t m : h.masks) bits += __builtin_popcountll(m);
+        int64_t gbits = 0;
+        for (uint64_t m : h.graze) gbits += __builtin_popcountll(m);
+        stats[0] = h.n_patch;
+        stats[1] = h.patches_all;
+        stats[2] = bits;
+        stats[3] = gbits;
+    }
     return RT_OK;
 }
 
@@ -954,6 +1039,8 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
     float* d_out = nullptr;
     unsigned long long* d_casts = nullptr;
     const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
+    rc = scene_ensure_ctab(scene, params);
+    if (rc != RT_OK) return rc;
     hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
     if (e == hipSuccess) e = hipMalloc(&d_out, out_bytes);
     if (e == hipSuccess) e = hipMalloc(&d_casts, sizeof(unsigned long long));
@@ -1004,6 +1091,8 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     const rt::BlockDesc* d_blocks = nullptr;
     int n_blocks = 0;
     rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
+    if (rc != RT_OK) return rc;
+    rc = scene_ensure_ctab(scene, params);
     if (rc != RT_OK) return rc;
     rt::RenderLaunch a = make_launch(scene, cam, params);
     a.blocks = d_blocks;

@@ -125,6 +125,40 @@ struct BvhHost {
 bool bvh_build(const float4* isect, int n, BvhHost* out);
 std::string bvh_check(const float4* isect, int n, const BvhHost& h);
 
+// Bounce-ray candidate table (rt_ctab.cpp, rt_trace.hpp closest_hit_ctab): hit rule 0, scenes
+// of at most 64 triangles, t_scale >= ts_min.  A bounce ray leaving surface s from origin o in
+// direction d: the patch of o in the 2D grid over s (its frame tri[4 s .. 4 s + 3]:
+// {O', 1 / cell}, {U, n_u}, {V, n_v}, {N, first patch}; |N.(o - O')| <= h_run) and the cube-map
+// bin of d (6 x kCtabBins^2; d in s's hemisphere, d.N >= -kCtabHemi) -> masks[patch][face][iu][iv], the
+// triangles the ray may pass the
+// exact test of; OR-ed with graze[face][gu][gv] (6 x kCtabGraze^2) and, where |d.N| < cop_th,
+// with cop[s] (the triangles coplanar with s).  About kCtabPatches patches over the scene.
+#ifndef RT_CTAB_PATCHES
+#define RT_CTAB_PATCHES 4096
+#endif
+#ifndef RT_CTAB_BINS
+#define RT_CTAB_BINS 16
+#endif
+#ifndef RT_CTAB_GRAZE
+#define RT_CTAB_GRAZE 256
+#endif
+constexpr int kCtabPatches = RT_CTAB_PATCHES;
+constexpr int kCtabBins = RT_CTAB_BINS;
+constexpr int kCtabGraze = RT_CTAB_GRAZE;
+constexpr float kCtabTsMin = 256.0f;  // the smallest t_scale the table serves
+constexpr float kCtabHemi = 2e-6f;    // directions with d.N_s < -kCtabHemi (off s's hemisphere) keep every triangle
+struct CtabHost {
+    int n_tri = 0, n_surf = 0, n_patch = 0;
+    int patches_all = 0;  // patches off their triangle (every triangle kept)
+    float ts_min = 0.f, h_run = 0.f;
+    float cop_th = 0.f;           // |d.N_s| below which the triangles coplanar with s join
+    std::vector<float4> tri;      // [n_surf][4]
+    std::vector<uint64_t> cop;    // [n_surf]: the triangles coplanar with s
+    std::vector<uint64_t> masks, graze;
+};
+bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min, CtabHost* out);
+uint64_t ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3]);
+
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
     float4* shade = nullptr;   // n_tri * kShadeF4
@@ -144,6 +178,16 @@ struct DeviceScene {
     const int32_t* bvh_dlist_cam = nullptr;
     float bvh_B_lists = 0.0f;
     float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f;
+    // bounce-ray candidate table (CtabHost; nullptr: none)
+    const unsigned long long* ctab = nullptr;
+    const unsigned long long* ctab_graze = nullptr;
+    const float4* ctab_tri = nullptr;
+    const unsigned long long* ctab_cop = nullptr;
+    float ctab_h = 0.0f;     // CtabHost::h_run
+    float ctab_ts_min = 0.0f;
+    float ctab_cop_th = 0.0f;
+    int ctab_bins = 0, ctab_graze_n = 0;  // the build's kCtabBins / kCtabGraze (the kernels use the
+                                          // table only if theirs agree)
     int n_surf = 0;
     int n_tri = 0;
 };

@@ -568,6 +568,9 @@ constexpr int kPsFields = 4;
 #ifndef RT_PS_STEAL
 #define RT_PS_STEAL 1  // 0: each lane bounces only its own samples (A/B builds)
 #endif
+#ifndef RT_PS_CTAB
+#define RT_PS_CTAB 1  // 0: k_render_ps's bounce casts on the matrix-core image even with a candidate table (A/B)
+#endif
 #ifndef RT_PS_LIGHT_SPLIT
 #define RT_PS_LIGHT_SPLIT 1  // 0: terminal casts always run the full closest hit (A/B builds)
 #endif
@@ -824,6 +827,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #endif
     // the bounce casts on the matrix cores when the scene has the image (wave-uniform)
     const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
+    // scenes of at most 64 triangles: the candidates from the scene's table (rt_ctab.cpp) instead
+    // of the image's masks (wave-uniform)
+    const bool use_ctab = RT_PS_CTAB && MF == 1 && RULE == 0 && ms.ctab != nullptr && a.t_scale >= ms.ctab_ts_min &&
+                          ms.ctab_bins == kCtabBins && ms.ctab_graze_n == kCtabGraze;
     // the next direction from the surface hit (pos, hit_tri) at bounce depth dep: cos theta
     // and the ray (o = pos + eps sd, d = normalize(sd)), sampled with the path's Philox draw
     auto shade_hit = [&](int dep, float* cos_out, f3* o_out, f3* d_out) {
@@ -906,7 +913,9 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         uint64_t tm = tb;
 #endif
         Hit h;
-        if (use_mf)
+        if (use_ctab)
+            h = closest_hit_ctab<RULE>(ms, s_tri, o, d, a.t_scale, live, wl);
+        else if (use_mf)
 #if RT_PROF
             h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl, nullptr, &tm);
 #else

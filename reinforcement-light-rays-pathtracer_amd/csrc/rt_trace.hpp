@@ -821,6 +821,86 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
     return h;
 }
 
+// The candidates of a bounce ray leaving surface `surf` (rt_ctab.cpp; hit rule 0, scenes of
+// at most 64 triangles, t_scale >= ctab_ts_min): the mask of its (origin patch, direction
+// bin) OR that of its grazing bin OR, for a direction within ctab_cop_th of the surface's
+// plane, the triangles coplanar with it -- every other triangle fails the exact test --
+// or every triangle where the table does not apply (origin off the surface's plane or grid,
+// a non-unit or non-finite direction).  rt_ctab.cpp ctab_lookup is the same lookup on the
+// host.
+__device__ __forceinline__ uint64_t ctab_candidates(const DeviceScene& s, int surf, f3 o, f3 d) {
+    const uint64_t all = (s.n_tri >= 64) ? ~0ull : ((1ull << s.n_tri) - 1ull);
+    if (surf < 0 || surf >= s.n_surf) return all;
+    const float4 R0 = s.ctab_tri[surf * 4 + 0], R1 = s.ctab_tri[surf * 4 + 1];
+    const float4 R2 = s.ctab_tri[surf * 4 + 2], R3 = s.ctab_tri[surf * 4 + 3];
+    const float bx = o.x - R0.x, by = o.y - R0.y, bz = o.z - R0.z;
+    const float w = (bx * R3.x + by * R3.y) + bz * R3.z;
+    const float pu = ((bx * R1.x + by * R1.y) + bz * R1.z) * R0.w;
+    const float pv = ((bx * R2.x + by * R2.y) + bz * R2.z) * R0.w;
+    const int nu = __float_as_int(R1.w), nv = __float_as_int(R2.w), base = __float_as_int(R3.w);
+    const float len2 = fmaf(d.x, d.x, fmaf(d.y, d.y, d.z * d.z));
+    const float cn = (d.x * R3.x + d.y * R3.y) + d.z * R3.z;  // R3: the surface's shading normal
+    const bool in = (fabsf(w) <= s.ctab_h) & (pu >= 0.0f) & (pu < (float)nu) & (pv >= 0.0f) & (pv < (float)nv) &
+                    (len2 >= 1.0f - 0x1p-20f) & (len2 <= 1.0f + 0x1p-20f) & (cn >= -kCtabHemi);
+    if (!in) return all;
+    // cube-map face: the axis of the largest |d_i| (x before y before z on ties), u, v the next two
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    const bool fx = (ax >= ay) & (ax >= az), fy = !fx & (ay >= az);
+    const float dm = fx ? d.x : (fy ? d.y : d.z);
+    const float da = fx ? d.y : (fy ? d.z : d.x);
+    const float db = fx ? d.z : (fy ? d.x : d.y);
+    const int f = (fx ? 0 : (fy ? 2 : 4)) + (dm < 0.0f ? 1 : 0);
+    const float r = __builtin_amdgcn_rcpf(fabsf(dm));
+    const float u1 = da * r + 1.0f, v1 = db * r + 1.0f;  // (the build contracts nothing: two roundings)
+    const int iu = min(kCtabBins - 1, max(0, (int)(u1 * (0.5f * kCtabBins))));
+    const int iv = min(kCtabBins - 1, max(0, (int)(v1 * (0.5f * kCtabBins))));
+    const int gu = min(kCtabGraze - 1, max(0, (int)(u1 * (0.5f * kCtabGraze))));
+    const int gv = min(kCtabGraze - 1, max(0, (int)(v1 * (0.5f * kCtabGraze))));
+    const int patch = base + (int)pu * nv + (int)pv;
+    // the triangles coplanar with the surface join only near its plane's great circle
+    const uint64_t cop = (fabsf(cn) < s.ctab_cop_th) ? s.ctab_cop[surf] : 0ull;
+    return s.ctab[(size_t)patch * (6 * kCtabBins * kCtabBins) + (f * kCtabBins + iu) * kCtabBins + iv] |
+           s.ctab_graze[(f * kCtabGraze + gu) * kCtabGraze + gv] | cop;
+}
+
+#ifndef RT_CTAB_OWN
+#define RT_CTAB_OWN 3  // candidates each lane tests on its own lane before the shared exact phase (Cornell
+                       // 512^2 x 256: 1 / 3 / 5 -> 3.04 / 2.90 / 2.96 ms with 8x8 bins, profiles/r5u)
+#endif
+template <int RULE>
+__device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, int surf, f3 o, f3 d, float t_scale,
+                                                bool active, float* wl) {
+    const float nDx = -(d.x * t_scale);
+    const float nDy = -(d.y * t_scale);
+    const float nDz = -(d.z * t_scale);
+    const int lane = threadIdx.x & 63;
+    // the lane's ray for the shared exact phase (rows 0-5 of wl, as closest_hit_mf parks it)
+    wl[0 * 64 + lane] = o.x;
+    wl[1 * 64 + lane] = o.y;
+    wl[2 * 64 + lane] = o.z;
+    wl[3 * 64 + lane] = nDx;
+    wl[4 * 64 + lane] = nDy;
+    wl[5 * 64 + lane] = nDz;
+    Hit h;
+    h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
+    h.tri = -1;
+    uint64_t F = active ? ctab_candidates(s, surf, o, d) : 0ull;
+#pragma unroll
+    for (int k = 0; k < RT_CTAB_OWN; ++k) {  // the lane's first candidates on its own lane
+        if (F != 0ull) {
+            const int b = __builtin_ctzll(F);
+            const float t = exact_tv<RULE>(s.isect, b, o, nDx, nDy, nDz);
+            if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
+                h.t = t;
+                h.tri = b;
+            }
+            F &= F - 1ull;
+        }
+    }
+    mf_exact_wave<RULE>(s.isect, 0, F, o, nDx, nDy, nDz, wl, lane, h);
+    return h;
+}
+
 #ifndef RT_FILTER
 #define RT_FILTER 1  // 0: always the single-phase scan (A/B builds)
 #endif

@@ -48,6 +48,7 @@ EXPORTS = (
     "rt_scene_create", "rt_scene_destroy", "rt_scene_normals",
     "rt_intersect", "rt_intersect_device", "rt_intersect_method", "rt_render", "rt_render_tiles_device",
     "rt_pack_argb", "rt_save_bmp", "rt_save_png", "rt_selftest", "rt_filter_build", "rt_rect_candidates", "rt_cull_masks_device",
+    "rt_ctab_candidates",
     "rt_dynet_read", "rt_dynet_write", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_set_mlp", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
@@ -127,6 +128,7 @@ def _declare(lib):
                                      _U64P, ctypes.POINTER(ctypes.c_int64)]),
         "rt_rect_candidates": (i, [_FP, i, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
                                    _U64P]),
+        "rt_ctab_candidates": (i, [_FP, i, i, _IP, _FP, _FP, i, _U64P, ctypes.POINTER(ctypes.c_int64)]),
         "rt_dynet_read": (i, [ctypes.c_char_p, i, _IP, _IP, _FP, ctypes.POINTER(i),
                               ctypes.POINTER(ctypes.c_int64)]),
         "rt_dynet_write": (i, [ctypes.c_char_p, i, _IP, _IP, _FP]),

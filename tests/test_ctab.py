@@ -1,0 +1,128 @@
+"""The bounce-ray candidate table of the CPU-preset kernel (rt_ctab.cpp; k_render_ps's bounce
+casts take their candidates from it).
+
+The table is sound if every triangle that passes the reference's exact test for a bounce ray
+(Triangle::intersects under the CPU engine's hit rule, CPU/rays/ray.cpp:14-28, restated in
+oracle/: orc_pass_masks) is among the ray's candidates.  CPU: the host lookup
+(rt_ctab_candidates, the kernel's operations) against the oracle's pass sets on rays from
+the scenes' surfaces -- sampled as the kernel samples them, aimed at vertices and edges, and
+nearly parallel to some triangle's plane -- at every t_scale the table serves.  GPU: the
+renders of k_render_ps that use it are bit-exact against the oracle (test_gpu_parity.py and
+the bench line's whole-frame check).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import MODELS
+
+
+def _scene(rtmi_mod, kind):
+    if kind == "cornell_cpu":
+        g = rtmi_mod.cornell_geometry(0)
+    elif kind == "cornell_gpu":
+        g = rtmi_mod.cornell_geometry(1)
+    else:
+        g = rtmi_mod.obj_geometry(os.path.join(MODELS, kind + ".obj"), kind)
+    return np.ascontiguousarray(g.all_triangles(), np.float32), g.n_surf
+
+
+def _frame(n):
+    t = np.array([n[2], 0.0, -n[0]]) if abs(n[0]) > abs(n[1]) else np.array([0.0, -n[2], n[1]])
+    t = t / np.linalg.norm(t)
+    return t, np.cross(n, t)
+
+
+def bounce_rays(tri, n_surf, n, seed):
+    """(surf, origin, direction, kind) of n rays leaving random surface points as the kernel
+    forms them: o = pos + 1e-5 sd, d = sd / |sd| in float32 (kind 0: uniform hemisphere, 1: at
+    a vertex of the scene, 2: nearly parallel to some triangle's plane, 3: nearly parallel to
+    the origin's own plane)"""
+    rng = np.random.default_rng(seed)
+    v = tri[:n_surf].reshape(-1, 3, 3).astype(np.float64)
+    N = np.cross(v[:, 2] - v[:, 0], v[:, 1] - v[:, 0])
+    area = 0.5 * np.linalg.norm(N, axis=1)
+    N /= np.linalg.norm(N, axis=1, keepdims=True)
+    j = rng.choice(n_surf, n, p=area / area.sum())
+    a, b = rng.random(n), rng.random(n)
+    f = a + b > 1
+    a[f], b[f] = 1 - a[f], 1 - b[f]
+    pos = (v[j, 0] + a[:, None] * (v[j, 1] - v[j, 0]) + b[:, None] * (v[j, 2] - v[j, 0])).astype(np.float32)
+    allv = tri.reshape(-1, 3).astype(np.float64)
+    kind = rng.integers(0, 4, n)
+    sd = np.zeros((n, 3))
+    for i in range(n):
+        nn = N[j[i]]
+        if kind[i] == 0:
+            T, B = _frame(nn)
+            r1, r2 = rng.random(), rng.random()
+            st = np.sqrt(max(0.0, 1 - r1 * r1))
+            s = st * np.cos(2 * np.pi * r2) * B + r1 * nn + st * np.sin(2 * np.pi * r2) * T
+        elif kind[i] == 1:
+            s = allv[rng.integers(0, len(allv))] - pos[i] + rng.normal(size=3) * 10.0 ** rng.uniform(-7, -3)
+        else:
+            k = rng.integers(0, len(tri)) if kind[i] == 2 else j[i]
+            vk = tri[k].reshape(3, 3).astype(np.float64)
+            nk = np.cross(vk[1] - vk[0], vk[2] - vk[0])
+            nk /= np.linalg.norm(nk)
+            T, B = _frame(nk)
+            ph = 2 * np.pi * rng.random()
+            s = np.cos(ph) * T + np.sin(ph) * B + nk * abs(rng.normal()) * 10.0 ** rng.uniform(-7, -1.5)
+        if np.dot(s, nn) < 0:
+            s = -s
+        sd[i] = s / np.linalg.norm(s)
+    sd = sd.astype(np.float32)
+    o = (pos + np.float32(1e-5) * sd).astype(np.float32)
+    ln = np.sqrt((sd[:, 0] * sd[:, 0] + sd[:, 1] * sd[:, 1]) + sd[:, 2] * sd[:, 2]).astype(np.float32)
+    d = (sd / ln[:, None]).astype(np.float32)
+    return j.astype(np.int32), o, d, kind
+
+
+def _popcount(m):
+    return np.array([bin(int(x)).count("1") for x in m])
+
+
+@pytest.mark.parametrize("kind", ["cornell_cpu", "cornell_gpu", "door_room"])
+def test_ctab_keeps_every_pass(rtmi_mod, oracle_mod, kind):
+    tri, n_surf = _scene(rtmi_mod, kind)
+    surf, o, d, rk = bounce_rays(tri, n_surf, 12000, seed=7)
+    cand, stats = rtmi_mod.ctab_candidates(tri, n_surf, surf, o, d)
+    assert stats[0] > 0 and stats[2] > 0
+    for ts in (256.0, 512.0, 720.0, 4096.0):
+        passes = oracle_mod.pass_masks(tri, o, d, ts, 0)[:, 0]
+        missed = passes & ~cand
+        bad = np.nonzero(missed)[0]
+        assert bad.size == 0, (f"t_scale {ts}: {bad.size} rays miss a passing triangle, e.g. ray {bad[0]} "
+                               f"(surface {surf[bad[0]]}, kind {rk[bad[0]]}) triangles {int(missed[bad[0]]):#x}")
+    # and the table culls: a bounce ray keeps a few of the scene's triangles
+    pc = _popcount(cand[rk == 0])
+    assert pc.mean() < 0.2 * tri.shape[0], pc.mean()
+
+
+def test_ctab_keeps_every_triangle_outside_its_domain(rtmi_mod):
+    tri, n_surf = _scene(rtmi_mod, "cornell_cpu")
+    surf, o, d, _ = bounce_rays(tri, n_surf, 8, seed=3)
+    allbits = (1 << tri.shape[0]) - 1
+    # an origin off its surface's plane, a surface index out of range, a non-unit direction,
+    # a non-finite origin
+    o2 = o.copy()
+    o2[0] += np.float32(1e-3) * np.asarray([1.0, 1.0, 1.0], np.float32)
+    s2 = surf.copy()
+    s2[1] = -1
+    s2[2] = n_surf
+    d2 = d.copy()
+    d2[3] *= np.float32(1.01)
+    o2[4, 0] = np.nan
+    cand, _ = rtmi_mod.ctab_candidates(tri, n_surf, s2, o2, d2)
+    for r in range(5):
+        assert int(cand[r]) == allbits, r
+    assert all(int(c) != allbits for c in cand[5:])
+
+
+def test_ctab_refuses_large_scenes(rtmi_mod):
+    tri, n_surf = _scene(rtmi_mod, "archway")
+    assert tri.shape[0] > 64
+    with pytest.raises(rtmi_mod.RtError):
+        rtmi_mod.ctab_candidates(tri, n_surf, np.zeros(1, np.int32), np.zeros((1, 3), np.float32),
+                                 np.asarray([[0.0, 0.0, 1.0]], np.float32))
