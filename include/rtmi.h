@@ -471,19 +471,20 @@ int rt_rect_candidates(const float* filt, int n_tri, const rt_camera* cam, const
  * out on entry, words written on return. */
 int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt_params* params,
                          int x0, int y0, int w, int h, uint64_t* out, int64_t* n_words);
-/* Host-side check of the bounce-ray candidate table (rt_scene_create builds it for scenes of
- * at most 64 triangles; k_render_ps's bounce casts take their candidates from it under the
- * CPU engine's hit rule, t_scale >= 256): for the triangle soup tri_v (n <= 64, the first
- * n_surf surfaces: the rt_scene_create order) build the table and look up each ray (surf: the
- * surface its origin lies on, orig, dir: n_rays x 3, dir unit length) as the kernel does:
- * bit i of masks[r] = triangle i is a candidate of ray r; every other triangle fails the
- * exact test (hit rule RT_HIT_RULE_CPU, t_scale >= 256) for it (rays the table does not cover
- * get every triangle).  stats (optional, 4 entries): patches, patches kept whole, candidate
- * bits over all (patch, bin) entries, grazing-table bits.  Replaces no reference interface:
- * tests check it against the CPU restatement's pass sets of Triangle::intersects
- * (CPU/rays/ray.cpp:14-28). */
-int rt_ctab_candidates(const float* tri_v, int n, int n_surf, const int32_t* surf, const float* orig, const float* dir,
-                       int n_rays, uint64_t* masks, int64_t* stats);
+/* Host-side check of the bounce-ray candidate table (rt_ctab.cpp): a render builds it on first
+ * use for a scene of at most 256 triangles -- hit rule RT_HIT_RULE_CPU (k_render_ps's bounce
+ * casts, t_scale >= 256) or RT_HIT_RULE_GPU (the DQN renderer's bounce casts) -- and the bounce
+ * casts take their candidates from it.  For the triangle soup tri_v (n <= 256, the first n_surf
+ * surfaces: the rt_scene_create order) build the table of `hit_rule` and look up each ray
+ * (surf: the surface its origin lies on, orig, dir: n_rays x 3, dir unit length) as the kernels
+ * do: bit i % 64 of masks[r * words + i / 64] (words = ceil(n / 64)) = triangle i is a
+ * candidate of ray r; every other triangle fails the exact test under that rule (rule CPU:
+ * t_scale >= 256) for it (rays the table does not cover get every triangle).  stats (optional,
+ * 4 entries): patches, patches kept whole, candidate bits over all (patch, bin) entries,
+ * grazing-table bits.  Replaces no reference interface: tests check it against the CPU
+ * restatement's pass sets of Triangle::intersects (CPU/rays/ray.cpp:14-28; GPU/rays/ray.cu:63-64). */
+int rt_ctab_candidates(const float* tri_v, int n, int n_surf, int hit_rule, const int32_t* surf, const float* orig,
+                       const float* dir, int n_rays, uint64_t* masks, int64_t* stats);
 
 /* Live kernel timing (no reference counterpart; bench.py's roofline): while enabled, every
  * launch of the kernel families below is bracketed by a HIP event pair on its own launch

@@ -81,7 +81,7 @@ struct rt_scene {
     int32_t* d_dir[3] = {nullptr, nullptr, nullptr};           // starts (2 sets), list, camera list
     // bounce-ray candidate table (rt_ctab.cpp): built on the first CPU-preset render that can
     // use it (scene_ensure_ctab), its device arrays in dev.ctab*
-    bool ctab_tried = false;
+    bool ctab_tried[2] = {false, false};  // per hit rule
 };
 
 namespace {
@@ -294,23 +294,26 @@ int check_params(const rt_params* p) {
 
 void isect_record(const float* v, float4* out);
 
-// The bounce-ray candidate table of a scene (rt_ctab.cpp), built and uploaded once, on the
-// first render that can use it: the CPU engine's hit rule, t_scale >= kCtabTsMin, a scene of at
-// most 64 triangles with the matrix-core image (whose origin bound it shares).  A lazily
-// built cache of the scene (hence the const_cast); RT_CTAB=0 leaves the bounce casts on the
-// image's masks (A/B builds).  A scene the table cannot be built for keeps the image.
-int scene_ensure_ctab(const rt_scene* scene, const rt_params* p) {
+// The bounce-ray candidate table of a scene for hit rule `rule` (rt_ctab.cpp), built and
+// uploaded once, on the first render that can use it: scenes of at most 256 triangles with
+// the matrix-core image (whose origin bound it shares); rule 0 serves t_scale >= kCtabTsMin.
+// A lazily built cache of the scene (hence the const_cast); RT_CTAB=0 leaves the bounce
+// casts on the image's masks (A/B builds).  A scene the table cannot be built for keeps
+// the image.
+}  // namespace
+namespace rt {
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
     rt_scene* sc = const_cast<rt_scene*>(scene);
-    if (sc->ctab_tried || p->preset != RT_PRESET_CPU || p->hit_rule != RT_HIT_RULE_CPU || !(p->t_scale >= rt::kCtabTsMin))
-        return RT_OK;
-    sc->ctab_tried = true;
+    if (rule != 0 && rule != 1) return RT_OK;
+    if (sc->ctab_tried[rule] || (rule == 0 && !(t_scale >= kCtabTsMin))) return RT_OK;
+    sc->ctab_tried[rule] = true;
     static const bool ctab_on = getenv("RT_CTAB") == nullptr || atoi(getenv("RT_CTAB")) != 0;
     const int n = sc->dev.n_tri, n_surf = sc->dev.n_surf;
-    if (!ctab_on || sc->dev.mf_frag == nullptr || n > 64 || n_surf <= 0) return RT_OK;
-    std::vector<float4> isect((size_t)n * rt::kIsectF4);
+    if (!ctab_on || sc->dev.mf_frag == nullptr || n > 64 * kCtabMaxWords || n_surf <= 0) return RT_OK;
+    std::vector<float4> isect((size_t)n * kIsectF4);
     for (int i = 0; i < n; ++i) isect_record(sc->tri.data() + (size_t)i * 9, &isect[(size_t)i * 3]);
-    rt::CtabHost ct;
-    if (!rt::ctab_build(isect.data(), n, n_surf, (double)sc->dev.mf_bound, rt::kCtabTsMin, &ct)) return RT_OK;
+    CtabHost ct;
+    if (!ctab_build(isect.data(), n, n_surf, (double)sc->dev.mf_bound, rule, kCtabTsMin, &ct)) return RT_OK;
     int rc = set_device(sc->ctx);
     if (rc != RT_OK) return rc;
     unsigned long long *dm = nullptr, *dg = nullptr, *dc = nullptr;
@@ -330,17 +333,21 @@ int scene_ensure_ctab(const rt_scene* scene, const rt_params* p) {
         if (dt) (void)hipFree(dt);
         return fail(RT_E_HIP, "candidate table upload failed: %s", hipGetErrorString(e));
     }
-    sc->dev.ctab = dm;
-    sc->dev.ctab_graze = dg;
-    sc->dev.ctab_cop = dc;
-    sc->dev.ctab_tri = dt;
-    sc->dev.ctab_h = ct.h_run;
-    sc->dev.ctab_ts_min = ct.ts_min;
-    sc->dev.ctab_cop_th = ct.cop_th;
-    sc->dev.ctab_bins = rt::kCtabBins;
-    sc->dev.ctab_graze_n = rt::kCtabGraze;
+    CtabDev& t = sc->dev.ctab[rule];
+    t.masks = dm;
+    t.graze = dg;
+    t.cop = dc;
+    t.tri = dt;
+    t.h = ct.h_run;
+    t.ts_min = ct.ts_min;
+    t.cop_th = ct.cop_th;
+    t.words = ct.words;
+    t.bins = kCtabBins;
+    t.graze_n = kCtabGraze;
     return RT_OK;
 }
+}  // namespace rt
+namespace {
 
 rt::RenderLaunch make_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p) {
     rt::RenderLaunch a;
@@ -789,10 +796,12 @@ int rt_scene_destroy(rt_scene* scene) {
     (void)hipFree(scene->dev.code_gpu);
     if (scene->dev.filt) (void)hipFree(scene->dev.filt);
     if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
-    if (scene->dev.ctab) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab));
-    if (scene->dev.ctab_graze) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab_graze));
-    if (scene->dev.ctab_tri) (void)hipFree(const_cast<float4*>(scene->dev.ctab_tri));
-    if (scene->dev.ctab_cop) (void)hipFree(const_cast<unsigned long long*>(scene->dev.ctab_cop));
+    for (const rt::CtabDev& t : scene->dev.ctab) {
+        if (t.masks) (void)hipFree(const_cast<unsigned long long*>(t.masks));
+        if (t.graze) (void)hipFree(const_cast<unsigned long long*>(t.graze));
+        if (t.cop) (void)hipFree(const_cast<unsigned long long*>(t.cop));
+        if (t.tri) (void)hipFree(const_cast<float4*>(t.tri));
+    }
     scene_free_bvh(scene);
     delete scene;
     return RT_OK;
@@ -812,9 +821,11 @@ int rt_scene_set_accel(rt_scene* scene, int mode) {
     return RT_OK;
 }
 
-int rt_ctab_candidates(const float* tri_v, int n, int n_surf, const int32_t* surf, const float* orig, const float* dir,
-                       int n_rays, uint64_t* masks, int64_t* stats) {
-    if (!tri_v || n <= 0 || n > 64 || n_surf <= 0 || n_surf > n) return fail(RT_E_INVALID, "need 1 to 64 triangles");
+int rt_ctab_candidates(const float* tri_v, int n, int n_surf, int hit_rule, const int32_t* surf, const float* orig,
+                       const float* dir, int n_rays, uint64_t* masks, int64_t* stats) {
+    if (!tri_v || n <= 0 || n > 64 * rt::kCtabMaxWords || n_surf <= 0 || n_surf > n)
+        return fail(RT_E_INVALID, "need 1 to %d triangles", 64 * rt::kCtabMaxWords);
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit rule %d", hit_rule);
     if (n_rays < 0 || (n_rays > 0 && (!surf || !orig || !dir || !masks))) return fail(RT_E_INVALID, "missing ray arrays");
     std::vector<float4> isect((size_t)n * rt::kIsectF4);
     double vmax = 0.0;
@@ -823,9 +834,10 @@ int rt_ctab_candidates(const float* tri_v, int n, int n_surf, const int32_t* sur
     // the scene's origin bound, as rt_scene_create gives the matrix-core image and the table
     const double mf_bound = (double)round_up(vmax * (1.0 + ldexp(1.0, -10)) + ldexp(1.0, -10));
     rt::CtabHost h;
-    if (!rt::ctab_build(isect.data(), n, n_surf, mf_bound, rt::kCtabTsMin, &h))
+    if (!rt::ctab_build(isect.data(), n, n_surf, mf_bound, hit_rule, rt::kCtabTsMin, &h))
         return fail(RT_E_UNSUPPORTED, "candidate table build failed");
-    for (int r = 0; r < n_rays; ++r) masks[r] = rt::ctab_lookup(h, surf[r], orig + (size_t)r * 3, dir + (size_t)r * 3);
+    for (int r = 0; r < n_rays; ++r)
+        rt::ctab_lookup(h, surf[r], orig + (size_t)r * 3, dir + (size_t)r * 3, masks + (size_t)r * h.words);
     if (stats) {
         int64_t bits = 0;
         for (uint64_t m : h.masks) bits += __builtin_popcountll(m);
@@ -1039,7 +1051,7 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
     float* d_out = nullptr;
     unsigned long long* d_casts = nullptr;
     const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
-    rc = scene_ensure_ctab(scene, params);
+    rc = params->preset == RT_PRESET_CPU ? rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale) : RT_OK;
     if (rc != RT_OK) return rc;
     hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
     if (e == hipSuccess) e = hipMalloc(&d_out, out_bytes);
@@ -1092,7 +1104,7 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     int n_blocks = 0;
     rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
     if (rc != RT_OK) return rc;
-    rc = scene_ensure_ctab(scene, params);
+    rc = params->preset == RT_PRESET_CPU ? rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale) : RT_OK;
     if (rc != RT_OK) return rc;
     rt::RenderLaunch a = make_launch(scene, cam, params);
     a.blocks = d_blocks;

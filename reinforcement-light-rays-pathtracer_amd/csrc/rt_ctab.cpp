@@ -310,8 +310,10 @@ bool tri_rect_2d(const double p[3][2], double x0, double x1, double y0, double y
 // (DeviceScene::mf_bound; raised to every origin the patch grids accept); ts_min: the
 // smallest t_scale it serves.  Returns false if the scene is out of the filter's ranges or
 // too large.
-bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min, CtabHost* out) {
-    if (n <= 0 || n > 64 || n_surf <= 0 || n_surf > n || !(B < ldexp(1.0, 20))) return false;
+bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, double ts_min, CtabHost* out) {
+    if (n <= 0 || n > 64 * kCtabMaxWords || n_surf <= 0 || n_surf > n || !(B < ldexp(1.0, 20))) return false;
+    if (rule != 0 && rule != 1) return false;
+    const int W = (n + 63) / 64;  // mask words per entry
     std::vector<bnd::TriAlg> ta((size_t)n);
     std::vector<double> vt((size_t)n * 9);
     double vmax = 0.0;
@@ -332,7 +334,9 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
     h = CtabHost();
     h.n_tri = n;
     h.n_surf = n_surf;
-    h.ts_min = (float)ts_min;
+    h.words = W;
+    h.rule = rule;
+    h.ts_min = rule == 0 ? (float)ts_min : 0.0f;
     // the origin slab: 1e-5 |sd| off the surface (|sd| = 1 to float precision) plus the
     // rounding of the hit point and of the kernel's frame (a few 1e-7 at these coordinates)
     h.h_run = bnd::up(1.1e-5 + 1e-6 * (1.0 + vmax));
@@ -443,8 +447,11 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
         if (!(ag > 2.0 * bo.eA)) return false;
         sig[(size_t)i] = bo.EW / ag * (1.0 + 1e-9);
         const double den = ag - bo.eA;
-        // rule 0 passes t > 1e-5f (= 9.99999975e-6 > 0.99999e-5)
-        lmin[(size_t)i] = std::max(0.0, (0.99999e-5 * ts_min - bo.ET / den) / (1.0 + bo.eA / den)) * (1.0 - 1e-6);
+        // rule 0 passes t > 1e-5f (= 9.99999975e-6 > 0.99999e-5); rule 1 passes t >= 0 (no bound
+        // away from the origin)
+        lmin[(size_t)i] = rule == 0 ? std::max(0.0, (0.99999e-5 * ts_min - bo.ET / den) / (1.0 + bo.eA / den)) *
+                                          (1.0 - 1e-6)
+                                    : 0.0;
         et_n[(size_t)i] = bo.ET / t.nlen;
         for (int k = 0; k < 3; ++k) un[(size_t)i * 3 + k] = t.N[k] / t.nlen;
         for (int f = 0; f < 6; ++f)
@@ -459,10 +466,10 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                     if (mn < kThetaG) band[(size_t)i * 6 + f].set(iu * kNc + iv);
                 }
     }
-    const int per_patch = 6 * kNc * kNc;
-    const uint64_t all = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
+    const int per_patch = 6 * kNc * kNc * W;  // mask words per patch
+    auto all_word = [&](int w) { return (n - 64 * w >= 64) ? ~0ull : ((1ull << (n - 64 * w)) - 1ull); };
     h.masks.assign((size_t)n_patch * per_patch, 0ull);
-    h.cop.assign((size_t)n_surf, 0ull);
+    h.cop.assign((size_t)n_surf * W, 0ull);
     // the surfaces' patches, one surface per task on the host's threads
     std::vector<double> cop_th_s((size_t)n_surf, 0.0);
     std::vector<int> whole_s((size_t)n_surf, 0);
@@ -474,7 +481,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
         // only along directions with |d.n| < theta_j (their plane within D of every patch of
         // s, D / lambda_min < theta_g); the kernel adds them where |d.N_s| < cop_th instead
         // of through the patches' bins
-        uint64_t cop = 0ull;
+        std::vector<uint64_t> cop((size_t)W, 0ull);
         {
             // the corners of s's whole patch grid
             const double R[3][3] = {{F.U[0], F.U[1], F.U[2]}, {F.V[0], F.V[1], F.V[2]}, {F.N[0], F.N[1], F.N[2]}};
@@ -495,8 +502,17 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                 for (const auto& x : gc) dmax = std::max(dmax, fabs(x[0] * nn[0] + x[1] * nn[1] + x[2] * nn[2] - pc));
                 const double D = dmax * (1.0 + 1e-9) + 1e-12 * (1.0 + fabs(pc));
                 const double lm = lmin[(size_t)i];
+                if (rule == 1) {
+                    // rule 1 (t >= 0): the plane of s, up to rounding, may be passed right at the
+                    // origin in any direction -- a candidate of every ray leaving s
+                    if (D <= 1e-4 * (1.0 + vmax)) {
+                        cop[(size_t)(i >> 6)] |= 1ull << (i & 63);
+                        cop_th = 4.0;
+                    }
+                    continue;
+                }
                 if (!(lm > 0.0 && D / lm < kThetaG * (1.0 - 1e-6))) continue;
-                cop |= 1ull << i;
+                cop[(size_t)(i >> 6)] |= 1ull << (i & 63);
                 const bnd::Bounds bo = bnd::bounds_for(ta[(size_t)i], B);
                 const double th_j = std::max(std::max(kK * bo.EW, kThetaG * ta[(size_t)i].nlen) / ta[(size_t)i].nlen,
                                              kThetaG) * (1.0 + 1e-5);
@@ -507,7 +523,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                 cop_th = std::max(cop_th, th_j + len3d(dn) * 1.001 + 1e-6);
             }
         }
-        h.cop[(size_t)s] = cop;
+        for (int w = 0; w < W; ++w) h.cop[(size_t)s * W + w] = cop[(size_t)w];
         // the bins holding a direction of s's hemisphere (d.N_s >= -kCtabHemi: the kernel keeps
         // every triangle for the others); the rest stay empty
         Bins hemi[6];
@@ -531,7 +547,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                 const double u0 = iu * cr - mu, u1 = (iu + 1) * cr + mu;
                 const double v0 = iv * cr - mu, v1 = (iv + 1) * cr + mu;
                 if (!tri_rect_2d(F.p2, u0 - 4.0 * mu, u1 + 4.0 * mu, v0 - 4.0 * mu, v1 + 4.0 * mu)) {
-                    for (int q = 0; q < per_patch; ++q) cm[q] = all;  // off the triangle
+                    for (int q = 0; q < per_patch; ++q) cm[q] = all_word(q % W);  // off the triangle
                     ++whole_s[(size_t)s];
                     continue;
                 }
@@ -546,7 +562,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                 double co[8][3];
                 corners(P, co);
                 for (int i = 0; i < n; ++i) {
-                    if ((cop >> i) & 1ull) continue;  // the kernel's |d.N_s| test
+                    if ((cop[(size_t)(i >> 6)] >> (i & 63)) & 1ull) continue;  // the kernel's |d.N_s| test
                     const double* v = &vt[(size_t)i * 9];
                     const double* nn = &un[(size_t)i * 3];
                     const double pc = (v[0] * nn[0] + v[1] * nn[1] + v[2] * nn[2]);
@@ -590,7 +606,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                         if (regular) sweep(tg, P, lm, f, 0, hemi[f], &bins);
                         if (band_near) bins |= band[(size_t)i * 6 + f] & hemi[f];
                         for (int q = 0; q < kNc * kNc; ++q)
-                            if (bins.test(q)) cm[f * kNc * kNc + q] |= 1ull << i;
+                            if (bins.test(q)) cm[(size_t)(f * kNc * kNc + q) * W + (i >> 6)] |= 1ull << (i & 63);
                     }
                 }
             }
@@ -614,7 +630,7 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
     }
 
     // grazing bins: every triangle a direction of the bin can run along (|d.N| < K EW)
-    h.graze.assign((size_t)6 * kNg * kNg, 0ull);
+    h.graze.assign((size_t)6 * kNg * kNg * W, 0ull);
     for (int f = 0; f < 6; ++f)
         for (int iu = 0; iu < kNg; ++iu)
             for (int iv = 0; iv < kNg; ++iv) {
@@ -622,15 +638,14 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
                 const double v0 = -1.0 + 2.0 * iv / kNg - kMuDir, v1 = -1.0 + 2.0 * (iv + 1) / kNg + kMuDir;
                 double dc[3];
                 const double chord = bnd::cell_chord(f, u0, u1, v0, v1, dc);
-                uint64_t m = 0;
+                uint64_t* m = &h.graze[((size_t)(f * kNg + iu) * kNg + iv) * W];
                 for (int i = 0; i < n; ++i) {
                     const bnd::TriAlg& t = ta[(size_t)i];
                     const bnd::Bounds bo = bnd::bounds_for(t, B);
                     const double dn = fabs(dc[0] * t.N[0] + dc[1] * t.N[1] + dc[2] * t.N[2]) / t.nlen;
                     // |d.N| >= (1 - 1e-6) |N| (dn - chord) for every direction of the bin
-                    if ((dn - chord) * (1.0 - 1e-6) * t.nlen < kK * bo.EW * 1.01) m |= 1ull << i;
+                    if ((dn - chord) * (1.0 - 1e-6) * t.nlen < kK * bo.EW * 1.01) m[i >> 6] |= 1ull << (i & 63);
                 }
-                h.graze[(size_t)(f * kNg + iu) * kNg + iv] = m;
             }
     h.n_patch = n_patch;
     h.cop_th = bnd::up(cop_th);
@@ -638,11 +653,12 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min,
 }
 
 // The kernel's lookup (rt_trace.hpp ctab_candidates) on the host, with the same float
-// operations: the candidate mask of the ray (o, d) leaving surface s, or every triangle
-// where the table does not apply.
-uint64_t ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3]) {
-    const uint64_t all = (h.n_tri == 64) ? ~0ull : ((1ull << h.n_tri) - 1ull);
-    if (s < 0 || s >= h.n_surf) return all;
+// operations: the candidate mask (h.words words into out) of the ray (o, d) leaving surface
+// s, or every triangle where the table does not apply.
+void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], uint64_t* out) {
+    const int W = h.words;
+    for (int w = 0; w < W; ++w) out[w] = (h.n_tri - 64 * w >= 64) ? ~0ull : ((1ull << (h.n_tri - 64 * w)) - 1ull);
+    if (s < 0 || s >= h.n_surf) return;
     const float4 R0 = h.tri[(size_t)s * 4], R1 = h.tri[(size_t)s * 4 + 1], R2 = h.tri[(size_t)s * 4 + 2],
                  R3 = h.tri[(size_t)s * 4 + 3];
     const float bx = o[0] - R0.x, by = o[1] - R0.y, bz = o[2] - R0.z;
@@ -653,11 +669,11 @@ uint64_t ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3
     memcpy(&nu, &R1.w, 4);
     memcpy(&nv, &R2.w, 4);
     memcpy(&base, &R3.w, 4);
-    if (!(fabsf(w) <= h.h_run) || !(pu >= 0.0f) || !(pu < (float)nu) || !(pv >= 0.0f) || !(pv < (float)nv)) return all;
+    if (!(fabsf(w) <= h.h_run) || !(pu >= 0.0f) || !(pu < (float)nu) || !(pv >= 0.0f) || !(pv < (float)nv)) return;
     const float len2 = fmaf(d[0], d[0], fmaf(d[1], d[1], d[2] * d[2]));
-    if (!(len2 >= 1.0f - 0x1p-20f) || !(len2 <= 1.0f + 0x1p-20f)) return all;
+    if (!(len2 >= 1.0f - 0x1p-20f) || !(len2 <= 1.0f + 0x1p-20f)) return;
     const float cn = (d[0] * R3.x + d[1] * R3.y) + d[2] * R3.z;
-    if (!(cn >= -kCtabHemi)) return all;
+    if (!(cn >= -kCtabHemi)) return;
     const float ax = fabsf(d[0]), ay = fabsf(d[1]), az = fabsf(d[2]);
     const int m = (ax >= ay && ax >= az) ? 0 : (ay >= az ? 1 : 2);
     const float dm = d[m];
@@ -666,9 +682,10 @@ uint64_t ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3
     const float u1 = d[(m + 1) % 3] * r + 1.0f, v1 = d[(m + 2) % 3] * r + 1.0f;
     auto bin = [](float x1, int nb) { return std::min(nb - 1, std::max(0, (int)(x1 * (0.5f * (float)nb)))); };
     const int patch = base + (int)pu * nv + (int)pv;
-    const uint64_t cp = (fabsf(cn) < h.cop_th) ? h.cop[(size_t)s] : 0ull;
-    return h.masks[(size_t)patch * 6 * kNc * kNc + (size_t)(f * kNc + bin(u1, kNc)) * kNc + bin(v1, kNc)] |
-           h.graze[(size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)] | cp;
+    const bool cp = fabsf(cn) < h.cop_th;
+    const uint64_t* mm = &h.masks[((size_t)patch * 6 * kNc * kNc + (size_t)(f * kNc + bin(u1, kNc)) * kNc + bin(v1, kNc)) * W];
+    const uint64_t* gg = &h.graze[((size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)) * W];
+    for (int k = 0; k < W; ++k) out[k] = mm[k] | gg[k] | (cp ? h.cop[(size_t)s * W + k] : 0ull);
 }
 
 }  // namespace rt

@@ -812,14 +812,22 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
 // MF > 0: the cast on the matrix-core filter (closest_hit_mf: every lane of the wave
 // calls, `active` false for a lane without a ray, which then returns false untouched).
 // MF < 0: the exact BVH (large scenes, closest_hit_bvh), wl = the lane's LDS stack column.
-template <int MF>
+// BOUNCE (MF > 0): a bounce ray leaving surface `surf`, its candidates from the scene's rule-1
+// candidate table when it has one (closest_hit_ctab, rt_ctab.cpp; wave-uniform choice)
+#ifndef RT_DQN_CTAB
+#define RT_DQN_CTAB 1  // 0: the bounce casts on the matrix-core image even with a candidate table (A/B)
+#endif
+template <int MF, bool BOUNCE = false>
 __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bool active, float* wl, f3* loc_out,
-                                          int* tri_out, f3* tp) {
+                                          int* tri_out, f3* tp, int surf = -1) {
     const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
     const f3 d = normalize(dir);
     Hit h;
     if constexpr (MF > 0) {
-        h = closest_hit_mf<1, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+        if (BOUNCE && RT_DQN_CTAB && ctab_usable(a.scene.ctab[1], a.t_scale) && a.scene.ctab[1].words <= MF)
+            h = closest_hit_ctab<1, MF>(a.scene, a.scene.ctab[1], surf, o, d, a.t_scale, active, wl);
+        else
+            h = closest_hit_mf<1, false, MF>(a.scene, o, d, a.t_scale, active, wl);
         if (!active) return false;
     } else if constexpr (MF < 0) {
         if (!active) return false;
@@ -998,7 +1006,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
             tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
         }
     }
-    keep = dqn_trace<MF>(a, pos, dir, want, dqn_lane_ws<MF>(s_mfw), &loc, &ntri, &tp);
+    keep = dqn_trace<MF, true>(a, pos, dir, want, dqn_lane_ws<MF>(s_mfw), &loc, &ntri, &tp, want ? ntri : -1);
     if (i < n_act) {
         if (keep) {
             st3(a.rays.loc, rid, loc);

@@ -24,6 +24,7 @@ int set_error(int code, const char* msg);
 int ctx_device(const rt_ctx* ctx);
 const DeviceScene& scene_device(const rt_scene* s);
 DeviceScene scene_launch_view(const rt_scene* s);
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale);
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 }  // namespace rt
@@ -418,6 +419,9 @@ int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_came
     if (const char* env = getenv("RTMI_DQN_RAYS_IN_FLIGHT")) rays_in_flight = std::max(1, atoi(env));  // tests
     const int in_flight = std::max(1, std::min(p->spp, rays_in_flight / n_pix));
     int rc = ws->ensure(n_pix * in_flight);
+    if (rc != RT_OK) return rc;
+    // the bounce casts' candidate table (rule 1: the GPU engine's hit rule), built on the first render
+    rc = rt::scene_ensure_ctab(scene, 1, p->t_scale);
     if (rc != RT_OK) return rc;
     rt::DqnLaunch a;
     memset(&a, 0, sizeof(a));

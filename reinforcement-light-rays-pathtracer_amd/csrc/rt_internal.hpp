@@ -147,8 +147,11 @@ constexpr int kCtabBins = RT_CTAB_BINS;
 constexpr int kCtabGraze = RT_CTAB_GRAZE;
 constexpr float kCtabTsMin = 256.0f;  // the smallest t_scale the table serves
 constexpr float kCtabHemi = 2e-6f;    // directions with d.N_s < -kCtabHemi (off s's hemisphere) keep every triangle
+constexpr int kCtabMaxWords = 4;  // mask words per entry: scenes of at most 256 triangles
 struct CtabHost {
     int n_tri = 0, n_surf = 0, n_patch = 0;
+    int words = 1;        // ceil(n_tri / 64): masks, graze and cop hold that many words per entry
+    int rule = 0;         // the hit rule it serves (0: ts_min applies; 1: any t_scale)
     int patches_all = 0;  // patches off their triangle (every triangle kept)
     float ts_min = 0.f, h_run = 0.f;
     float cop_th = 0.f;           // |d.N_s| below which the triangles coplanar with s join
@@ -156,8 +159,19 @@ struct CtabHost {
     std::vector<uint64_t> cop;    // [n_surf]: the triangles coplanar with s
     std::vector<uint64_t> masks, graze;
 };
-bool ctab_build(const float4* isect, int n, int n_surf, double B, double ts_min, CtabHost* out);
-uint64_t ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3]);
+bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, double ts_min, CtabHost* out);
+void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], uint64_t* out);
+
+// a candidate table on the device (CtabHost's arrays and constants)
+struct CtabDev {
+    const unsigned long long* masks = nullptr;  // [patch][face][iu][iv][words]
+    const unsigned long long* graze = nullptr;  // [face][gu][gv][words]
+    const unsigned long long* cop = nullptr;    // [n_surf][words]
+    const float4* tri = nullptr;                // [n_surf][4]: the surfaces' patch frames
+    float h = 0.0f, ts_min = 0.0f, cop_th = 0.0f;
+    int words = 0;
+    int bins = 0, graze_n = 0;  // the build's kCtabBins / kCtabGraze (kernels use the table only if theirs agree)
+};
 
 struct DeviceScene {
     float4* isect = nullptr;   // n_tri * kIsectF4
@@ -178,16 +192,8 @@ struct DeviceScene {
     const int32_t* bvh_dlist_cam = nullptr;
     float bvh_B_lists = 0.0f;
     float bvh_sig_a = 0.0f, bvh_sig_b = 0.0f;
-    // bounce-ray candidate table (CtabHost; nullptr: none)
-    const unsigned long long* ctab = nullptr;
-    const unsigned long long* ctab_graze = nullptr;
-    const float4* ctab_tri = nullptr;
-    const unsigned long long* ctab_cop = nullptr;
-    float ctab_h = 0.0f;     // CtabHost::h_run
-    float ctab_ts_min = 0.0f;
-    float ctab_cop_th = 0.0f;
-    int ctab_bins = 0, ctab_graze_n = 0;  // the build's kCtabBins / kCtabGraze (the kernels use the
-                                          // table only if theirs agree)
+    // bounce-ray candidate tables (CtabHost), one per hit rule (masks nullptr: none)
+    CtabDev ctab[2];
     int n_surf = 0;
     int n_tri = 0;
 };

@@ -829,8 +829,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
     // scenes of at most 64 triangles: the candidates from the scene's table (rt_ctab.cpp) instead
     // of the image's masks (wave-uniform)
-    const bool use_ctab = RT_PS_CTAB && MF == 1 && RULE == 0 && ms.ctab != nullptr && a.t_scale >= ms.ctab_ts_min &&
-                          ms.ctab_bins == kCtabBins && ms.ctab_graze_n == kCtabGraze;
+    const bool use_ctab = RT_PS_CTAB && MF == 1 && ctab_usable(ms.ctab[RULE], a.t_scale) && ms.ctab[RULE].words == 1;
     // the next direction from the surface hit (pos, hit_tri) at bounce depth dep: cos theta
     // and the ray (o = pos + eps sd, d = normalize(sd)), sampled with the path's Philox draw
     auto shade_hit = [&](int dep, float* cos_out, f3* o_out, f3* d_out) {
@@ -914,7 +913,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #endif
         Hit h;
         if (use_ctab)
-            h = closest_hit_ctab<RULE>(ms, s_tri, o, d, a.t_scale, live, wl);
+            h = closest_hit_ctab<RULE, 1>(ms, ms.ctab[RULE], s_tri, o, d, a.t_scale, live, wl);
         else if (use_mf)
 #if RT_PROF
             h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl, nullptr, &tm);

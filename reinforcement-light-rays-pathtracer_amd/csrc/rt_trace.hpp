@@ -821,18 +821,22 @@ __device__ __forceinline__ Hit closest_hit_mf(const DeviceScene& s, f3 o, f3 d, 
     return h;
 }
 
-// The candidates of a bounce ray leaving surface `surf` (rt_ctab.cpp; hit rule 0, scenes of
-// at most 64 triangles, t_scale >= ctab_ts_min): the mask of its (origin patch, direction
-// bin) OR that of its grazing bin OR, for a direction within ctab_cop_th of the surface's
-// plane, the triangles coplanar with it -- every other triangle fails the exact test --
-// or every triangle where the table does not apply (origin off the surface's plane or grid,
-// a non-unit or non-finite direction).  rt_ctab.cpp ctab_lookup is the same lookup on the
-// host.
-__device__ __forceinline__ uint64_t ctab_candidates(const DeviceScene& s, int surf, f3 o, f3 d) {
-    const uint64_t all = (s.n_tri >= 64) ? ~0ull : ((1ull << s.n_tri) - 1ull);
-    if (surf < 0 || surf >= s.n_surf) return all;
-    const float4 R0 = s.ctab_tri[surf * 4 + 0], R1 = s.ctab_tri[surf * 4 + 1];
-    const float4 R2 = s.ctab_tri[surf * 4 + 2], R3 = s.ctab_tri[surf * 4 + 3];
+// The candidates of a bounce ray leaving surface `surf` (rt_ctab.cpp) from the table T of the
+// launch's hit rule: the mask of its (origin patch, direction bin) OR that of its grazing bin
+// OR, for a direction within T.cop_th of the surface's plane (always, under rule 1), the
+// triangles coplanar with it -- every other triangle fails the exact test for this ray -- or
+// every triangle where the table does not apply (origin off the surface's plane or grid, a
+// direction off its hemisphere, non-unit or non-finite).  F: NW >= T.words mask words (the
+// rest 0).  rt_ctab.cpp ctab_lookup is the same lookup on the host.
+template <int NW>
+__device__ __forceinline__ void ctab_candidates(const CtabDev& T, int n_tri, int n_surf, int surf, f3 o, f3 d,
+                                                uint64_t (&F)[NW]) {
+    const int W = T.words;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) F[w] = (w < W) ? ((n_tri - 64 * w >= 64) ? ~0ull : ((1ull << (n_tri - 64 * w)) - 1ull)) : 0ull;
+    if (surf < 0 || surf >= n_surf) return;
+    const float4 R0 = T.tri[surf * 4 + 0], R1 = T.tri[surf * 4 + 1];
+    const float4 R2 = T.tri[surf * 4 + 2], R3 = T.tri[surf * 4 + 3];
     const float bx = o.x - R0.x, by = o.y - R0.y, bz = o.z - R0.z;
     const float w = (bx * R3.x + by * R3.y) + bz * R3.z;
     const float pu = ((bx * R1.x + by * R1.y) + bz * R1.z) * R0.w;
@@ -840,9 +844,9 @@ __device__ __forceinline__ uint64_t ctab_candidates(const DeviceScene& s, int su
     const int nu = __float_as_int(R1.w), nv = __float_as_int(R2.w), base = __float_as_int(R3.w);
     const float len2 = fmaf(d.x, d.x, fmaf(d.y, d.y, d.z * d.z));
     const float cn = (d.x * R3.x + d.y * R3.y) + d.z * R3.z;  // R3: the surface's shading normal
-    const bool in = (fabsf(w) <= s.ctab_h) & (pu >= 0.0f) & (pu < (float)nu) & (pv >= 0.0f) & (pv < (float)nv) &
+    const bool in = (fabsf(w) <= T.h) & (pu >= 0.0f) & (pu < (float)nu) & (pv >= 0.0f) & (pv < (float)nv) &
                     (len2 >= 1.0f - 0x1p-20f) & (len2 <= 1.0f + 0x1p-20f) & (cn >= -kCtabHemi);
-    if (!in) return all;
+    if (!in) return;
     // cube-map face: the axis of the largest |d_i| (x before y before z on ties), u, v the next two
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     const bool fx = (ax >= ay) & (ax >= az), fy = !fx & (ay >= az);
@@ -857,19 +861,30 @@ __device__ __forceinline__ uint64_t ctab_candidates(const DeviceScene& s, int su
     const int gu = min(kCtabGraze - 1, max(0, (int)(u1 * (0.5f * kCtabGraze))));
     const int gv = min(kCtabGraze - 1, max(0, (int)(v1 * (0.5f * kCtabGraze))));
     const int patch = base + (int)pu * nv + (int)pv;
-    // the triangles coplanar with the surface join only near its plane's great circle
-    const uint64_t cop = (fabsf(cn) < s.ctab_cop_th) ? s.ctab_cop[surf] : 0ull;
-    return s.ctab[(size_t)patch * (6 * kCtabBins * kCtabBins) + (f * kCtabBins + iu) * kCtabBins + iv] |
-           s.ctab_graze[(f * kCtabGraze + gu) * kCtabGraze + gv] | cop;
+    const unsigned long long* mm = T.masks + ((size_t)patch * (6 * kCtabBins * kCtabBins) + (f * kCtabBins + iu) * kCtabBins + iv) * W;
+    const unsigned long long* gg = T.graze + ((size_t)(f * kCtabGraze + gu) * kCtabGraze + gv) * W;
+    // the triangles coplanar with the surface join near its plane's great circle (rule 0) or always (rule 1)
+    const bool cp = fabsf(cn) < T.cop_th;
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+        if (k < W) F[k] = mm[k] | gg[k] | (cp ? T.cop[surf * W + k] : 0ull);
 }
 
 #ifndef RT_CTAB_OWN
 #define RT_CTAB_OWN 3  // candidates each lane tests on its own lane before the shared exact phase (Cornell
-                       // 512^2 x 256: 1 / 3 / 5 -> 3.04 / 2.90 / 2.96 ms with 8x8 bins, profiles/r5u)
+                       // 512^2 x 256: 1 / 3 / 5 -> 3.04 / 2.90 / 2.96 ms with 8x8 bins, profiles/r5t)
 #endif
-template <int RULE>
-__device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, int surf, f3 o, f3 d, float t_scale,
-                                                bool active, float* wl) {
+// the table usable for a launch: built with this build's dimensions, for its t_scale
+__device__ __forceinline__ bool ctab_usable(const CtabDev& T, float t_scale) {
+    return T.masks != nullptr && T.bins == kCtabBins && T.graze_n == kCtabGraze && t_scale >= T.ts_min;
+}
+// closest_hit_mf's result for a bounce ray leaving surface `surf`, its candidates from the
+// table T (ctab_candidates): the lane's first RT_CTAB_OWN candidates on its own lane, the rest
+// shared by the wave (mf_exact_wave, per 64-triangle block).  Wave-level like closest_hit_mf
+// (`active` false: no candidates).  NW: mask words (>= T.words).
+template <int RULE, int NW>
+__device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const CtabDev& T, int surf, f3 o, f3 d,
+                                                float t_scale, bool active, float* wl) {
     const float nDx = -(d.x * t_scale);
     const float nDy = -(d.y * t_scale);
     const float nDz = -(d.z * t_scale);
@@ -884,20 +899,39 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, int surf, 
     Hit h;
     h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
     h.tri = -1;
-    uint64_t F = active ? ctab_candidates(s, surf, o, d) : 0ull;
+    uint64_t F[NW];
+    if (active) {
+        ctab_candidates<NW>(T, s.n_tri, s.n_surf, surf, o, d, F);
+    } else {
 #pragma unroll
-    for (int k = 0; k < RT_CTAB_OWN; ++k) {  // the lane's first candidates on its own lane
-        if (F != 0ull) {
-            const int b = __builtin_ctzll(F);
+        for (int k = 0; k < NW; ++k) F[k] = 0ull;
+    }
+    // the lane's first candidates (in index order) on its own lane
+#pragma unroll
+    for (int k = 0; k < RT_CTAB_OWN; ++k) {
+        int wsel = -1;
+#pragma unroll
+        for (int w = NW - 1; w >= 0; --w)
+            if (F[w] != 0ull) wsel = w;
+        if (wsel >= 0) {
+            uint64_t fw = 0ull;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (w == wsel) fw = F[w];
+            const int b = 64 * wsel + __builtin_ctzll(fw);
             const float t = exact_tv<RULE>(s.isect, b, o, nDx, nDy, nDz);
             if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
                 h.t = t;
                 h.tri = b;
             }
-            F &= F - 1ull;
+#pragma unroll
+            for (int w = 0; w < NW; ++w)
+                if (w == wsel) F[w] &= F[w] - 1ull;
         }
     }
-    mf_exact_wave<RULE>(s.isect, 0, F, o, nDx, nDy, nDz, wl, lane, h);
+#pragma unroll
+    for (int w = 0; w < NW; ++w)
+        if (64 * w < s.n_tri) mf_exact_wave<RULE>(s.isect, 64 * w, F[w], o, nDx, nDy, nDz, wl, lane, h);
     return h;
 }
 

@@ -128,7 +128,7 @@ def _declare(lib):
                                      _U64P, ctypes.POINTER(ctypes.c_int64)]),
         "rt_rect_candidates": (i, [_FP, i, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
                                    _U64P]),
-        "rt_ctab_candidates": (i, [_FP, i, i, _IP, _FP, _FP, i, _U64P, ctypes.POINTER(ctypes.c_int64)]),
+        "rt_ctab_candidates": (i, [_FP, i, i, i, _IP, _FP, _FP, i, _U64P, ctypes.POINTER(ctypes.c_int64)]),
         "rt_dynet_read": (i, [ctypes.c_char_p, i, _IP, _IP, _FP, ctypes.POINTER(i),
                               ctypes.POINTER(ctypes.c_int64)]),
         "rt_dynet_write": (i, [ctypes.c_char_p, i, _IP, _IP, _FP]),

@@ -278,19 +278,21 @@ def rect_candidates(filt: np.ndarray, cam: RtCamera, params: RtParams, px0: int,
     return bits[:n].astype(bool)
 
 
-def ctab_candidates(tri_all: np.ndarray, n_surf: int, surf: np.ndarray, orig: np.ndarray, direction: np.ndarray):
-    """The bounce-ray candidate table of k_render_ps (rt_ctab_candidates, host only): the
-    (n_rays,) uint64 candidate masks of rays leaving surfaces `surf` from `orig` along unit
+def ctab_candidates(tri_all: np.ndarray, n_surf: int, surf: np.ndarray, orig: np.ndarray, direction: np.ndarray,
+                    hit_rule: int = 0):
+    """The bounce-ray candidate table of the renderers (rt_ctab_candidates, host only): the
+    (n_rays, words) uint64 candidate masks of rays leaving surfaces `surf` from `orig` along unit
     `direction`, and the table's stats (patches, patches kept whole, candidate bits, grazing
-    bits).  Every triangle outside a ray's mask fails the exact test (CPU hit rule,
-    t_scale >= 256) for it."""
+    bits).  Every triangle outside a ray's mask fails the exact test (hit rule `hit_rule`; the
+    CPU rule at t_scale >= 256) for it."""
     t = np.ascontiguousarray(tri_all, np.float32).reshape(-1, 9)
     s = np.ascontiguousarray(surf, np.int32).ravel()
     o = np.ascontiguousarray(orig, np.float32).reshape(-1, 3)
     d = np.ascontiguousarray(direction, np.float32).reshape(-1, 3)
-    out = np.zeros(o.shape[0], np.uint64)
+    words = (t.shape[0] + 63) // 64
+    out = np.zeros((o.shape[0], words), np.uint64)
     stats = np.zeros(4, np.int64)
-    check(lib().rt_ctab_candidates(_fp(t), t.shape[0], n_surf, _ip(s), _fp(o), _fp(d), o.shape[0],
+    check(lib().rt_ctab_candidates(_fp(t), t.shape[0], n_surf, hit_rule, _ip(s), _fp(o), _fp(d), o.shape[0],
                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
                                    stats.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
     return out, stats

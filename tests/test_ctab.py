@@ -1,14 +1,14 @@
-"""The bounce-ray candidate table of the CPU-preset kernel (rt_ctab.cpp; k_render_ps's bounce
-casts take their candidates from it).
+"""The bounce-ray candidate table (rt_ctab.cpp): k_render_ps's bounce casts (the CPU engine's
+hit rule) and the DQN renderer's (the GPU engine's) take their candidates from it.
 
 The table is sound if every triangle that passes the reference's exact test for a bounce ray
-(Triangle::intersects under the CPU engine's hit rule, CPU/rays/ray.cpp:14-28, restated in
-oracle/: orc_pass_masks) is among the ray's candidates.  CPU: the host lookup
+(Triangle::intersects, CPU/rays/ray.cpp:14-28 / GPU/rays/ray.cu:63-64, restated in oracle/:
+orc_pass_masks) is among the ray's candidates.  CPU: the host lookup
 (rt_ctab_candidates, the kernel's operations) against the oracle's pass sets on rays from
 the scenes' surfaces -- sampled as the kernel samples them, aimed at vertices and edges, and
 nearly parallel to some triangle's plane -- at every t_scale the table serves.  GPU: the
-renders of k_render_ps that use it are bit-exact against the oracle (test_gpu_parity.py and
-the bench line's whole-frame check).
+renders that use it are bit-exact against the oracle (test_gpu_parity.py, test_dqn.py and the
+bench line's whole-frame check).
 """
 import os
 
@@ -23,6 +23,8 @@ def _scene(rtmi_mod, kind):
         g = rtmi_mod.cornell_geometry(0)
     elif kind == "cornell_gpu":
         g = rtmi_mod.cornell_geometry(1)
+    elif kind == "bunny":
+        g = rtmi_mod.obj_geometry(os.path.join(MODELS, "bunny.obj"), "generic")
     else:
         g = rtmi_mod.obj_geometry(os.path.join(MODELS, kind + ".obj"), kind)
     return np.ascontiguousarray(g.all_triangles(), np.float32), g.n_surf
@@ -83,21 +85,25 @@ def _popcount(m):
     return np.array([bin(int(x)).count("1") for x in m])
 
 
-@pytest.mark.parametrize("kind", ["cornell_cpu", "cornell_gpu", "door_room"])
-def test_ctab_keeps_every_pass(rtmi_mod, oracle_mod, kind):
+@pytest.mark.parametrize("kind,rule", [("cornell_cpu", 0), ("cornell_gpu", 0), ("door_room", 0),
+                                       ("cornell_gpu", 1), ("door_room", 1), ("archway", 1),
+                                       ("complex_light_room", 1)])
+def test_ctab_keeps_every_pass(rtmi_mod, oracle_mod, kind, rule):
     tri, n_surf = _scene(rtmi_mod, kind)
-    surf, o, d, rk = bounce_rays(tri, n_surf, 12000, seed=7)
-    cand, stats = rtmi_mod.ctab_candidates(tri, n_surf, surf, o, d)
+    surf, o, d, rk = bounce_rays(tri, n_surf, 8000, seed=7 + rule)
+    cand, stats = rtmi_mod.ctab_candidates(tri, n_surf, surf, o, d, hit_rule=rule)
     assert stats[0] > 0 and stats[2] > 0
-    for ts in (256.0, 512.0, 720.0, 4096.0):
-        passes = oracle_mod.pass_masks(tri, o, d, ts, 0)[:, 0]
+    assert cand.shape == (o.shape[0], (tri.shape[0] + 63) // 64)
+    # rule 0: the t_scale the table serves (>= 256); rule 1: any
+    for ts in ((256.0, 512.0, 720.0, 4096.0) if rule == 0 else (1.0, 256.0, 720.0, 1024.0)):
+        passes = oracle_mod.pass_masks(tri, o, d, ts, rule)
         missed = passes & ~cand
-        bad = np.nonzero(missed)[0]
+        bad = np.nonzero(missed.any(axis=1))[0]
         assert bad.size == 0, (f"t_scale {ts}: {bad.size} rays miss a passing triangle, e.g. ray {bad[0]} "
-                               f"(surface {surf[bad[0]]}, kind {rk[bad[0]]}) triangles {int(missed[bad[0]]):#x}")
+                               f"(surface {surf[bad[0]]}, kind {rk[bad[0]]}) words {[hex(int(x)) for x in missed[bad[0]]]}")
     # and the table culls: a bounce ray keeps a few of the scene's triangles
-    pc = _popcount(cand[rk == 0])
-    assert pc.mean() < 0.2 * tri.shape[0], pc.mean()
+    pc = sum(_popcount(cand[rk == 0, w]) for w in range(cand.shape[1]))
+    assert pc.mean() < (0.2 if rule == 0 else 0.3) * tri.shape[0], pc.mean()
 
 
 def test_ctab_keeps_every_triangle_outside_its_domain(rtmi_mod):
@@ -116,13 +122,13 @@ def test_ctab_keeps_every_triangle_outside_its_domain(rtmi_mod):
     o2[4, 0] = np.nan
     cand, _ = rtmi_mod.ctab_candidates(tri, n_surf, s2, o2, d2)
     for r in range(5):
-        assert int(cand[r]) == allbits, r
-    assert all(int(c) != allbits for c in cand[5:])
+        assert int(cand[r, 0]) == allbits, r
+    assert all(int(c) != allbits for c in cand[5:, 0])
 
 
 def test_ctab_refuses_large_scenes(rtmi_mod):
-    tri, n_surf = _scene(rtmi_mod, "archway")
-    assert tri.shape[0] > 64
+    tri, n_surf = _scene(rtmi_mod, "bunny")
+    assert tri.shape[0] > 256
     with pytest.raises(rtmi_mod.RtError):
         rtmi_mod.ctab_candidates(tri, n_surf, np.zeros(1, np.int32), np.zeros((1, 3), np.float32),
-                                 np.asarray([[0.0, 0.0, 1.0]], np.float32))
+                                 np.asarray([[0.0, 0.0, 1.0]], np.float32), hit_rule=1)
