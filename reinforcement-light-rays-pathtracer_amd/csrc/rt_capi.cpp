@@ -79,8 +79,8 @@ struct rt_scene {
     rt::BvhHost bvh;
     float4* d_bvh[4] = {nullptr, nullptr, nullptr, nullptr};  // nodes, tris, graze, grec
     int32_t* d_dir[3] = {nullptr, nullptr, nullptr};           // starts (2 sets), list, camera list
-    // bounce-ray candidate table (rt_ctab.cpp): built on the first CPU-preset render that can
-    // use it (scene_ensure_ctab), its device arrays in dev.ctab*
+    // bounce-ray candidate table (rt_ctab.cpp): built on the first render that can use it
+    // (scene_ensure_ctab), its device arrays in dev.ctab*
     bool ctab_tried[2] = {false, false};  // per hit rule
 };
 
@@ -233,7 +233,7 @@ int ctx_cull(rt_ctx* ctx, RenderLaunch* a) {
 }
 
 // The GPU preset's chunk-queue workspace (k_render_pq): one float3 per (pixel, chunk) of the
-// launch and the work counter (grown on demand, kept by the context)
+// launch, the work counter and the camera-ray masks (grown on demand, kept by the context)
 int ctx_chunks(rt_ctx* ctx, RenderLaunch* a) {
     if (a->preset != RT_PRESET_GPU) return RT_OK;
     const size_t n = (size_t)a->n_blocks * 256 * (size_t)a->split * 3;
@@ -247,6 +247,16 @@ int ctx_chunks(rt_ctx* ctx, RenderLaunch* a) {
     if (!ctx->d_work) RT_HIP(hipMalloc(&ctx->d_work, sizeof(unsigned long long)));
     a->csum = ctx->d_csum;
     a->work = ctx->d_work;
+    // the camera rays' rectangle masks of k_render_pq's table route: four 16x4 rectangles per block
+    const size_t words = (size_t)a->n_blocks * 4 * kRenderCullWords;
+    if (words > ctx->cull_cap) {
+        if (ctx->d_cull) RT_HIP(hipFree(ctx->d_cull));
+        ctx->d_cull = nullptr;
+        ctx->cull_cap = 0;
+        RT_HIP(hipMalloc(&ctx->d_cull, sizeof(unsigned long long) * words));
+        ctx->cull_cap = words;
+    }
+    a->cull = ctx->d_cull;
     return RT_OK;
 }
 }  // namespace rt
@@ -316,17 +326,21 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
     if (!ctab_build(isect.data(), n, n_surf, (double)sc->dev.mf_bound, rule, kCtabTsMin, &ct)) return RT_OK;
     int rc = set_device(sc->ctx);
     if (rc != RT_OK) return rc;
-    unsigned long long *dm = nullptr, *dg = nullptr, *dc = nullptr;
+    unsigned long long *dm = nullptr, *dd = nullptr, *dc = nullptr;
+    uint16_t* dg = nullptr;
     float4* dt = nullptr;
     hipError_t e = hipMalloc(&dm, sizeof(uint64_t) * ct.masks.size());
-    if (e == hipSuccess) e = hipMalloc(&dg, sizeof(uint64_t) * ct.graze.size());
+    if (e == hipSuccess) e = hipMalloc(&dd, sizeof(uint64_t) * ct.gdict.size());
+    if (e == hipSuccess) e = hipMalloc(&dg, sizeof(uint16_t) * ct.gid.size());
     if (e == hipSuccess) e = hipMalloc(&dc, sizeof(uint64_t) * ct.cop.size());
     if (e == hipSuccess) e = hipMalloc(&dt, sizeof(float4) * ct.tri.size());
     if (e == hipSuccess) e = hipMemcpy(dm, ct.masks.data(), sizeof(uint64_t) * ct.masks.size(), hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(dg, ct.graze.data(), sizeof(uint64_t) * ct.graze.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dd, ct.gdict.data(), sizeof(uint64_t) * ct.gdict.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dg, ct.gid.data(), sizeof(uint16_t) * ct.gid.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dc, ct.cop.data(), sizeof(uint64_t) * ct.cop.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMemcpy(dt, ct.tri.data(), sizeof(float4) * ct.tri.size(), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
+        if (dd) (void)hipFree(dd);
         if (dm) (void)hipFree(dm);
         if (dg) (void)hipFree(dg);
         if (dc) (void)hipFree(dc);
@@ -335,7 +349,8 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
     }
     CtabDev& t = sc->dev.ctab[rule];
     t.masks = dm;
-    t.graze = dg;
+    t.gdict = dd;
+    t.gid = dg;
     t.cop = dc;
     t.tri = dt;
     t.h = ct.h_run;
@@ -798,7 +813,8 @@ int rt_scene_destroy(rt_scene* scene) {
     if (scene->dev.mf_frag) (void)hipFree(scene->dev.mf_frag);
     for (const rt::CtabDev& t : scene->dev.ctab) {
         if (t.masks) (void)hipFree(const_cast<unsigned long long*>(t.masks));
-        if (t.graze) (void)hipFree(const_cast<unsigned long long*>(t.graze));
+        if (t.gdict) (void)hipFree(const_cast<unsigned long long*>(t.gdict));
+        if (t.gid) (void)hipFree(const_cast<uint16_t*>(t.gid));
         if (t.cop) (void)hipFree(const_cast<unsigned long long*>(t.cop));
         if (t.tri) (void)hipFree(const_cast<float4*>(t.tri));
     }
@@ -839,10 +855,12 @@ int rt_ctab_candidates(const float* tri_v, int n, int n_surf, int hit_rule, cons
     for (int r = 0; r < n_rays; ++r)
         rt::ctab_lookup(h, surf[r], orig + (size_t)r * 3, dir + (size_t)r * 3, masks + (size_t)r * h.words);
     if (stats) {
+        std::vector<int64_t> pc(h.gdict.size() / (size_t)h.words, 0);  // bits of each grazing dictionary mask
+        for (size_t e = 0; e < h.gdict.size(); ++e) pc[e / (size_t)h.words] += __builtin_popcountll(h.gdict[e]);
         int64_t bits = 0;
         for (uint64_t m : h.masks) bits += __builtin_popcountll(m);
         int64_t gbits = 0;
-        for (uint64_t m : h.graze) gbits += __builtin_popcountll(m);
+        for (uint16_t i : h.gid) gbits += pc[i];
         stats[0] = h.n_patch;
         stats[1] = h.patches_all;
         stats[2] = bits;
@@ -1051,7 +1069,7 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
     float* d_out = nullptr;
     unsigned long long* d_casts = nullptr;
     const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
-    rc = params->preset == RT_PRESET_CPU ? rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale) : RT_OK;
+    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale);
     if (rc != RT_OK) return rc;
     hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
     if (e == hipSuccess) e = hipMalloc(&d_out, out_bytes);
@@ -1104,7 +1122,7 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     int n_blocks = 0;
     rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
     if (rc != RT_OK) return rc;
-    rc = params->preset == RT_PRESET_CPU ? rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale) : RT_OK;
+    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale);
     if (rc != RT_OK) return rc;
     rt::RenderLaunch a = make_launch(scene, cam, params);
     a.blocks = d_blocks;

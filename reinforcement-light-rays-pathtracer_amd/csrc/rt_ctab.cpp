@@ -47,6 +47,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "rt_bounds.hpp"
@@ -649,6 +650,38 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, doub
             }
     h.n_patch = n_patch;
     h.cop_th = bnd::up(cop_th);
+    // the grazing bins' dictionary (16-bit indices: a table with more is not built)
+    {
+        struct Key {
+            uint64_t w[kCtabMaxWords];
+            bool operator==(const Key& o) const { return memcmp(w, o.w, sizeof w) == 0; }
+        };
+        struct KeyHash {
+            size_t operator()(const Key& k) const {
+                uint64_t x = 0x9e3779b97f4a7c15ull;
+                for (uint64_t v : k.w) x = (x ^ v) * 0xff51afd7ed558ccdull ^ (x >> 29);
+                return (size_t)x;
+            }
+        };
+        std::unordered_map<Key, uint32_t, KeyHash> ids;
+        h.gid.resize(h.graze.size() / (size_t)W);
+        for (size_t e = 0; e < h.gid.size(); ++e) {
+            Key k;
+            memset(k.w, 0, sizeof k.w);
+            for (int w = 0; w < W; ++w) k.w[w] = h.graze[e * (size_t)W + (size_t)w];
+            auto it = ids.find(k);
+            if (it == ids.end()) {
+                if (ids.size() > 0xffffu) return false;
+                it = ids.emplace(k, (uint32_t)ids.size()).first;
+                for (int w = 0; w < W; ++w) h.gdict.push_back(k.w[w]);
+            }
+            h.gid[e] = (uint16_t)it->second;
+        }
+        std::vector<uint64_t>().swap(h.graze);
+        if (getenv("RT_CTAB_VERBOSE"))
+            fprintf(stderr, "rtmi: candidate table: %d triangles, rule %d, %d patches (%.1f MB), %zu distinct grazing masks\n",
+                    n, rule, n_patch, h.masks.size() * 8e-6, ids.size());
+    }
     return true;
 }
 
@@ -684,7 +717,7 @@ void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], u
     const int patch = base + (int)pu * nv + (int)pv;
     const bool cp = fabsf(cn) < h.cop_th;
     const uint64_t* mm = &h.masks[((size_t)patch * 6 * kNc * kNc + (size_t)(f * kNc + bin(u1, kNc)) * kNc + bin(v1, kNc)) * W];
-    const uint64_t* gg = &h.graze[((size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)) * W];
+    const uint64_t* gg = &h.gdict[(size_t)h.gid[(size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)] * W];
     for (int k = 0; k < W; ++k) out[k] = mm[k] | gg[k] | (cp ? h.cop[(size_t)s * W + k] : 0ull);
 }
 

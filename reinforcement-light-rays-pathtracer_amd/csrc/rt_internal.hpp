@@ -156,8 +156,13 @@ struct CtabHost {
     float ts_min = 0.f, h_run = 0.f;
     float cop_th = 0.f;           // |d.N_s| below which the triangles coplanar with s join
     std::vector<float4> tri;      // [n_surf][4]
-    std::vector<uint64_t> cop;    // [n_surf]: the triangles coplanar with s
-    std::vector<uint64_t> masks, graze;
+    std::vector<uint64_t> cop;    // [n_surf][words]: the triangles coplanar with s
+    std::vector<uint64_t> masks;  // [patch][face][iu][iv][words]
+    // the grazing bins' masks as 16-bit indices into a dictionary of their distinct masks (a few
+    // hundred: 0.8 MB of indices instead of 9.4 MB of masks at 3 words, resident in L2)
+    std::vector<uint64_t> gdict;  // [n_gdict][words]
+    std::vector<uint16_t> gid;    // [face][gu][gv]
+    std::vector<uint64_t> graze;  // the build's uncompressed grazing bins (emptied once indexed)
 };
 bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, double ts_min, CtabHost* out);
 void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], uint64_t* out);
@@ -165,7 +170,8 @@ void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], u
 // a candidate table on the device (CtabHost's arrays and constants)
 struct CtabDev {
     const unsigned long long* masks = nullptr;  // [patch][face][iu][iv][words]
-    const unsigned long long* graze = nullptr;  // [face][gu][gv][words]
+    const unsigned long long* gdict = nullptr;  // [n_gdict][words]
+    const uint16_t* gid = nullptr;              // [face][gu][gv] -> gdict
     const unsigned long long* cop = nullptr;    // [n_surf][words]
     const float4* tri = nullptr;                // [n_surf][4]: the surfaces' patch frames
     float h = 0.0f, ts_min = 0.0f, cop_th = 0.0f;
@@ -433,6 +439,7 @@ constexpr int kKdStack = RT_KD_STACK;  // traversal stack entries per lane (LDS)
 hipError_t launch_sarsa_render(const RenderLaunch& r, const SarsaMap& m, hipStream_t stream);
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream);
 bool sarsa_prof_compiled();  // rt_sarsa.hip was built with RT_SARSA_PROF=1 (per-phase cycle counters)
+bool sarsa_ctab_compiled();  // rt_sarsa.hip was built with RT_SARSA_CTAB=1 (the table route of its persistent kernel)
 hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream);  // CDF + argmax from Q
 hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float* nrm, int n, int32_t* out,
                                 hipStream_t stream);

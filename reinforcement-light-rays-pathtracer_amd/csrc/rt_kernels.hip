@@ -375,10 +375,14 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
 // k_fold_chunks then adds each pixel's chunk sums in chunk order (((P0 + P1) + P2) + ...)
 // and divides by spp, as k_render's fold does.  The wave takes items 64 at a time from the
 // global counter (one atomic per 64 chunks) and hands them to its lanes by ballot rank.
-// Camera inside the matrix-core image's bound (no camera-ray cull), MF > 0.
-template <int SAMPLER, int RULE, int MF>
+// Camera inside the matrix-core image's bound, MF > 0.
+// CT: the casts take their candidates from tables instead of the matrix-core filter -- a
+// camera ray the cull of its pixel's 16x4 rectangle (rect_cull, k_cull_ps over the launch's
+// blocks, a.cull), a bounce ray the candidate table of the surface it leaves (ctab_candidates,
+// rt_ctab.cpp) -- and closest_hit_cand tests them in index order: the same hit.
+template <int SAMPLER, int RULE, int MF, bool CT = false>
 __global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const RenderLaunch a) {
-    __shared__ float s_mfw[4 * kMfWaveFloats];
+    __shared__ __attribute__((aligned(16))) float s_mfw[4 * kMfWaveFloats];
     float* const wl = s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats;
     const int lane = threadIdx.x & 63;
     const float4* __restrict__ shade = a.scene.shade;
@@ -392,6 +396,7 @@ __global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const Ren
     int s = 0, s_end = 0, px = 0, py = 0;
     uint32_t pix = 0;
     int depth = 0;
+    int surf = -1, cidx = 0;  // CT: the surface the ray leaves; the pixel's rectangle in a.cull
     f3 o = cam, d = make3(0.0f, 0.0f, 1.0f), tp = make3(1.0f, 1.0f, 1.0f), acc = make3(0.0f, 0.0f, 0.0f);
     unsigned n_casts = 0;
     auto camera = [&]() {
@@ -431,6 +436,7 @@ __global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const Ren
                         py = blk.py0 + (q >> 4);
                         if (px < a.clip_x1 && py < a.clip_y1) {  // (a clipped pixel's chunks: nothing)
                             pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+                            cidx = (int)(p >> 8) * 4 + (q >> 6);
                             s = c * a.per_chunk;
                             s_end = s + a.per_chunk;
                             acc = make3(0.0f, 0.0f, 0.0f);
@@ -453,7 +459,23 @@ __global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const Ren
             if (exhausted) break;
             continue;  // (every claimed item was a clipped pixel's)
         }
-        const Hit h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+        Hit h;
+        if constexpr (CT) {
+            constexpr int NW = MF;
+            uint64_t F[NW];
+#pragma unroll
+            for (int k = 0; k < NW; ++k) F[k] = 0ull;
+            if (active && depth == 0) {
+#pragma unroll
+                for (int k = 0; k < NW; ++k)
+                    F[k] = (k < kRenderCullWords) ? a.cull[(size_t)cidx * kRenderCullWords + k] : 0ull;
+            } else if (active) {
+                ctab_candidates<NW>(a.scene.ctab[RULE], a.scene.n_tri, n_surf, surf, o, d, F);
+            }
+            h = closest_hit_cand<RULE, NW>(a.scene, F, o, d, a.t_scale, wl);
+        } else {
+            h = closest_hit_mf<RULE, false, MF>(a.scene, o, d, a.t_scale, active, wl);
+        }
         if (!active) continue;
         ++n_casts;
         bool terminal = false;
@@ -498,6 +520,7 @@ __global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const Ren
             }
             o = make3(pos.x + kEps * sd.x, pos.y + kEps * sd.y, pos.z + kEps * sd.z);
             d = normalize(sd);
+            surf = h.tri;
             ++depth;
             if (depth == a.max_bounces) terminal = true;  // loop exhausted -> 0
         }
@@ -539,6 +562,9 @@ __global__ __launch_bounds__(256) void k_fold_chunks(const RenderLaunch a) {
     store_rgb(dst, tot.x / fs, tot.y / fs, tot.z / fs);
 }
 
+#ifndef RT_PQ_CTAB
+#define RT_PQ_CTAB 1  // 0: k_render_pq's casts always on the matrix-core filter (A/B)
+#endif
 #ifndef RT_RENDER_PQ
 #define RT_RENDER_PQ 1  // 0: the GPU preset's matrix-core renders keep the per-pixel k_render (A/B)
 #endif
@@ -1256,7 +1282,23 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                 (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
                 // a persistent grid: as many workgroups as the device holds at 4 waves per SIMD
                 const unsigned wgs = (unsigned)min(a.n_blocks * a.split, RT_MF_RENDER_WAVES * device_cu_count());
-                if (one)
+                // the table route (k_render_pq CT): the scene's candidate table for this hit rule and
+                // t_scale, and the camera rays' rectangle cull -- CPU-preset camera geometry, i.e.
+                // pitch 0 (camera_ray: the second rotation is then the identity, exactly)
+                const CtabDev& T = a.scene.ctab[RULE];
+                const bool ct = RT_PQ_CTAB && a.cull != nullptr && a.cos_x == 1.0f && a.sin_x == 0.0f &&
+                                a.scene.n_tri <= 64 * kRenderCullWords && T.masks != nullptr && T.bins == kCtabBins &&
+                                T.graze_n == kCtabGraze && a.t_scale >= T.ts_min && T.words <= (one ? 1 : 4);
+                if (ct) {
+                    RenderLaunch c = b;  // one workgroup per 16x16 block: the masks of its four 16x4 rectangles
+                    c.split = 1;
+                    c.split_log2 = 0;
+                    hipLaunchKernelGGL((k_cull_ps<RULE>), dim3((unsigned)a.n_blocks), dim3(256), 0, stream, c);
+                    if (one)
+                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1, true>), dim3(wgs), dim3(256), 0, stream, b);
+                    else
+                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 4, true>), dim3(wgs), dim3(256), 0, stream, b);
+                } else if (one)
                     hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1>), dim3(wgs), dim3(256), 0, stream, b);
                 else
                     hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 4>), dim3(wgs), dim3(256), 0, stream, b);

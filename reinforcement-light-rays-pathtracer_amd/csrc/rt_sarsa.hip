@@ -789,13 +789,17 @@ __global__ __launch_bounds__(256, MF == 1 ? RT_MF_SARSA_WAVES : 1) void k_sarsa_
 #endif
 // BVH: scenes with the exact BVH (large models, rt_scene_set_accel): the casts through
 // closest_hit_bvh, its stack in the lane's k-d stack column (free until the volume search)
-template <int RULE, int MF, int TD, bool BVH = false>
+// CT > 0: the casts take their candidates from tables (CT mask words; k_render_pq's CT route:
+// a camera ray the cull of its pixel's 16x4 rectangle in a.cull, a bounce ray the candidate
+// table of the surface it leaves) and closest_hit_cand tests them in index order
+template <int RULE, int MF, int TD, bool BVH = false, int CT = 0>
 #ifndef RT_SARSA_BVH_WAVES
 #define RT_SARSA_BVH_WAVES 4  // the BVH variant's traversal state: 128 VGPRs, no spills (96 at 5 waves spilled)
 #endif
 __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES)) void k_sarsa_render_pq(const RenderLaunch a,
                                                                                         const SarsaMap m) {
-    __shared__ int kd_stack[kKdStack * 256];
+    __shared__ __attribute__((aligned(16))) int kd_stack[kKdStack * 256];
+    static_assert(kKdStack * 64 >= kMfWaveFloats, "the exact phase's LDS fits a wave's stack block");
     int* const st = kd_stack_of(kd_stack);
     int* const blk_ws = kd_stack + ((int)threadIdx.x >> 6) * (kKdStack * 64);  // the wave's block
     float* const wl = reinterpret_cast<float*>(blk_ws);
@@ -810,6 +814,7 @@ __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SA
     long long item = 0;
     int s = 0, s_end = 0, px = 0, py = 0;
     uint32_t pix = 0;
+    int surf = -1, cidx = 0;  // CT: the surface the ray leaves; the pixel's rectangle in a.cull
     SarsaPath P{cam, make3(0.f, 0.f, 1.f), make3(1.f, 1.f, 1.f), 0, -1, -1, 0.0f, false};
     f3 acc = make3(0.f, 0.f, 0.f);
     unsigned n_casts = 0, n_zero = 0, casts0 = 0;
@@ -855,6 +860,7 @@ __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SA
                         py = blk.py0 + (q >> 4);
                         if (px < a.clip_x1 && py < a.clip_y1) {
                             pix = (uint32_t)py * (uint32_t)a.width + (uint32_t)px;
+                            cidx = (int)(p >> 8) * 4 + (q >> 6);
                             s = c * a.per_chunk;
                             s_end = s + a.per_chunk;
                             acc = make3(0.f, 0.f, 0.f);
@@ -888,6 +894,20 @@ __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SA
         if constexpr (BVH) {
             static_assert(kKdStack >= kBvhMaxDepth, "the BVH stack fits the k-d stack column");
             if (active) h = closest_hit_bvh<RULE, 64>(a.scene, P.o, P.d, a.t_scale, st);
+        } else if constexpr (CT > 0) {
+            uint64_t F[CT];
+#pragma unroll
+            for (int k = 0; k < CT; ++k) F[k] = 0ull;
+            if (active && P.depth == 0) {
+#pragma unroll
+                for (int k = 0; k < CT; ++k)
+                    F[k] = (k < kRenderCullWords) ? a.cull[(size_t)cidx * kRenderCullWords + k] : 0ull;
+            } else if (active) {
+                ctab_candidates<CT>(a.scene.ctab[RULE], a.scene.n_tri, n_surf, surf, P.o, P.d, F);
+            }
+            wave_lds_sync();
+            h = closest_hit_cand<RULE, CT>(a.scene, F, P.o, P.d, a.t_scale, wl);
+            wave_lds_sync();
         } else if constexpr (MF > 0) {
             wave_lds_sync();
             h = closest_hit_mf<RULE, false, MF>(a.scene, P.o, P.d, a.t_scale, active, wl);
@@ -923,6 +943,7 @@ __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SA
         const uint64_t pt3 = __builtin_amdgcn_s_memtime();
         f3 L;
         const bool term = active && sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
+        surf = h.tri;
         const uint64_t pt4 = __builtin_amdgcn_s_memtime();
         pr[0] += pt1 - pt0;
         pr[1] += pt2 - pt1;
@@ -934,7 +955,9 @@ __global__ __launch_bounds__(256, BVH ? RT_SARSA_BVH_WAVES : (MF == 1 ? RT_MF_SA
 #else
         if (!active) continue;
         f3 L;
-        if (sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L)) {
+        const bool term = sarsa_step<TD>(a, m, h, is_surf, pos, nrm, rv, td, pix, s, P, n_casts, &L);
+        surf = h.tri;  // (a continuing path leaves the surface it hit)
+        if (term) {
 #endif
             acc.x = acc.x + L.x;
             acc.y = acc.y + L.y;
@@ -1097,6 +1120,10 @@ hipError_t launch_sarsa_nearest(const SarsaMap& m, const float* pos, const float
 #define RT_MF_SARSA 0  // 1: the casts on the matrix-core filter (measured slower: DESIGN.md §4)
 #endif
 
+#ifndef RT_SARSA_CTAB
+#define RT_SARSA_CTAB 0  // 1: k_sarsa_render_pq's casts from the candidate tables (door_room 512^2 x 256: 110.3 vs 92.1 ms per frame)
+#endif
+
 #ifndef RT_SARSA_PQ
 #define RT_SARSA_PQ 1  // 0: the per-pixel k_sarsa_render (A/B builds)
 #endif
@@ -1112,6 +1139,14 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
                     a.t_scale <= kFiltMaxTScale && fabsf(a.cam_x) <= cb && fabsf(a.cam_y) <= cb &&
                     fabsf(a.cam_z) <= cb;
     const bool one = a.scene.n_tri <= 64;
+    // the table route (k_sarsa_render_pq CT): as k_render_pq's -- the scene's candidate table for
+    // this hit rule and t_scale, the camera rays' rectangle cull (pitch 0, filter records valid
+    // for the camera)
+    const CtabDev& T = a.scene.ctab[a.hit_rule == 0 ? 0 : 1];
+    const bool ct = !mf && RT_SARSA_CTAB && a.scene.bvh_nodes == nullptr && a.cull != nullptr && a.use_filter &&
+                    a.cos_x == 1.0f && a.sin_x == 0.0f && a.scene.n_tri <= 64 * kRenderCullWords &&
+                    T.masks != nullptr && T.bins == kCtabBins && T.graze_n == kCtabGraze && a.t_scale >= T.ts_min &&
+                    T.words <= (one ? 1 : 4);
     if constexpr (RT_SARSA_PQ) {
         if (a.csum == nullptr || a.work == nullptr) return hipErrorInvalidValue;
         (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
@@ -1135,6 +1170,22 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
                 hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD, true>), grid, dim3(256), 0, stream, a, m);
             else
                 hipLaunchKernelGGL((k_sarsa_render_pq<1, 0, TD, true>), grid, dim3(256), 0, stream, a, m);
+        } else if (ct) {
+            RenderLaunch c = a;  // one workgroup per 16x16 block: the masks of its four 16x4 rectangles
+            c.split = 1;
+            c.split_log2 = 0;
+            (void)launch_cull(c, stream);
+            if (a.hit_rule == 0) {
+                if (one)
+                    hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD, false, 1>), grid, dim3(256), 0, stream, a, m);
+                else
+                    hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD, false, 4>), grid, dim3(256), 0, stream, a, m);
+            } else {
+                if (one)
+                    hipLaunchKernelGGL((k_sarsa_render_pq<1, 0, TD, false, 1>), grid, dim3(256), 0, stream, a, m);
+                else
+                    hipLaunchKernelGGL((k_sarsa_render_pq<1, 0, TD, false, 4>), grid, dim3(256), 0, stream, a, m);
+            }
         } else if (!mf) {
             if (a.hit_rule == 0)
                 hipLaunchKernelGGL((k_sarsa_render_pq<0, 0, TD>), grid, dim3(256), 0, stream, a, m);
@@ -1182,6 +1233,7 @@ hipError_t launch_sarsa_rebuild(const SarsaMap& m, hipStream_t stream) {
 }
 
 bool sarsa_prof_compiled() { return RT_SARSA_PROF != 0; }
+bool sarsa_ctab_compiled() { return RT_SARSA_CTAB != 0; }
 
 hipError_t launch_sarsa_apply(const SarsaMap& m, hipStream_t stream) {
     if (m.n_vol <= 0) return hipSuccess;

@@ -32,6 +32,7 @@ void scene_host(const rt_scene* s, const float** tri, const float** normals, con
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 RenderLaunch render_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p);
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale);
 
 // read_hemisphere_locations_and_normals (GPU/utils/hemisphere_helpers.cu:230-278): one
 // "x y z nx ny nz" per line, tokens split on ' ' and read with std::stof, the first
@@ -363,10 +364,14 @@ struct rt_sarsa {
     float* d_csum = nullptr;
     size_t csum_cap = 0;
     unsigned long long* d_work = nullptr;
+    // the camera rays' rectangle masks of its table route (four 16x4 rectangles per block)
+    unsigned long long* d_cull = nullptr;
+    size_t cull_cap = 0;
     ~rt_sarsa() {
         (void)hipSetDevice(device);
         for (void* p : allocs) (void)hipFree(p);
         if (d_csum) (void)hipFree(d_csum);
+        if (d_cull) (void)hipFree(d_cull);
         if (d_work) (void)hipFree(d_work);
         if (m.prof) (void)hipFree(m.prof);
     }
@@ -409,6 +414,8 @@ int check_sarsa_params(const rt_params* p) {
 int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, const rt_params* p,
                  const rt::BlockDesc* d_blocks, int n_blocks, int clip_x1, int clip_y1, int out_pitch,
                  float* d_out, unsigned long long* d_casts, hipStream_t stream, bool apply) {
+    const int rc = rt::sarsa_ctab_compiled() ? rt::scene_ensure_ctab(scene, p->hit_rule, p->t_scale) : RT_OK;
+    if (rc != RT_OK) return rc;
     rt::RenderLaunch a = rt::render_launch(scene, cam, p);
     a.blocks = d_blocks;
     a.n_blocks = n_blocks;
@@ -430,6 +437,15 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
     if (!sa->d_work) RT_HIPE(hipMalloc(&sa->d_work, sizeof(unsigned long long)));
     a.csum = sa->d_csum;
     a.work = sa->d_work;
+    const size_t ncull = (size_t)n_blocks * 4 * rt::kRenderCullWords;
+    if (ncull > sa->cull_cap) {
+        if (sa->d_cull) (void)hipFree(sa->d_cull);
+        sa->d_cull = nullptr;
+        sa->cull_cap = 0;
+        RT_HIPE(hipMalloc(&sa->d_cull, sizeof(unsigned long long) * ncull));
+        sa->cull_cap = ncull;
+    }
+    a.cull = sa->d_cull;
     RT_HIPE(hipMemsetAsync(sa->m.stats, 0, 2 * sizeof(unsigned long long), stream));
     // RT_SARSA_PROF (with an RT_SARSA_PROF=1 kernel build): the render's per-phase cycles to stderr.
     // On a default build the counters are never written: warn once, and do not synchronise.

@@ -528,6 +528,7 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 #endif
 constexpr int kMfPairCap = RT_MF_PAIR_CAP;
 constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2 + (RT_MF_TV_LDS ? kMfPairCap : 0);
+static_assert(kMfWaveFloats >= 11 * 64, "cand_exact_min's LDS (rays, first, mask, key) fits a wave's block");
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -862,7 +863,7 @@ __device__ __forceinline__ void ctab_candidates(const CtabDev& T, int n_tri, int
     const int gv = min(kCtabGraze - 1, max(0, (int)(v1 * (0.5f * kCtabGraze))));
     const int patch = base + (int)pu * nv + (int)pv;
     const unsigned long long* mm = T.masks + ((size_t)patch * (6 * kCtabBins * kCtabBins) + (f * kCtabBins + iu) * kCtabBins + iv) * W;
-    const unsigned long long* gg = T.graze + ((size_t)(f * kCtabGraze + gu) * kCtabGraze + gv) * W;
+    const unsigned long long* gg = T.gdict + (size_t)T.gid[(f * kCtabGraze + gu) * kCtabGraze + gv] * W;
     // the triangles coplanar with the surface join near its plane's great circle (rule 0) or always (rule 1)
     const bool cp = fabsf(cn) < T.cop_th;
 #pragma unroll
@@ -878,13 +879,93 @@ __device__ __forceinline__ void ctab_candidates(const CtabDev& T, int n_tri, int
 __device__ __forceinline__ bool ctab_usable(const CtabDev& T, float t_scale) {
     return T.masks != nullptr && T.bins == kCtabBins && T.graze_n == kCtabGraze && t_scale >= T.ts_min;
 }
-// closest_hit_mf's result for a bounce ray leaving surface `surf`, its candidates from the
-// table T (ctab_candidates): the lane's first RT_CTAB_OWN candidates on its own lane, the rest
-// shared by the wave (mf_exact_wave, per 64-triangle block).  Wave-level like closest_hit_mf
-// (`active` false: no candidates).  NW: mask words (>= T.words).
+// closest_hit_mf's result for a ray whose candidates are given, F (NW mask words): every other
+// triangle fails the exact test for the lane's ray, so testing F in index order gives the scan's
+// hit.  The lane's first RT_CTAB_OWN candidates on its own lane, the rest shared by the wave
+// (mf_exact_wave, per 64-triangle block).  Wave-level like closest_hit_mf (a lane without a ray:
+// F = 0).  closest_hit_ctab: F from the table T for a bounce ray leaving surface `surf`.
+#ifndef RT_CAND_MIN
+#define RT_CAND_MIN 1  // 0: RULE 1's shared exact phase folds as RULE 0's (per-lane list walks)
+#endif
+#ifndef RT_CAND_OWN_MIN
+#define RT_CAND_OWN_MIN 0  // RT_CTAB_OWN of the min-fold phase (complex_light_room 512^2 x 64: 0 / 1 -> 50.9 / 66.8 ms)
+#endif
+
+// RULE 1's window (accept t < best, in index order, from best = 999999, tri -1) picks the
+// lexicographic minimum of (t, index) over the passing candidates and the start: a 64-bit key,
+// |t|'s bits above the index + 1 (0: the start, which wins a tie at its t) and t's sign bit
+// (a pass can be -0: ordered as +0, returned as it was)
+__device__ __forceinline__ uint64_t min_key(float t, int tri) {
+    const uint32_t b = __float_as_uint(t);
+    return ((uint64_t)(b & 0x7fffffffu) << 32) | ((uint64_t)(uint32_t)(tri + 1) << 1) | (uint64_t)(b >> 31);
+}
+__device__ __forceinline__ void min_unkey(uint64_t k, Hit& h) {
+    const uint32_t hi = (uint32_t)(k >> 32), lo = (uint32_t)k;
+    h.t = __uint_as_float(hi | (lo << 31));
+    h.tri = (int)(lo >> 1) - 1;
+}
+// position of the j-th (from 0) set bit of x (j < popcount(x))
+__device__ __forceinline__ int select_bit(uint64_t x, int j) {
+    uint32_t w = (uint32_t)x;
+    int pos = 0, c = __builtin_popcount(w);
+    if (j >= c) {
+        j -= c;
+        w = (uint32_t)(x >> 32);
+        pos = 32;
+    }
+#pragma unroll
+    for (int sh = 16; sh >= 1; sh >>= 1) {
+        c = __builtin_popcount(w & ((1u << sh) - 1u));
+        if (j >= c) {
+            j -= c;
+            w >>= sh;
+            pos += sh;
+        }
+    }
+    return pos;
+}
+// The shared exact phase of one 64-triangle block under RULE 1, folded by minimum: the wave's
+// (lane, candidate) pairs are numbered lane-major, and lane k of each round of 64 finds pair
+// cb + k's lane (binary search over the lanes' first pair numbers) and triangle (the j-th set
+// bit of that lane's mask), tests it and folds its t into that lane's key with an LDS atomic
+// minimum.  No lane walks its own list: a round costs the same whatever the lanes' counts.
+// LDS (wl, after the rays' 6 x 64 floats): first[64] int, mask[64] u64, key[64] u64.
+__device__ __forceinline__ void cand_exact_min(const float4* __restrict__ isect, int tri0, uint64_t F, float* wl,
+                                               int lane, unsigned long long* key) {
+    const int cnt = __builtin_popcountll(F);
+    int excl = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 7; ++b) {
+        const uint64_t bm = __ballot((cnt >> b) & 1);
+        excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u)) << b;
+        total += __builtin_popcountll(bm) << b;
+    }
+    if (total == 0) return;
+    int* first = reinterpret_cast<int*>(wl + 6 * 64);
+    unsigned long long* mask = reinterpret_cast<unsigned long long*>(wl + 7 * 64);
+    first[lane] = excl;
+    mask[lane] = F;
+    wave_lds_sync();
+    const float* ray = wl;
+    for (int cb = 0; cb < total; cb += 64) {
+        const int k = cb + lane;
+        if (k < total) {
+            int r = 0;
+#pragma unroll
+            for (int st = 32; st >= 1; st >>= 1)
+                if (first[r + st] <= k) r += st;
+            const int i = tri0 + select_bit(mask[r], k - first[r]);
+            const f3 ro = make3(ray[0 * 64 + r], ray[1 * 64 + r], ray[2 * 64 + r]);
+            const float t = exact_tv<1>(isect, i, ro, ray[3 * 64 + r], ray[4 * 64 + r], ray[5 * 64 + r]);
+            if (t < 999999.0f) atomicMin(key + r, (unsigned long long)min_key(t, i));
+        }
+    }
+    wave_lds_sync();
+}
+
 template <int RULE, int NW>
-__device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const CtabDev& T, int surf, f3 o, f3 d,
-                                                float t_scale, bool active, float* wl) {
+__device__ __forceinline__ Hit closest_hit_cand(const DeviceScene& s, uint64_t (&F)[NW], f3 o, f3 d, float t_scale,
+                                                float* wl) {
     const float nDx = -(d.x * t_scale);
     const float nDy = -(d.y * t_scale);
     const float nDz = -(d.z * t_scale);
@@ -899,16 +980,10 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const Ctab
     Hit h;
     h.t = (RULE == 0) ? FLT_MAX : 999999.0f;
     h.tri = -1;
-    uint64_t F[NW];
-    if (active) {
-        ctab_candidates<NW>(T, s.n_tri, s.n_surf, surf, o, d, F);
-    } else {
-#pragma unroll
-        for (int k = 0; k < NW; ++k) F[k] = 0ull;
-    }
+    constexpr bool kMin = RULE == 1 && RT_CAND_MIN;
     // the lane's first candidates (in index order) on its own lane
 #pragma unroll
-    for (int k = 0; k < RT_CTAB_OWN; ++k) {
+    for (int k = 0; k < (kMin ? RT_CAND_OWN_MIN : RT_CTAB_OWN); ++k) {
         int wsel = -1;
 #pragma unroll
         for (int w = NW - 1; w >= 0; --w)
@@ -929,10 +1004,32 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const Ctab
                 if (w == wsel) F[w] &= F[w] - 1ull;
         }
     }
+    if constexpr (kMin) {
+        unsigned long long* key = reinterpret_cast<unsigned long long*>(wl + 9 * 64);
+        key[lane] = min_key(h.t, h.tri);
 #pragma unroll
-    for (int w = 0; w < NW; ++w)
-        if (64 * w < s.n_tri) mf_exact_wave<RULE>(s.isect, 64 * w, F[w], o, nDx, nDy, nDz, wl, lane, h);
+        for (int w = 0; w < NW; ++w)
+            if (64 * w < s.n_tri) cand_exact_min(s.isect, 64 * w, F[w], wl, lane, key);
+        wave_lds_sync();
+        min_unkey(key[lane], h);
+    } else {
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if (64 * w < s.n_tri) mf_exact_wave<RULE>(s.isect, 64 * w, F[w], o, nDx, nDy, nDz, wl, lane, h);
+    }
     return h;
+}
+template <int RULE, int NW>
+__device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const CtabDev& T, int surf, f3 o, f3 d,
+                                                float t_scale, bool active, float* wl) {
+    uint64_t F[NW];
+    if (active) {
+        ctab_candidates<NW>(T, s.n_tri, s.n_surf, surf, o, d, F);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) F[k] = 0ull;
+    }
+    return closest_hit_cand<RULE, NW>(s, F, o, d, t_scale, wl);
 }
 
 #ifndef RT_FILTER

@@ -78,3 +78,52 @@ int main() {
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", inc, str(src), "-o", exe], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout
+
+
+def _min_key(t, tri):
+    """rt_trace.hpp min_key, restated"""
+    import struct
+    b = struct.unpack("<I", struct.pack("<f", t))[0]
+    return ((b & 0x7FFFFFFF) << 32) | ((tri + 1) << 1) | (b >> 31)
+
+
+def _min_unkey(k):
+    import struct
+    hi, lo = k >> 32, k & 0xFFFFFFFF
+    return struct.unpack("<f", struct.pack("<I", (hi | ((lo & 1) << 31)) & 0xFFFFFFFF))[0], (lo >> 1) - 1
+
+
+def test_rule1_min_fold_equals_index_order_window():
+    """cand_exact_min (rt_trace.hpp) folds RULE 1's passes by a 64-bit minimum instead of the
+    reference's index-order window (accept t < best, from best = 999999, tri -1): the same
+    (t, tri) bits for every sequence -- ties (the first index wins), -0 against +0, passes at
+    or above the start's 999999, and passes before or after the lane's own tests."""
+    import math
+    import random
+    import struct
+    rng = random.Random(5)
+    specials = [0.0, -0.0, 999999.0, 999998.9375, 1e-30, 1.0, 2.0, 5e5, 1e6, math.inf]
+    for trial in range(20000):
+        n = rng.randint(0, 12)
+        seq = []
+        for i in range(n):
+            r = rng.random()
+            t = rng.choice(specials) if r < 0.5 else (rng.choice(specials[:6]) if r < 0.6 else rng.uniform(0, 2e6))
+            t = struct.unpack("<f", struct.pack("<f", t))[0]
+            seq.append((t, i))
+        best_t, best_i = 999999.0, -1
+        for t, i in seq:
+            if t < best_t:
+                best_t, best_i = t, i
+        own = rng.randint(0, n)  # the lane's first `own` candidates tested on its lane
+        h_t, h_i = 999999.0, -1
+        for t, i in seq[:own]:
+            if t < h_t:
+                h_t, h_i = t, i
+        key = _min_key(h_t, h_i)
+        for t, i in seq[own:]:
+            if t < 999999.0:
+                key = min(key, _min_key(t, i))
+        got_t, got_i = _min_unkey(key)
+        assert got_i == best_i, (seq, own)
+        assert struct.pack("<f", got_t) == struct.pack("<f", best_t), (seq, own)
