@@ -131,10 +131,10 @@ std::string bvh_check(const float4* isect, int n, const BvhHost& h);
 // {O', 1 / cell}, {U, n_u}, {V, n_v}, {N, first patch}; |N.(o - O')| <= h_run) and the cube-map
 // bin of d (6 x kCtabBins^2; d in s's hemisphere, d.N >= -kCtabHemi) -> masks[patch][face][iu][iv], the
 // triangles the ray may pass the
-// exact test of; OR-ed with graze[face][gu][gv] (6 x kCtabGraze^2) and, where |d.N| < cop_th,
+// exact test of; OR-ed with graze[face][gu][gv] (6 x kCtabGraze^2, as gid indices into gdict) and, where |d.N| < cop_th,
 // with cop[s] (the triangles coplanar with s).  About kCtabPatches patches over the scene.
 #ifndef RT_CTAB_PATCHES
-#define RT_CTAB_PATCHES 4096
+#define RT_CTAB_PATCHES 16384  // 4,096 / 16,384 / 32,768: complex_light_room 2048^2 x 64 687 / 640 / 679 ms, Cornell 512^2 x 256 2.69 / 2.66 ms
 #endif
 #ifndef RT_CTAB_BINS
 #define RT_CTAB_BINS 16
