@@ -380,8 +380,11 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_RENDER_WAVES : RT_MIN_WAVES) vo
 // camera ray the cull of its pixel's 16x4 rectangle (rect_cull, k_cull_ps over the launch's
 // blocks, a.cull), a bounce ray the candidate table of the surface it leaves (ctab_candidates,
 // rt_ctab.cpp) -- and closest_hit_cand tests them in index order: the same hit.
+#ifndef RT_PQ_CT_WAVES
+#define RT_PQ_CT_WAVES 8  // waves per SIMD of the table route's persistent grid (complex_light_room 2048^2 x 64: 4 / 6 / 8 -> 640 / 536 / 517 ms: its lookups' latency)
+#endif
 template <int SAMPLER, int RULE, int MF, bool CT = false>
-__global__ __launch_bounds__(256, RT_MF_RENDER_WAVES) void k_render_pq(const RenderLaunch a) {
+__global__ __launch_bounds__(256, CT ? RT_PQ_CT_WAVES : RT_MF_RENDER_WAVES) void k_render_pq(const RenderLaunch a) {
     __shared__ __attribute__((aligned(16))) float s_mfw[4 * kMfWaveFloats];
     float* const wl = s_mfw + ((int)threadIdx.x >> 6) * kMfWaveFloats;
     const int lane = threadIdx.x & 63;
@@ -642,8 +645,10 @@ __global__ __launch_bounds__(256) void k_cull_ps(const RenderLaunch a) {
     }
 }
 
-// the work of k_render_ps for one wave with at least one pixel; returns the lane's casts
-template <int SAMPLER, int RULE, int MF>
+// the work of k_render_ps for one wave with at least one pixel; returns the lane's casts.
+// CT: the bounce casts from the scene's candidate table (the launcher checked it serves this
+// launch) -- the matrix-core path is not compiled in, so the kernel's registers allow more waves
+template <int SAMPLER, int RULE, int MF, bool CT = false>
 __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceScene& ms, float* wl,
                                             const BlockDesc& blk, int q, int chunk, int lane, int lx, int ly, int px,
                                             int py, bool valid) {
@@ -855,7 +860,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     const bool use_mf = MF > 0;  // the launcher: MF = 64-triangle blocks of the scene (image present), else 0
     // scenes of at most 64 triangles: the candidates from the scene's table (rt_ctab.cpp) instead
     // of the image's masks (wave-uniform)
-    const bool use_ctab = RT_PS_CTAB && MF == 1 && ctab_usable(ms.ctab[RULE], a.t_scale) && ms.ctab[RULE].words == 1;
+    constexpr bool use_ctab = CT && MF == 1;
     // the next direction from the surface hit (pos, hit_tri) at bounce depth dep: cos theta
     // and the ray (o = pos + eps sd, d = normalize(sd)), sampled with the path's Philox draw
     auto shade_hit = [&](int dep, float* cos_out, f3* o_out, f3* d_out) {
@@ -938,7 +943,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         uint64_t tm = tb;
 #endif
         Hit h;
-        if (use_ctab)
+        if constexpr (use_ctab)
             h = closest_hit_ctab<RULE, 1>(ms, ms.ctab[RULE], s_tri, o, d, a.t_scale, live, wl);
         else if (use_mf)
 #if RT_PROF
@@ -1048,8 +1053,11 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #ifndef RT_PS_MIN_WAVES
 #define RT_PS_MIN_WAVES 4  // the matrix-core filter's operands: ~99 VGPRs
 #endif
-template <int SAMPLER, int RULE, int MF>
-__global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
+#ifndef RT_PS_CT_WAVES
+#define RT_PS_CT_WAVES 4  // occupancy floor of the table-route variant (85 VGPRs: 5 waves; Cornell 512^2 x 256: 2.64 ms, 6 waves 2.67, 8 waves 3.00 with spills)
+#endif
+template <int SAMPLER, int RULE, int MF, bool CT = false>
+__global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
     const int lg = a.split_log2;
     const BlockDesc blk = a.blocks[blockIdx.x >> lg];
     // XCD-aware parts: workgroups go to the 8 XCDs round-robin by blockIdx, so the
@@ -1096,15 +1104,17 @@ __global__ __launch_bounds__(256, RT_PS_MIN_WAVES) void k_render_ps(const Render
         }
 #endif
 #if RT_MF_LDS
-        const int ng = mf_groups(a.scene.n_tri);
-        uint4* lf = reinterpret_cast<uint4*>(next);
-        for (int i = threadIdx.x; i < ng * 64; i += 256) lf[i] = a.scene.mf_frag[i];
-        ms.mf_frag = lf;
+        if (!CT) {
+            const int ng = mf_groups(a.scene.n_tri);
+            uint4* lf = reinterpret_cast<uint4*>(next);
+            for (int i = threadIdx.x; i < ng * 64; i += 256) lf[i] = a.scene.mf_frag[i];
+            ms.mf_frag = lf;
+        }
 #endif
-        if (RT_PS_SCENE_LDS || RT_MF_LDS) __syncthreads();
+        if (RT_PS_SCENE_LDS || (RT_MF_LDS && !CT)) __syncthreads();
     }
     const unsigned n_casts =
-        (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE, MF>(a, ms, wl, blk, q, chunk, lane, lx, ly, px, py, valid);
+        (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE, MF, CT>(a, ms, wl, blk, q, chunk, lane, lx, ly, px, py, valid);
     if (a.casts != nullptr) {
         const unsigned total = wave_sum(n_casts);
         if (lane == 0) wg_casts[threadIdx.x >> 6] = total;
@@ -1239,16 +1249,24 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
         a.scene.bvh_nodes == nullptr) {
         const size_t ps_lds = (size_t)4 * ps_wave_floats(a.per_chunk) * sizeof(float);
         if (ps_lds <= (size_t)RT_PS_MAX_LDS) {
+            // the bounce casts from the scene's candidate table (rt_ctab.cpp) when it serves this
+            // launch: one mask word, this build's bins, t_scale >= its ts_min
+            const CtabDev& T = a.scene.ctab[RULE];
+            const bool ct = RT_PS_CTAB && RT_MF && a.scene.mf_frag != nullptr && a.scene.n_tri <= 64 &&
+                            T.masks != nullptr && T.bins == kCtabBins && T.graze_n == kCtabGraze &&
+                            a.t_scale >= T.ts_min && T.words == 1;
             size_t mf_lds = 0;
             if (RT_MF && a.scene.mf_frag != nullptr) {
                 mf_lds = (size_t)4 * kMfWaveFloats * sizeof(float);
                 if (RT_PS_SCENE_LDS)
                     mf_lds += (size_t)a.scene.n_tri * (kIsectF4 + (RT_PS_SHADE_LDS ? kShadeF4 : 0)) * sizeof(float4);
-                if (RT_MF_LDS) mf_lds += (size_t)mf_groups(a.scene.n_tri) * 64 * sizeof(uint4);
+                if (RT_MF_LDS && !ct) mf_lds += (size_t)mf_groups(a.scene.n_tri) * 64 * sizeof(uint4);
             }
             const dim3 grid((unsigned)(a.n_blocks * a.split));
             KernelTimer kt(KT_RENDER_PS, stream);
-            if (mf_lds > 0 && a.scene.n_tri <= 64)
+            if (ct)
+                hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 1, true>), grid, dim3(256), ps_lds + mf_lds, stream, a);
+            else if (mf_lds > 0 && a.scene.n_tri <= 64)
                 hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 1>), grid, dim3(256), ps_lds + mf_lds, stream, a);
             else if (mf_lds > 0)
                 hipLaunchKernelGGL((k_render_ps<SAMPLER, RULE, 4>), grid, dim3(256), ps_lds + mf_lds, stream, a);
@@ -1294,10 +1312,11 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                     c.split = 1;
                     c.split_log2 = 0;
                     hipLaunchKernelGGL((k_cull_ps<RULE>), dim3((unsigned)a.n_blocks), dim3(256), 0, stream, c);
+                    const unsigned wct = (unsigned)min(a.n_blocks * a.split, RT_PQ_CT_WAVES * device_cu_count());
                     if (one)
-                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1, true>), dim3(wgs), dim3(256), 0, stream, b);
+                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1, true>), dim3(wct), dim3(256), 0, stream, b);
                     else
-                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 4, true>), dim3(wgs), dim3(256), 0, stream, b);
+                        hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 4, true>), dim3(wct), dim3(256), 0, stream, b);
                 } else if (one)
                     hipLaunchKernelGGL((k_render_pq<SAMPLER, RULE, 1>), dim3(wgs), dim3(256), 0, stream, b);
                 else
