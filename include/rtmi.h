@@ -473,8 +473,10 @@ int rt_cull_masks_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* ca
                          int x0, int y0, int w, int h, uint64_t* out, int64_t* n_words);
 /* Host-side check of the bounce-ray candidate table (rt_ctab.cpp): a render builds it on first
  * use for a scene of at most 256 triangles -- hit rule RT_HIT_RULE_CPU (k_render_ps's bounce
- * casts, t_scale >= 256) or RT_HIT_RULE_GPU (the DQN renderer's bounce casts) -- and the bounce
- * casts take their candidates from it.  For the triangle soup tri_v (n <= 256, the first n_surf
+ * casts, t_scale >= 256) or RT_HIT_RULE_GPU (the GPU-engine renders' and the DQN renderer's
+ * bounce casts; the GPU-engine renders' camera rays take the cull of their 16x4 pixel
+ * rectangle) -- and the bounce casts take their candidates from it (RT_CTAB=0 in the
+ * environment: never built).  For the triangle soup tri_v (n <= 256, the first n_surf
  * surfaces: the rt_scene_create order) build the table of `hit_rule` and look up each ray
  * (surf: the surface its origin lies on, orig, dir: n_rays x 3, dir unit length) as the kernels
  * do: bit i % 64 of masks[r * words + i / 64] (words = ceil(n / 64)) = triangle i is a
