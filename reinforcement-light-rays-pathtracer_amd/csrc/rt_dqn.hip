@@ -817,14 +817,17 @@ __device__ __forceinline__ SampleOut sample_from_q(float* __restrict__ q, size_t
 #ifndef RT_DQN_CTAB
 #define RT_DQN_CTAB 1  // 0: the bounce casts on the matrix-core image even with a candidate table (A/B)
 #endif
-template <int MF, bool BOUNCE = false>
+template <int MF, bool BOUNCE = false, bool CT = false>
 __device__ __forceinline__ bool dqn_trace(const DqnLaunch& a, f3 pos, f3 dir, bool active, float* wl, f3* loc_out,
                                           int* tri_out, f3* tp, int surf = -1) {
     const f3 o = make3(pos.x + dir.x * kEps, pos.y + dir.y * kEps, pos.z + dir.z * kEps);
     const f3 d = normalize(dir);
     Hit h;
     if constexpr (MF > 0) {
-        if (BOUNCE && RT_DQN_CTAB && ctab_usable(a.scene.ctab[1], a.t_scale) && a.scene.ctab[1].words <= MF)
+        // CT: the launcher checked the table serves this launch (no matrix-core path compiled in)
+        if constexpr (CT)
+            h = closest_hit_ctab<1, MF>(a.scene, a.scene.ctab[1], surf, o, d, a.t_scale, active, wl);
+        else if (BOUNCE && RT_DQN_CTAB && ctab_usable(a.scene.ctab[1], a.t_scale) && a.scene.ctab[1].words <= MF)
             h = closest_hit_ctab<1, MF>(a.scene, a.scene.ctab[1], surf, o, d, a.t_scale, active, wl);
         else
             h = closest_hit_mf<1, false, MF>(a.scene, o, d, a.t_scale, active, wl);
@@ -962,8 +965,11 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_camer
 
 // one bounce >= 1 for the rays of list[cur]: sample (Q already in a.rays.q), trace
 // FUSED: the cell was chosen by k_dqn_mlp<MT, true> (q[i] = its index bits, q[ldq + i] = qd)
-template <int MF, bool FUSED = false, bool QB = false>
-__global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounce(const DqnLaunch a, int bounce) {
+#ifndef RT_DQN_CT_WAVES
+#define RT_DQN_CT_WAVES 4  // occupancy floor of the table-route bounce kernel (archway 1024^2 x 16: 4 / 6 / 8 waves 375.5 / 417.7 / 416.3 ms per frame)
+#endif
+template <int MF, bool FUSED = false, bool QB = false, bool CT = false>
+__global__ __launch_bounds__(256, CT ? RT_DQN_CT_WAVES : (MF > 0 ? RT_MF_DQN_WAVES : 1)) void k_dqn_bounce(const DqnLaunch a, int bounce) {
     __shared__ float s_mfw[dqn_lds_floats(MF)];
     const int cur = (bounce - 1) & 1, nxt = bounce & 1;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1006,7 +1012,7 @@ __global__ __launch_bounds__(256, MF > 0 ? RT_MF_DQN_WAVES : 1) void k_dqn_bounc
             tp = make3(tp.x * a.env_light, tp.y * a.env_light, tp.z * a.env_light);
         }
     }
-    keep = dqn_trace<MF, true>(a, pos, dir, want, dqn_lane_ws<MF>(s_mfw), &loc, &ntri, &tp, want ? ntri : -1);
+    keep = dqn_trace<MF, true, CT>(a, pos, dir, want, dqn_lane_ws<MF>(s_mfw), &loc, &ntri, &tp, want ? ntri : -1);
     if (i < n_act) {
         if (keep) {
             st3(a.rays.loc, rid, loc);
@@ -1366,6 +1372,17 @@ hipError_t launch_dqn_bounce(const DqnLaunch& a, int bounce, hipStream_t stream)
     if (e != hipSuccess) return e;
     KernelTimer kt(KT_DQN_BOUNCE, stream);
     const dim3 grid(ray_blocks(a));
+    const CtabDev& T = a.scene.ctab[1];
+    const int mf = dqn_mf(a);
+    const bool ct = RT_DQN_CTAB && qb && mf > 0 && T.masks != nullptr && T.bins == kCtabBins &&
+                    T.graze_n == kCtabGraze && a.t_scale >= T.ts_min && T.words <= mf;
+    if (ct) {
+        if (mf == 1)
+            hipLaunchKernelGGL((k_dqn_bounce<1, false, true, true>), grid, dim3(256), 0, stream, a, bounce);
+        else
+            hipLaunchKernelGGL((k_dqn_bounce<4, false, true, true>), grid, dim3(256), 0, stream, a, bounce);
+        return hipGetLastError();
+    }
     if (qb) {
         switch (dqn_mf(a)) {
             case 1: hipLaunchKernelGGL((k_dqn_bounce<1, false, true>), grid, dim3(256), 0, stream, a, bounce); break;
