@@ -341,6 +341,13 @@ typedef struct rt_sarsa rt_sarsa;
  * initialise_radiance_grid (radiance_volume.cu:46-89); the KD tree of radiance_tree.cu in
  * its array form.  The map lives on the context's device. */
 int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa** out);
+/* The same with the volume density as an argument: floor(area / area_per_sample) volumes per
+ * surface -- AREA_PER_SAMPLE (GPU/constants/radiance_volumes_settings.h:12), a compile-time
+ * constant of the reference (0.001f) that its thesis runs varied (Images/door_room/
+ * sarsa_128_344_volumes.bmp, 4_critical_evaluation.tex:240-245).  area_per_sample must be a
+ * finite float > 0; rt_sarsa_create(...) is rt_sarsa_create_density(..., 0.001f, ...). */
+int rt_sarsa_create_density(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float area_per_sample,
+                            rt_sarsa** out);
 int rt_sarsa_destroy(rt_sarsa* sarsa);
 /* sizes: volumes, KD array elements, frames rendered so far (any pointer may be NULL) */
 int rt_sarsa_info(const rt_sarsa* sarsa, int32_t* n_volumes, int32_t* n_nodes, uint32_t* frames);

@@ -349,11 +349,12 @@ KD_DTYPE = np.dtype([("dim", "<i4"), ("leaf", "<i4"), ("left", "<i4"), ("right",
 class Sarsa:
     """Expected-SARSA radiance map of the restatement (orc_sarsa_*)."""
 
-    def __init__(self, geom, seed: int):
+    def __init__(self, geom, seed: int, area_per_sample: float = 0.001):
         L = lib()
         VP = ctypes.c_void_p
-        L.orc_sarsa_create.restype = VP
-        L.orc_sarsa_create.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.c_uint64]
+        L.orc_sarsa_create_density.restype = VP
+        L.orc_sarsa_create_density.argtypes = [_FP, _FP, ctypes.c_int, _FP, _IP, ctypes.c_int, ctypes.c_uint64,
+                                               ctypes.c_float]
         L.orc_sarsa_destroy.argtypes = [VP]
         L.orc_sarsa_info.argtypes = [VP, _IP, _IP]
         L.orc_sarsa_volumes.argtypes = [VP, _FP, _FP, _IP, VP]
@@ -378,8 +379,8 @@ class Sarsa:
                       np.ascontiguousarray(get("light_group"), np.int32)]
         tri, alb, em, grp = self._keep
         self._L = L
-        self._h = L.orc_sarsa_create(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp),
-                                     get("light").shape[0], seed)
+        self._h = L.orc_sarsa_create_density(_f(tri), _f(alb), get("tri").shape[0], _f(em), _i(grp),
+                                             get("light").shape[0], seed, area_per_sample)
         nv, nk = ctypes.c_int32(0), ctypes.c_int32(0)
         L.orc_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk))
         self.n_volumes, self.n_nodes = nv.value, nk.value

@@ -1295,8 +1295,12 @@ static void kd_insert(orc_sarsa *m, const kd_sub *subs, int s, int slot) {
     kd_insert(m, subs, u->right, last + 2);
 }
 
-ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n_surf, const float *emission,
-                                    const int32_t *light_group, int n_light, uint64_t seed) {
+/* RadianceMap::get_radiance_volumes_count / uniformly_sample_radiance_volumes
+ * (GPU/radiance_volumes/radiance_map.cu:58-84): floor(area / AREA_PER_SAMPLE) volumes per surface;
+ * AREA_PER_SAMPLE (radiance_volumes_settings.h:12, 0.001f) as an argument */
+ORC_API orc_sarsa *orc_sarsa_create_density(const float *tri, const float *albedo, int n_surf, const float *emission,
+                                            const int32_t *light_group, int n_light, uint64_t seed,
+                                            float area_per_sample) {
     orc_sarsa *m = (orc_sarsa *)calloc(1, sizeof(orc_sarsa));
     int nt = n_surf + n_light;
     m->n_surf = n_surf; m->n_light = n_light; m->seed = seed;
@@ -1312,7 +1316,7 @@ ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n
     orc_triangle_normals(m->tri, nt, m->normal);
     /* count, then place */
     int n = 0;
-    for (int j = 0; j < n_surf; j++) n += (int)floorf(tri_area(tri + 9 * j) / 0.001f);
+    for (int j = 0; j < n_surf; j++) n += (int)floorf(tri_area(tri + 9 * j) / area_per_sample);
     m->n_vol = n;
     m->pos = (float *)malloc(sizeof(float) * 4 * (size_t)(n + 1));
     m->nrm = (float *)malloc(sizeof(float) * 3 * (size_t)(n + 1));
@@ -1321,7 +1325,7 @@ ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n
     int x = 0;
     for (int j = 0; j < n_surf; j++) {
         const float *v = tri + 9 * j;
-        int cnt = (int)floorf(tri_area(v) / 0.001f);
+        int cnt = (int)floorf(tri_area(v) / area_per_sample);
         for (int i = 0; i < cnt; i++, x++) {
             float a1, a2;
             uint32_t attempt = 0;
@@ -1390,6 +1394,11 @@ ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n
         free(idx);
     }
     return m;
+}
+
+ORC_API orc_sarsa *orc_sarsa_create(const float *tri, const float *albedo, int n_surf, const float *emission,
+                                    const int32_t *light_group, int n_light, uint64_t seed) {
+    return orc_sarsa_create_density(tri, albedo, n_surf, emission, light_group, n_light, seed, 0.001f);
 }
 
 ORC_API void orc_sarsa_destroy(orc_sarsa *m) {

@@ -476,8 +476,25 @@ int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, cons
 extern "C" {
 
 int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa** out) {
+    return rt_sarsa_create_density(ctx, scene, seed, kAreaPerSample, out);
+}
+
+int rt_sarsa_create_density(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, float area_per_sample,
+                            rt_sarsa** out) {
     if (!ctx || !scene || !out) return err(RT_E_INVALID, "NULL argument");
     *out = nullptr;
+    if (!(area_per_sample > 0.f) || !isfinite(area_per_sample))
+        return err(RT_E_INVALID, "area_per_sample must be a finite float > 0");
+    {
+        // the map takes ~4.7 KB of device memory per volume: refuse densities beyond 2^24 volumes
+        const float *tri0, *nrm0, *alb0, *em0;
+        int ns0, nl0;
+        rt::scene_host(scene, &tri0, &nrm0, &alb0, &em0, &ns0, &nl0);
+        double total = 0;
+        for (int j = 0; j < ns0; ++j) total += floor((double)(triangle_area(tri0 + 9 * j) / area_per_sample));
+        if (!(total <= (double)(1 << 24)))
+            return err(RT_E_UNSUPPORTED, "area_per_sample gives more than 2^24 radiance volumes");
+    }
     const float *tri, *normals, *albedo, *emission;
     int n_surf, n_light;
     rt::scene_host(scene, &tri, &normals, &albedo, &emission, &n_surf, &n_light);
@@ -490,7 +507,7 @@ int rt_sarsa_create(rt_ctx* ctx, const rt_scene* scene, uint64_t seed, rt_sarsa*
     // Philox counter (volume, attempt, kPlacementEvent, 0) in place of rand().
     for (int j = 0; j < n_surf; ++j) {
         const float* v = tri + 9 * j;
-        const int cnt = (int)floorf(triangle_area(v) / kAreaPerSample);
+        const int cnt = (int)floorf(triangle_area(v) / area_per_sample);
         for (int i = 0; i < cnt; ++i) {
             const uint32_t x = (uint32_t)sa->pos.size() / 4;
             float a1, a2;

@@ -52,7 +52,7 @@ EXPORTS = (
     "rt_dynet_read", "rt_dynet_write", "rt_dqn_create", "rt_dqn_destroy", "rt_dqn_set_mlp", "rt_dqn_forward", "rt_dqn_forward_device",
     "rt_dqn_sample",
     "rt_render_dqn", "rt_render_dqn_tiles_device",
-    "rt_sarsa_create", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
+    "rt_sarsa_create", "rt_sarsa_create_density", "rt_sarsa_destroy", "rt_sarsa_info", "rt_sarsa_volumes", "rt_sarsa_read",
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
     "rt_neuralq_create", "rt_neuralq_destroy", "rt_neuralq_epsilon", "rt_neuralq_render_frame",
@@ -150,6 +150,7 @@ def _declare(lib):
         "rt_render_dqn_tiles_device": (i, [_P, _P, _P, ctypes.POINTER(RtCamera),
                                            ctypes.POINTER(RtParams), _IP, i, i, _P, _P, _P]),
         "rt_sarsa_create": (i, [_P, _P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+        "rt_sarsa_create_density": (i, [_P, _P, ctypes.c_uint64, ctypes.c_float, ctypes.POINTER(_P)]),
         "rt_sarsa_destroy": (i, [_P]),
         "rt_sarsa_info": (i, [_P, _IP, _IP, _UP]),
         "rt_sarsa_set_search": (i, [_P, i]),

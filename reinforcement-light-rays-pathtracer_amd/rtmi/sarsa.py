@@ -1,6 +1,7 @@
 """Expected-SARSA radiance volumes (BASELINE config 3) on top of the C ABI.
 
   RadianceMap(ctx, scene, seed)   rt_sarsa_create: volumes, Q-table, KD tree on the device
+  RadianceMap(..., area_per_sample=a)   rt_sarsa_create_density: another AREA_PER_SAMPLE
   .render(cam, params, frames)    draw_reinforcement_path_tracing + update_radiance_volume_
                                   distributions per frame (rt_render_sarsa)
   .render_tiles_device(...)       one frame over a tile list; apply=False leaves the frame's TD
@@ -37,11 +38,17 @@ KD_DTYPE = np.dtype([("dim", "<i4"), ("leaf", "<i4"), ("left", "<i4"), ("right",
 
 
 class RadianceMap:
-    def __init__(self, ctx: Context, scene: Scene, seed: int = 1984):
+    def __init__(self, ctx: Context, scene: Scene, seed: int = 1984, area_per_sample: float | None = None):
+        """area_per_sample: the volume density, floor(area / area_per_sample) volumes per
+        surface (AREA_PER_SAMPLE, radiance_volumes_settings.h:12; None = the reference's 0.001)"""
         self.ctx = ctx
         self.scene = scene
         self._h = ctypes.c_void_p()
-        check(lib().rt_sarsa_create(ctx.handle, scene.handle, seed, ctypes.byref(self._h)))
+        if area_per_sample is None:
+            check(lib().rt_sarsa_create(ctx.handle, scene.handle, seed, ctypes.byref(self._h)))
+        else:
+            check(lib().rt_sarsa_create_density(ctx.handle, scene.handle, seed, float(area_per_sample),
+                                                ctypes.byref(self._h)))
         nv, nk, fr = ctypes.c_int32(0), ctypes.c_int32(0), ctypes.c_uint32(0)
         check(lib().rt_sarsa_info(self._h, ctypes.byref(nv), ctypes.byref(nk), ctypes.byref(fr)))
         self.n_volumes, self.n_nodes = nv.value, nk.value

@@ -27,8 +27,8 @@ def geometry(rtmi_mod, scene):
     return rtmi_mod.obj_geometry(os.path.join(MODELS, scene + ".obj"), scene)
 
 
-def area_counts(tri):
-    """floor(area / 0.001) per triangle, Triangle::compute_area's arithmetic (numpy float32)"""
+def area_counts(tri, area_per_sample=0.001):
+    """floor(area / AREA_PER_SAMPLE) per triangle, Triangle::compute_area's arithmetic (numpy float32)"""
     v = tri.reshape(-1, 3, 3).astype(np.float32)
     a, b = v[:, 1] - v[:, 0], v[:, 2] - v[:, 0]
     dot = lambda x, y: (x[:, 0] * y[:, 0] + x[:, 1] * y[:, 1]) + x[:, 2] * y[:, 2]
@@ -36,7 +36,17 @@ def area_counts(tri):
     c = dot(a, b) / e
     s = np.sqrt(1.0 - c.astype(np.float64) ** 2).astype(np.float32)
     area = np.float32(0.5) * e * s
-    return np.floor(area / np.float32(0.001)).astype(np.int64)
+    return np.floor(area / np.float32(area_per_sample)).astype(np.int64)
+
+
+# sizeof(RadianceVolume) of the reference (GPU/radiance_volumes/radiance_volume.cuh:40-49):
+# vec4 position 16 + radiance_grid, radiance_distribution, visits 3 x 144 x 4 + irradiance_accum 4
+# + surface_index 4 + vec3 normal 12 + mat4 transformation_matrix 64 + int index 4
+RADIANCE_VOLUME_BYTES = 16 + 3 * 144 * 4 + 4 + 4 + 12 + 64 + 4
+# Q-table memory the reference's authors record, MB: the thesis's table
+# (Descriptions/write_up/chapters/4_critical_evaluation.tex:217-232: Cornell Box 44, Door Room 66,
+# Complex Pillars 300) and the archway SARSA render's file name (Images/archway/sarsa_128spp_3avg_272Mb.png)
+THESIS_QTABLE_MB = {"cornell": 44, "door_room": 66, "complex_light_room": 300, "archway": 272}
 
 
 def leaves_under(kd, i, out):
@@ -87,6 +97,32 @@ def test_oracle_volume_placement(rtmi_mod, oracle_mod, scene):
     G = np.stack([e1, e2], 2)
     ab = np.einsum("nij,nj->ni", np.linalg.pinv(G), d)
     assert np.all(ab > -1e-4) and np.all(ab.sum(1) < 1 + 1e-4)
+
+
+@pytest.mark.parametrize("scene", SCENES)
+def test_volume_count_matches_reference_qtable_memory(rtmi_mod, oracle_mod, scene):
+    """The volume count at the reference's AREA_PER_SAMPLE 0.001 times sizeof(RadianceVolume)
+    is the Q-table memory its thesis reports for the scene (floor to the MB): the density the
+    reference ran those scenes at is the default one."""
+    m = oracle_mod.Sarsa(geometry(rtmi_mod, scene), 1984)
+    assert int(m.n_volumes * RADIANCE_VOLUME_BYTES // 10**6) == THESIS_QTABLE_MB[scene], m.n_volumes
+
+
+def test_oracle_volume_density(rtmi_mod, oracle_mod):
+    """AREA_PER_SAMPLE as an argument: 0.1 gives the door room the 344 volumes of the reference's
+    Images/door_room/sarsa_128_344_volumes.bmp and sarsa_12_344_volumes.png, 0.001 the 36,028 of
+    vor_36028.png; placement follows the same per-surface rule."""
+    g = geometry(rtmi_mod, "door_room")
+    assert oracle_mod.Sarsa(g, 1984, 0.001).n_volumes == 36028
+    m = oracle_mod.Sarsa(g, 1984, 0.1)
+    assert m.n_volumes == 344 == int(area_counts(g.tri, 0.1).sum())
+    pos, nrm, surf, kd = m.volumes()
+    assert np.array_equal(np.bincount(surf, minlength=g.n_surf), area_counts(g.tri, 0.1))
+    assert m.n_nodes == 2 * 344 - 1
+    # the first volumes are the default map's first volumes (same Philox stream per volume index)
+    pd, _, sd, _ = oracle_mod.Sarsa(g, 1984, 0.001).volumes()
+    k = int(area_counts(g.tri, 0.1)[0])
+    assert np.array_equal(pos[:k], pd[:k]) and np.array_equal(surf[:k], sd[:k])
 
 
 @pytest.mark.parametrize("scene", ("door_room", "archway"))
@@ -320,6 +356,43 @@ def test_gpu_render_and_learning_equal_oracle(rtmi_mod, oracle_mod, gpu_ctx, sce
     finally:
         rm.close()
         sc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scene,area", [("door_room", 0.1), ("door_room", 0.0045), ("cornell", 0.01)])
+def test_gpu_volume_density_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, area):
+    """rt_sarsa_create_density: placement, KD array, initial state and two learned frames
+    bit-exact with the restatement at another AREA_PER_SAMPLE (sparse maps: most queries
+    leave the grid's acceptance radius and walk the KD array)."""
+    g = geometry(rtmi_mod, scene)
+    sc = rtmi_mod.Scene(gpu_ctx, g)
+    rm = rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984, area_per_sample=area)
+    om = oracle_mod.Sarsa(g, 1984, area)
+    try:
+        assert rm.n_volumes == om.n_volumes == int(area_counts(g.tri, area).sum())
+        for a, b in zip(rm.volumes(), om.volumes()):
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=48, height=40, spp=8, spp_split=4)
+        for _ in range(2):
+            img_g, casts_g = rm.render(rtmi_mod.camera(rtmi_mod.CAMERAS[scene]), p, 1)
+            img_o, casts_o = om.render(oracle_mod.camera(rtmi_mod.CAMERAS[scene]), oracle_mod.params_from(p), 1)
+            assert casts_g == casts_o and np.array_equal(img_g, img_o)
+            for a, b in zip(rm.read(), om.read()):
+                assert np.array_equal(a, b)
+            assert rm.frame_stats() == om.stats()
+    finally:
+        rm.close()
+        sc.close()
+
+
+def test_density_argument_refused(rtmi_mod):
+    """area_per_sample must be finite and > 0 (checked before any device work)."""
+    import ctypes
+    h = ctypes.c_void_p()
+    for bad in (0.0, -0.001, float("inf"), float("nan")):
+        rc = rtmi_mod.lib().rt_sarsa_create_density(ctypes.c_void_p(1), ctypes.c_void_p(1), 1984, bad,
+                                                    ctypes.byref(h))
+        assert rc == rtmi_mod._lib.RT_E_INVALID and not h.value
 
 
 def _same_bits_nan_aware(a, b):

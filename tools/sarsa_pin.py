@@ -12,9 +12,10 @@ For each scene, TD rule (frame-synchronous, in-frame) and spp this renders frame
 reference's 720x720 with the GPU-engine preset and records each frame's logged statistic and
 zero count next to the reference's, plus the block means of the last frame.
 
-    python tools/sarsa_pin.py [--frames 8] [--spp 1 32] [--seeds 1984] [--out gpurun_out/sarsa_pin]
+    python tools/sarsa_pin.py [--frames 8] [--spp 1 32] [--seeds 1984] [--areas 0.001 0.1] [--out gpurun_out/sarsa_pin]
 """
 import argparse
+import itertools
 import json
 import os
 import sys
@@ -47,6 +48,8 @@ def main():
     ap.add_argument("--modes", nargs="*", default=["frame", "inframe"])
     ap.add_argument("--scenes", nargs="*", default=list(SCENES))
     ap.add_argument("--size", type=int, default=720)
+    ap.add_argument("--areas", type=float, nargs="*", default=[0.001],
+                    help="AREA_PER_SAMPLE values (radiance_volumes_settings.h:12) to sweep")
     ap.add_argument("--final-spp", type=int, default=0,
                     help="after the frames, one frame at this spp compared with the reference's SARSA render")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "sarsa_pin"))
@@ -64,53 +67,52 @@ def main():
             scene = spec.partition(":")[0]
             cam = rtmi.camera(rtmi.CAMERAS[scene])
             with rtmi.Scene(ctx, g) as sc:
-                for mode in args.modes:
-                    for spp in args.spp:
-                        for seed in args.seeds:
-                            rm = rtmi.sarsa.RadianceMap(ctx, sc, 1984)  # placement seed fixed; seed = render RNG
-                            try:
-                                if mode == "inframe":
-                                    rm.set_td_mode(rtmi.sarsa.TD_INFRAME)
-                                p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=W, height=H, spp=spp,
-                                                        spp_split=min(spp, 8), seed=seed)
-                                logged, zero, cps, ms = [], [], [], []
-                                for f in range(args.frames):
-                                    t = time.time()
-                                    img, casts = rm.render(cam, p, 1)
-                                    ms.append(round((time.time() - t) * 1e3, 1))
-                                    paths, z = rm.frame_stats()
-                                    logged.append(paths // (W * H))
-                                    zero.append(z)
-                                    cps.append(round(casts / (W * H * spp), 4))
-                                final = None
-                                if args.final_spp:
-                                    pf = rtmi.default_params(rtmi.RT_PRESET_GPU, width=W, height=H,
-                                                             spp=args.final_spp, spp_split=8, seed=seed)
-                                    img, casts = rm.render(cam, pf, 1)
-                                    paths, z = rm.frame_stats()
-                                    rgb8 = rtmi.metrics.argb_to_rgb8(rtmi.pack_argb(img)).astype(np.float64)
-                                    final = {"spp": args.final_spp, "logged_avg_path": paths // (W * H),
-                                             "casts_per_sample": round(casts / (W * H * args.final_spp), 4),
-                                             "mean8": round(float(rgb8.mean()), 3)}
-                                    key = png_key[scene]
-                                    if W == 720 and key in imgs:
-                                        bm = rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3))
-                                        rb = np.array(imgs[key]["means"])
-                                        d = np.abs(bm - rb)
-                                        final.update({"ref_png": imgs[key]["file"], "ref_mean8": round(float(rb.mean()), 3),
-                                                      "block_mean_abs_diff": round(float(d.mean()), 3),
-                                                      "block_max_abs_diff": round(float(d.max()), 3)})
-                                r = {"scene": spec, "final": final, "mode": mode, "spp": spp, "seed": seed,
-                                     "logged_avg_path": logged, "zero_paths": zero,
-                                     "zero_frac": [round(z / (W * H * spp), 5) for z in zero],
-                                     "casts_per_sample": cps, "ms": ms,
-                                     "ref_avg_path": ref[scene]["avg_path_length"][:args.frames],
-                                     "ref_zero_paths": ref[scene]["zero_contribution_paths"][:args.frames],
-                                     "mean8": float(rtmi.metrics.argb_to_rgb8(rtmi.pack_argb(img)).mean())}
-                                res["runs"].append(r)
-                                print(json.dumps(r), flush=True)
-                            finally:
-                                rm.close()
+                for area, mode, spp, seed in itertools.product(args.areas, args.modes, args.spp, args.seeds):
+                    rm = rtmi.sarsa.RadianceMap(ctx, sc, 1984, area_per_sample=area)  # placement seed fixed
+                    try:
+                        if mode == "inframe":
+                            rm.set_td_mode(rtmi.sarsa.TD_INFRAME)
+                        p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=W, height=H, spp=spp,
+                                                spp_split=min(spp, 8), seed=seed)
+                        logged, zero, cps, ms = [], [], [], []
+                        for f in range(args.frames):
+                            t = time.time()
+                            img, casts = rm.render(cam, p, 1)
+                            ms.append(round((time.time() - t) * 1e3, 1))
+                            paths, z = rm.frame_stats()
+                            logged.append(paths // (W * H))
+                            zero.append(z)
+                            cps.append(round(casts / (W * H * spp), 4))
+                        final = None
+                        if args.final_spp:
+                            pf = rtmi.default_params(rtmi.RT_PRESET_GPU, width=W, height=H,
+                                                     spp=args.final_spp, spp_split=8, seed=seed)
+                            img, casts = rm.render(cam, pf, 1)
+                            paths, z = rm.frame_stats()
+                            rgb8 = rtmi.metrics.argb_to_rgb8(rtmi.pack_argb(img)).astype(np.float64)
+                            final = {"spp": args.final_spp, "logged_avg_path": paths // (W * H),
+                                     "casts_per_sample": round(casts / (W * H * args.final_spp), 4),
+                                     "mean8": round(float(rgb8.mean()), 3)}
+                            key = png_key[scene]
+                            if W == 720 and key in imgs:
+                                bm = rgb8.reshape(16, 45, 16, 45, 3).mean(axis=(1, 3))
+                                rb = np.array(imgs[key]["means"])
+                                d = np.abs(bm - rb)
+                                final.update({"ref_png": imgs[key]["file"], "ref_mean8": round(float(rb.mean()), 3),
+                                              "block_mean_abs_diff": round(float(d.mean()), 3),
+                                              "block_max_abs_diff": round(float(d.max()), 3)})
+                        r = {"scene": spec, "final": final, "mode": mode, "spp": spp, "seed": seed,
+                             "area_per_sample": area, "n_volumes": rm.n_volumes,
+                             "logged_avg_path": logged, "zero_paths": zero,
+                             "zero_frac": [round(z / (W * H * spp), 5) for z in zero],
+                             "casts_per_sample": cps, "ms": ms,
+                             "ref_avg_path": ref[scene]["avg_path_length"][:args.frames],
+                             "ref_zero_paths": ref[scene]["zero_contribution_paths"][:args.frames],
+                             "mean8": float(rtmi.metrics.argb_to_rgb8(rtmi.pack_argb(img)).mean())}
+                        res["runs"].append(r)
+                        print(json.dumps(r), flush=True)
+                    finally:
+                        rm.close()
     with open(os.path.join(args.out, "sarsa_pin.json"), "w") as f:
         json.dump(res, f, indent=1)
 
