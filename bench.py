@@ -36,7 +36,6 @@ import hashlib
 import json
 import os
 import re
-import socket
 import subprocess
 import sys
 import time
@@ -44,11 +43,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def launch_command(argv, n: int, port: int):
+def launch_command(argv, n: int):
     """The torch.distributed.run command that starts n ranks of this script (one per GPU of
-    this node) with the same arguments."""
+    this node) with the same arguments.  --standalone: the launcher's own rendezvous store
+    binds a free port and keeps it (no probe-then-close race for the port); --local-addr pins
+    the address the ranks meet on to 127.0.0.1."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+            "--standalone", "--local-addr=127.0.0.1", os.path.abspath(__file__)] + list(argv)
 
 
 def rank_launch(argv, env) -> int | None:
@@ -71,10 +72,7 @@ def rank_launch(argv, env) -> int | None:
         return None
     if n == 1:
         return None
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = launch_command(argv, n, port)
+    cmd = launch_command(argv, n)
     if env.get("RTMI_BENCH_DRY_RUN") == "1":  # (tests: the command, not the run)
         print(json.dumps(cmd))
         return 0

@@ -182,6 +182,11 @@ int rt_scene_set_accel(rt_scene* scene, int mode);
 /* nodes of the triangle BVH, its depth, nodes of the plane-space BVH (out pointers may
  * be NULL; zeros when the scene has no BVH) */
 int rt_scene_accel_info(const rt_scene* scene, int* n_nodes, int* depth, int64_t* plane_nodes);
+/* The bounce-ray candidate table of hit rule `hit_rule` (no reference counterpart: the
+ * scene's preprocessing, like a BVH build): built on the first render that takes it.
+ * built: 1 once on the device; build_s: host build + upload seconds; bytes: device bytes.
+ * Out pointers may be NULL; zeros before the build or when no render took it. */
+int rt_scene_ctab_info(const rt_scene* scene, int hit_rule, int* built, double* build_s, uint64_t* bytes);
 /* Host only (no GPU): build the BVH of n triangles (n x 9 vertices, the rt_scene_create
  * order) and check its invariants (every triangle in one leaf of each tree, boxes nested
  * and holding their triangles, planes inside their plane-space leaves).  stats
@@ -389,6 +394,13 @@ int rt_sarsa_set_sampling(rt_sarsa* sarsa, int mode);
 #define RT_SARSA_TD_INFRAME 1
 int rt_sarsa_set_td_mode(rt_sarsa* sarsa, int mode);
 int rt_sarsa_get_td_mode(const rt_sarsa* sarsa, int* mode);
+/* Paths in flight of the in-frame rule's render.  Its races -- and with them how fast a frame
+ * learns -- depend on how many paths update the table at once: the reference's GTX 1070 Ti
+ * holds at most 19 SMs x 2048 threads = 38,912.  lanes > 0 caps the render's persistent grid
+ * at ceil(lanes / 256) workgroups of 256 lanes (the image and its statistics are then
+ * rendered by fewer lanes, each taking more work items); 0 (default): the device's full
+ * occupancy.  No effect on the frame-synchronous rule's results. */
+int rt_sarsa_set_inframe_lanes(rt_sarsa* sarsa, int lanes);
 /* Training statistics of the last frame rendered (GPU/main.cu:321-339, one line of
  * Radiance_Map_Data/sarsa_training_stats.txt per frame): path_floor_sum = the sum over the
  * frame's pixels of int(path lengths / spp) (path_trace_reinforcement,

@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <chrono>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -82,6 +84,9 @@ struct rt_scene {
     // bounce-ray candidate table (rt_ctab.cpp): built on the first render that can use it
     // (scene_ensure_ctab), its device arrays in dev.ctab*
     bool ctab_tried[2] = {false, false};  // per hit rule
+    std::mutex ctab_mu;                    // (renders of one scene from several threads)
+    double ctab_build_s[2] = {0.0, 0.0};   // host build + upload, seconds (rt_scene_ctab_info)
+    uint64_t ctab_bytes[2] = {0, 0};       // device bytes of the table
 };
 
 namespace {
@@ -305,17 +310,41 @@ int check_params(const rt_params* p) {
 void isect_record(const float* v, float4* out);
 
 // The bounce-ray candidate table of a scene for hit rule `rule` (rt_ctab.cpp), built and
-// uploaded once, on the first render that can use it: scenes of at most 256 triangles with
-// the matrix-core image (whose origin bound it shares); rule 0 serves t_scale >= kCtabTsMin.
-// A lazily built cache of the scene (hence the const_cast); RT_CTAB=0 leaves the bounce
-// casts on the image's masks (A/B builds).  A scene the table cannot be built for keeps
-// the image.
+// uploaded once, on the first render that will take it (ctab_wanted: the launchers' own
+// predicates); rule 0 serves t_scale >= kCtabTsMin.  A lazily built cache of the scene
+// (hence the const_cast), guarded by the scene's mutex.  RT_CTAB=0 leaves the bounce casts on
+// the image's masks (A/B builds).  The table is an accelerator, never required: a scene it
+// cannot be built or uploaded for (host build refused, device memory short) keeps the image,
+// and the render goes on (RT_CTAB_TEST_FAIL=1 forces the upload failure, for the tests).
 }  // namespace
 namespace rt {
-int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
+bool ctab_wanted(const rt_scene* sc, const rt_camera* cam, const rt_params* p, int user) {
+    const DeviceScene& d = sc->dev;
+    if (d.mf_frag == nullptr || d.n_surf <= 0 || d.n_tri > 64 * kCtabMaxWords || scene_uses_bvh(sc)) return false;
+    if (!filter_usable(d, cam->pos[0], cam->pos[1], cam->pos[2], p->t_scale)) return false;
+    const float cb = d.mf_bound;
+    const bool cam_in = fabsf(cam->pos[0]) <= cb && fabsf(cam->pos[1]) <= cb && fabsf(cam->pos[2]) <= cb;
+    const bool t_ok = p->t_scale > 0.0f && p->t_scale <= kFiltMaxTScale;
+    // the launch's pitch rotation is the identity (make_launch's cos_x / sin_x)
+    const bool pitch0 = (float)cos((double)cam->yaw_x) == 1.0f && (float)sin((double)cam->yaw_x) == 0.0f;
+    switch (user) {
+        case kCtabForRender:  // launch_render_t: k_render_ps<.., CT> (CPU preset), k_render_pq<.., CT> (GPU)
+            if (p->preset == RT_PRESET_CPU) return d.n_tri <= 64;
+            return cam_in && t_ok && pitch0;
+        case kCtabForDqn:  // launch_dqn_bounce: dqn_mf > 0
+            return cam_in && t_ok;
+        case kCtabForSarsa:  // k_sarsa_render_pq<.., CT> (built, off by default: RT_SARSA_CTAB)
+            return sarsa_ctab_compiled() && t_ok;
+    }
+    return false;
+}
+
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale, bool wanted) {
     rt_scene* sc = const_cast<rt_scene*>(scene);
     if (rule != 0 && rule != 1) return RT_OK;
-    if (sc->ctab_tried[rule] || (rule == 0 && !(t_scale >= kCtabTsMin))) return RT_OK;
+    if (!wanted || (rule == 0 && !(t_scale >= kCtabTsMin))) return RT_OK;
+    std::lock_guard<std::mutex> lock(sc->ctab_mu);
+    if (sc->ctab_tried[rule]) return RT_OK;
     sc->ctab_tried[rule] = true;
     static const bool ctab_on = getenv("RT_CTAB") == nullptr || atoi(getenv("RT_CTAB")) != 0;
     const int n = sc->dev.n_tri, n_surf = sc->dev.n_surf;
@@ -323,13 +352,16 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
     std::vector<float4> isect((size_t)n * kIsectF4);
     for (int i = 0; i < n; ++i) isect_record(sc->tri.data() + (size_t)i * 9, &isect[(size_t)i * 3]);
     CtabHost ct;
+    const auto t0 = std::chrono::steady_clock::now();
     if (!ctab_build(isect.data(), n, n_surf, (double)sc->dev.mf_bound, rule, kCtabTsMin, &ct)) return RT_OK;
     int rc = set_device(sc->ctx);
     if (rc != RT_OK) return rc;
     unsigned long long *dm = nullptr, *dd = nullptr, *dc = nullptr;
     uint16_t* dg = nullptr;
     float4* dt = nullptr;
-    hipError_t e = hipMalloc(&dm, sizeof(uint64_t) * ct.masks.size());
+    const char* force = getenv("RT_CTAB_TEST_FAIL");
+    hipError_t e = (force && atoi(force) != 0) ? hipErrorOutOfMemory : hipSuccess;
+    if (e == hipSuccess) e = hipMalloc(&dm, sizeof(uint64_t) * ct.masks.size());
     if (e == hipSuccess) e = hipMalloc(&dd, sizeof(uint64_t) * ct.gdict.size());
     if (e == hipSuccess) e = hipMalloc(&dg, sizeof(uint16_t) * ct.gid.size());
     if (e == hipSuccess) e = hipMalloc(&dc, sizeof(uint64_t) * ct.cop.size());
@@ -345,7 +377,14 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
         if (dg) (void)hipFree(dg);
         if (dc) (void)hipFree(dc);
         if (dt) (void)hipFree(dt);
-        return fail(RT_E_HIP, "candidate table upload failed: %s", hipGetErrorString(e));
+        (void)hipGetLastError();  // the failed allocation must not fail the render's own launches
+        static bool warned = false;
+        if (!warned) {
+            warned = true;
+            fprintf(stderr, "rtmi: candidate table upload failed (%s); the bounce casts stay on the matrix-core image\n",
+                    hipGetErrorString(e));
+        }
+        return RT_OK;
     }
     CtabDev& t = sc->dev.ctab[rule];
     t.masks = dm;
@@ -359,6 +398,9 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale) {
     t.words = ct.words;
     t.bins = kCtabBins;
     t.graze_n = kCtabGraze;
+    sc->ctab_build_s[rule] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    sc->ctab_bytes[rule] = sizeof(uint64_t) * (ct.masks.size() + ct.gdict.size() + ct.cop.size()) +
+                           sizeof(uint16_t) * ct.gid.size() + sizeof(float4) * ct.tri.size();
     return RT_OK;
 }
 }  // namespace rt
@@ -823,6 +865,17 @@ int rt_scene_destroy(rt_scene* scene) {
     return RT_OK;
 }
 
+int rt_scene_ctab_info(const rt_scene* scene, int hit_rule, int* built, double* build_s, uint64_t* bytes) {
+    if (!scene) return fail(RT_E_INVALID, "scene is NULL");
+    if (hit_rule != RT_HIT_RULE_CPU && hit_rule != RT_HIT_RULE_GPU) return fail(RT_E_INVALID, "bad hit_rule %d", hit_rule);
+    std::lock_guard<std::mutex> lock(const_cast<rt_scene*>(scene)->ctab_mu);
+    const bool on = scene->dev.ctab[hit_rule].masks != nullptr;
+    if (built) *built = on ? 1 : 0;
+    if (build_s) *build_s = on ? scene->ctab_build_s[hit_rule] : 0.0;
+    if (bytes) *bytes = on ? scene->ctab_bytes[hit_rule] : 0;
+    return RT_OK;
+}
+
 int rt_scene_set_accel(rt_scene* scene, int mode) {
     if (!scene) return fail(RT_E_INVALID, "scene is NULL");
     if (mode != RT_ACCEL_AUTO && mode != RT_ACCEL_SCAN && mode != RT_ACCEL_BVH)
@@ -1069,7 +1122,8 @@ int rt_render(rt_ctx* ctx, const rt_scene* scene, const rt_camera* cam, const rt
     float* d_out = nullptr;
     unsigned long long* d_casts = nullptr;
     const size_t out_bytes = sizeof(float) * 3 * (size_t)w * (size_t)h;
-    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale);
+    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale,
+                               rt::ctab_wanted(scene, cam, params, rt::kCtabForRender));
     if (rc != RT_OK) return rc;
     hipError_t e = hipMalloc(&d_blocks, sizeof(rt::BlockDesc) * blocks.size());
     if (e == hipSuccess) e = hipMalloc(&d_out, out_bytes);
@@ -1122,7 +1176,8 @@ int rt_render_tiles_device(rt_ctx* ctx, const rt_scene* scene, const rt_camera* 
     int n_blocks = 0;
     rc = rt::ctx_blocks(ctx, tiles, n_tiles, tile_size, params->width, params->height, &d_blocks, &n_blocks);
     if (rc != RT_OK) return rc;
-    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale);
+    rc = rt::scene_ensure_ctab(scene, params->hit_rule, params->t_scale,
+                               rt::ctab_wanted(scene, cam, params, rt::kCtabForRender));
     if (rc != RT_OK) return rc;
     rt::RenderLaunch a = make_launch(scene, cam, params);
     a.blocks = d_blocks;

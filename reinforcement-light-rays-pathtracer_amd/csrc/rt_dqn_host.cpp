@@ -24,7 +24,8 @@ int set_error(int code, const char* msg);
 int ctx_device(const rt_ctx* ctx);
 const DeviceScene& scene_device(const rt_scene* s);
 DeviceScene scene_launch_view(const rt_scene* s);
-int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale);
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale, bool wanted);
+bool ctab_wanted(const rt_scene* sc, const rt_camera* cam, const rt_params* p, int user);
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 }  // namespace rt
@@ -421,7 +422,7 @@ int run_dqn(rt_ctx* ctx, const rt_scene* scene, const rt_dqn* dqn, const rt_came
     int rc = ws->ensure(n_pix * in_flight);
     if (rc != RT_OK) return rc;
     // the bounce casts' candidate table (rule 1: the GPU engine's hit rule), built on the first render
-    rc = rt::scene_ensure_ctab(scene, 1, p->t_scale);
+    rc = rt::scene_ensure_ctab(scene, 1, p->t_scale, rt::ctab_wanted(scene, cam, p, rt::kCtabForDqn));
     if (rc != RT_OK) return rc;
     rt::DqnLaunch a;
     memset(&a, 0, sizeof(a));

@@ -148,6 +148,8 @@ constexpr int kCtabGraze = RT_CTAB_GRAZE;
 constexpr float kCtabTsMin = 256.0f;  // the smallest t_scale the table serves
 constexpr float kCtabHemi = 2e-6f;    // directions with d.N_s < -kCtabHemi (off s's hemisphere) keep every triangle
 constexpr int kCtabMaxWords = 4;  // mask words per entry: scenes of at most 256 triangles
+// the render paths that may take the table (rt_capi.cpp ctab_wanted)
+constexpr int kCtabForRender = 0, kCtabForDqn = 1, kCtabForSarsa = 2;
 struct CtabHost {
     int n_tri = 0, n_surf = 0, n_patch = 0;
     int words = 1;        // ceil(n_tri / 64): masks, graze and cop hold that many words per entry
@@ -402,6 +404,7 @@ struct SarsaMap {
     int n_kd = 0;
     float root_x = 0.f, root_y = 0.f, root_z = 0.f;  // position of KD element 0 (0 if internal)
     float max_dist = 0.003f;            // MAX_DIST (compared with delta^2)
+    int max_wgs = 0;                    // host: cap on the persistent render's workgroups (0: none)
     // Exact fast path of the nearest-volume search (rt_sarsa.hip sarsa_nearest_grid):
     // per normal class (volumes whose normals compare equal), a uniform grid of cell
     // size >= grid_h over the class's volume positions.

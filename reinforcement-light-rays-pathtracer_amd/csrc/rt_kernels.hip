@@ -944,7 +944,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #endif
         Hit h;
         if constexpr (use_ctab)
-            h = closest_hit_ctab<RULE, 1>(ms, ms.ctab[RULE], s_tri, o, d, a.t_scale, live, wl);
+            h = closest_hit_ctab<RULE, 1, kCtPairCap>(ms, ms.ctab[RULE], s_tri, o, d, a.t_scale, live, wl);
         else if (use_mf)
 #if RT_PROF
             h = closest_hit_mf<RULE, false, (MF > 0 ? MF : 1)>(ms, o, d, a.t_scale, live, wl, nullptr, &tm);
@@ -1085,8 +1085,10 @@ __global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_
     if (MF > 0) {
         extern __shared__ float s_ps[];
         float* const mf_base = s_ps + (size_t)4 * ps_wave_floats(a.per_chunk);
-        wl = mf_base + (size_t)(threadIdx.x >> 6) * kMfWaveFloats;
-        float* next = mf_base + 4 * kMfWaveFloats;
+        // (the table route's wave blocks hold a shorter pair list: mf_wave_floats)
+        constexpr int wf = CT ? mf_wave_floats(kCtPairCap, RULE) : kMfWaveFloats;
+        wl = mf_base + (size_t)(threadIdx.x >> 6) * wf;
+        float* next = mf_base + 4 * wf;
 #if RT_PS_SCENE_LDS
         // hit-test and shading records of the scene (divergent per-lane reads: LDS latency
         // instead of L1/L2)
@@ -1096,11 +1098,12 @@ __global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_
             float4* ls = li + (size_t)n * kIsectF4;
             for (int i = threadIdx.x; i < n * kIsectF4; i += 256) li[i] = a.scene.isect[i];
             ms.isect = li;
-            if (RT_PS_SHADE_LDS) {
+            constexpr bool shade_lds = RT_PS_SHADE_LDS && (!CT || RT_PS_CT_SHADE_LDS);
+            if (shade_lds) {
                 for (int i = threadIdx.x; i < n * kShadeF4; i += 256) ls[i] = a.scene.shade[i];
                 ms.shade = ls;
             }
-            next = reinterpret_cast<float*>(ls + (RT_PS_SHADE_LDS ? (size_t)n * kShadeF4 : 0));
+            next = reinterpret_cast<float*>(ls + (shade_lds ? (size_t)n * kShadeF4 : 0));
         }
 #endif
 #if RT_MF_LDS
@@ -1257,9 +1260,10 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                             a.t_scale >= T.ts_min && T.words == 1;
             size_t mf_lds = 0;
             if (RT_MF && a.scene.mf_frag != nullptr) {
-                mf_lds = (size_t)4 * kMfWaveFloats * sizeof(float);
+                mf_lds = (size_t)4 * (ct ? mf_wave_floats(kCtPairCap, RULE) : kMfWaveFloats) * sizeof(float);
                 if (RT_PS_SCENE_LDS)
-                    mf_lds += (size_t)a.scene.n_tri * (kIsectF4 + (RT_PS_SHADE_LDS ? kShadeF4 : 0)) * sizeof(float4);
+                    mf_lds += (size_t)a.scene.n_tri *
+                              (kIsectF4 + (RT_PS_SHADE_LDS && (!ct || RT_PS_CT_SHADE_LDS) ? kShadeF4 : 0)) * sizeof(float4);
                 if (RT_MF_LDS && !ct) mf_lds += (size_t)mf_groups(a.scene.n_tri) * 64 * sizeof(uint4);
             }
             const dim3 grid((unsigned)(a.n_blocks * a.split));

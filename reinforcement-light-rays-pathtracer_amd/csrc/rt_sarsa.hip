@@ -485,9 +485,10 @@ __device__ void sarsa_sample_max(const SarsaMap& m, int rv, const VolPre& vp, fl
         const float* q = m.Q + (size_t)rv * kSarsaSectors;
         mi = 0;
         float mq = live_load(q);
-        // from k = 0, as the reference's scan (radiance_volume.cu:251-257 reads grid[0] twice):
-        // in this racy mode the second read of q[0] may see another lane's update
-        for (int k = 0; k < kSarsaSectors; ++k) {
+        // the reference's scan (radiance_volume.cu:251-257) starts at i = 0 with grid[0] already
+        // loaded; its plain (non-volatile) loads let the compiler read grid[0] once, so the
+        // k = 0 step (mq < q[0] with mq = q[0]) is skipped: 144 device-scope loads, not 145
+        for (int k = 1; k < kSarsaSectors; ++k) {
             const float v = live_load(q + k);
             if (mq < v) {
                 mq = v;
@@ -1152,7 +1153,9 @@ hipError_t launch_sarsa_render_t(const RenderLaunch& a, const SarsaMap& m, hipSt
         (void)hipMemsetAsync(a.work, 0, sizeof(unsigned long long), stream);
         // as many workgroups as fit: RT_SARSA_WAVES per CU (registers and the k-d stack's LDS)
         const int per_cu = a.scene.bvh_nodes != nullptr ? RT_SARSA_BVH_WAVES : (mf ? RT_MF_SARSA_WAVES : RT_SARSA_WAVES);
-        const dim3 grid((unsigned)min(a.n_blocks * a.split, per_cu * device_cu_count()));
+        int wgs = min(a.n_blocks * a.split, per_cu * device_cu_count());
+        if (m.max_wgs > 0) wgs = min(wgs, m.max_wgs);  // rt_sarsa_set_inframe_lanes
+        const dim3 grid((unsigned)wgs);
         if constexpr (RT_MF_SARSA) {
             if (mf) {
                 if (a.hit_rule == 0 && one)

@@ -32,7 +32,8 @@ void scene_host(const rt_scene* s, const float** tri, const float** normals, con
 int ctx_blocks(rt_ctx* ctx, const int32_t* tiles, int n_tiles, int tile_size, int width, int height,
                const BlockDesc** d_blocks, int* n_blocks);
 RenderLaunch render_launch(const rt_scene* scene, const rt_camera* cam, const rt_params* p);
-int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale);
+int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale, bool wanted);
+bool ctab_wanted(const rt_scene* sc, const rt_camera* cam, const rt_params* p, int user);
 
 // read_hemisphere_locations_and_normals (GPU/utils/hemisphere_helpers.cu:230-278): one
 // "x y z nx ny nz" per line, tokens split on ' ' and read with std::stof, the first
@@ -414,7 +415,7 @@ int check_sarsa_params(const rt_params* p) {
 int render_frame(rt_sarsa* sa, const rt_scene* scene, const rt_camera* cam, const rt_params* p,
                  const rt::BlockDesc* d_blocks, int n_blocks, int clip_x1, int clip_y1, int out_pitch,
                  float* d_out, unsigned long long* d_casts, hipStream_t stream, bool apply) {
-    const int rc = rt::sarsa_ctab_compiled() ? rt::scene_ensure_ctab(scene, p->hit_rule, p->t_scale) : RT_OK;
+    const int rc = rt::scene_ensure_ctab(scene, p->hit_rule, p->t_scale, rt::ctab_wanted(scene, cam, p, rt::kCtabForSarsa));
     if (rc != RT_OK) return rc;
     rt::RenderLaunch a = rt::render_launch(scene, cam, p);
     a.blocks = d_blocks;
@@ -915,6 +916,13 @@ int rt_sarsa_set_td_mode(rt_sarsa* sa, int mode) {
     if (!sa) return err(RT_E_INVALID, "NULL argument");
     if (mode != RT_SARSA_TD_FRAME && mode != RT_SARSA_TD_INFRAME) return err(RT_E_INVALID, "bad TD mode");
     sa->m.td_inframe = mode == RT_SARSA_TD_INFRAME;
+    return RT_OK;
+}
+
+int rt_sarsa_set_inframe_lanes(rt_sarsa* sa, int lanes) {
+    if (!sa) return err(RT_E_INVALID, "NULL argument");
+    if (lanes < 0) return err(RT_E_INVALID, "lanes must be >= 0");
+    sa->m.max_wgs = lanes == 0 ? 0 : (int)(((int64_t)lanes + 255) / 256);
     return RT_OK;
 }
 

@@ -529,6 +529,17 @@ __device__ __forceinline__ float exact_tv(const float4* __restrict__ tri, int i,
 constexpr int kMfPairCap = RT_MF_PAIR_CAP;
 constexpr int kMfWaveFloats = 6 * 64 + kMfPairCap / 2 + (RT_MF_TV_LDS ? kMfPairCap : 0);
 static_assert(kMfWaveFloats >= 11 * 64, "cand_exact_min's LDS (rays, first, mask, key) fits a wave's block");
+// The table-route kernel k_render_ps<.., CT> (RULE 0): about 3 candidates per ray of which the
+// lane tests its first RT_CTAB_OWN itself, so the shared phase lists a few dozen pairs per wave;
+// a smaller list block (with RT_PS_CT_SHADE_LDS) lets one more workgroup fit a CU's LDS
+#ifndef RT_PS_CT_PAIR_CAP
+#define RT_PS_CT_PAIR_CAP 96  // (64 / 96 / 128 / 256: 2.37 / 2.33 / 2.34 / 2.63 ms with the shading records in L1/L2)
+#endif
+constexpr int kCtPairCap = RT_PS_CT_PAIR_CAP;
+__host__ __device__ constexpr int mf_wave_floats(int cap, int rule) {
+    return (rule == 1 && 6 * 64 + cap / 2 + (RT_MF_TV_LDS ? cap : 0) < 11 * 64) ? 11 * 64
+                                                                              : 6 * 64 + cap / 2 + (RT_MF_TV_LDS ? cap : 0);
+}
 
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
@@ -536,7 +547,7 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // wave: the lanes' candidate pairs are listed in LDS in (lane, index) order and tested
 // 64 at a time by all lanes, then each lane folds its own results in index order.  The
 // trip count is (candidates of the wave) / 64 instead of the largest per-lane count.
-template <int RULE>
+template <int RULE, int CAP = kMfPairCap>
 __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, int tri0, uint64_t F, f3 o,
                                               float nDx, float nDy, float nDz, float* wl, int lane, Hit& h) {
     const int cnt = __builtin_popcountll(F);  // 0..64: 7 bits
@@ -555,21 +566,21 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
     // the lane's pairs not yet folded (lowest bit first) and the list position of the next
     uint64_t R = F;
     int pos = excl;
-    for (int cb = 0; cb < total; cb += kMfPairCap) {
+    for (int cb = 0; cb < total; cb += CAP) {
         {
             uint64_t G = F;
             int p = excl - cb;
             while (G != 0ull) {
                 const int b = __builtin_ctzll(G);
                 G &= G - 1ull;
-                if (p >= 0 && p < kMfPairCap) pr[p] = (uint16_t)((lane << 6) | b);
+                if (p >= 0 && p < CAP) pr[p] = (uint16_t)((lane << 6) | b);
                 ++p;
             }
         }
         wave_lds_sync();
-        const int nb = min(kMfPairCap, total - cb);
+        const int nb = min(CAP, total - cb);
 #if RT_MF_TV_LDS
-        float* tv = wl + 6 * 64 + kMfPairCap / 2;
+        float* tv = wl + 6 * 64 + CAP / 2;
         for (int k = lane; k < nb; k += 64) {
             const uint32_t q = pr[k];
             const int rl = (int)(q >> 6);
@@ -584,7 +595,7 @@ __device__ __forceinline__ void mf_exact_wave(const float4* __restrict__ isect, 
             while (G != 0ull) {
                 const int b = __builtin_ctzll(G);
                 G &= G - 1ull;
-                if (p >= 0 && p < kMfPairCap) {
+                if (p >= 0 && p < CAP) {
                     const float t = tv[p];
                     if ((RULE == 0) ? (t < h.t + kEps) : (t < h.t)) {
                         h.t = t;
@@ -963,7 +974,7 @@ __device__ __forceinline__ void cand_exact_min(const float4* __restrict__ isect,
     wave_lds_sync();
 }
 
-template <int RULE, int NW>
+template <int RULE, int NW, int CAP = kMfPairCap>
 __device__ __forceinline__ Hit closest_hit_cand(const DeviceScene& s, uint64_t (&F)[NW], f3 o, f3 d, float t_scale,
                                                 float* wl) {
     const float nDx = -(d.x * t_scale);
@@ -1015,11 +1026,11 @@ __device__ __forceinline__ Hit closest_hit_cand(const DeviceScene& s, uint64_t (
     } else {
 #pragma unroll
         for (int w = 0; w < NW; ++w)
-            if (64 * w < s.n_tri) mf_exact_wave<RULE>(s.isect, 64 * w, F[w], o, nDx, nDy, nDz, wl, lane, h);
+            if (64 * w < s.n_tri) mf_exact_wave<RULE, CAP>(s.isect, 64 * w, F[w], o, nDx, nDy, nDz, wl, lane, h);
     }
     return h;
 }
-template <int RULE, int NW>
+template <int RULE, int NW, int CAP = kMfPairCap>
 __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const CtabDev& T, int surf, f3 o, f3 d,
                                                 float t_scale, bool active, float* wl) {
     uint64_t F[NW];
@@ -1029,7 +1040,7 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const Ctab
 #pragma unroll
         for (int k = 0; k < NW; ++k) F[k] = 0ull;
     }
-    return closest_hit_cand<RULE, NW>(s, F, o, d, t_scale, wl);
+    return closest_hit_cand<RULE, NW, CAP>(s, F, o, d, t_scale, wl);
 }
 
 #ifndef RT_FILTER
@@ -1043,6 +1054,12 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const Ctab
 #endif
 #ifndef RT_PS_SHADE_LDS
 #define RT_PS_SHADE_LDS 1  // 0: with RT_PS_SCENE_LDS, only the isect records in LDS (shading from L1/L2)
+#endif
+#ifndef RT_PS_CT_SHADE_LDS
+// the table-route kernel's shading records: from L1/L2 (0) -- with the shorter pair list it keeps
+// the workgroup at 29.4 KB of LDS, five per CU (Cornell 512^2 x 256: 2.33 ms, in LDS 2.37-2.40;
+// the 35.6-KB layout of round 5 held four per CU: 2.63 ms, profiles/r6f/ab.log)
+#define RT_PS_CT_SHADE_LDS 0
 #endif
 #ifndef RT_MF_LDS
 #define RT_MF_LDS 0  // 1: k_render_ps reads the image from a workgroup copy in LDS (0: global)

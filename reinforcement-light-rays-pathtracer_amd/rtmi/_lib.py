@@ -56,11 +56,11 @@ EXPORTS = (
     "rt_sarsa_nearest", "rt_render_sarsa", "rt_render_sarsa_tiles_device", "rt_sarsa_td_device",
     "rt_sarsa_apply", "rt_sarsa_set_search", "rt_sarsa_search_stats", "rt_sarsa_save_q",
     "rt_neuralq_create", "rt_neuralq_destroy", "rt_neuralq_epsilon", "rt_neuralq_render_frame",
-    "rt_sarsa_save_selected", "rt_sarsa_load_q", "rt_sarsa_set_sampling", "rt_sarsa_set_td_mode", "rt_sarsa_get_td_mode", "rt_sarsa_frame_stats",
+    "rt_sarsa_save_selected", "rt_sarsa_load_q", "rt_sarsa_set_sampling", "rt_sarsa_set_td_mode", "rt_sarsa_get_td_mode", "rt_sarsa_set_inframe_lanes", "rt_sarsa_frame_stats",
     "rt_dqn_save_selected",
     "rt_dqn_trainer_create", "rt_dqn_trainer_destroy", "rt_dqn_trainer_params", "rt_dqn_train_step_device",
     "rt_dqn_td_targets_device",
-    "rt_scene_set_accel", "rt_scene_accel_info", "rt_bvh_check",
+    "rt_scene_set_accel", "rt_scene_accel_info", "rt_scene_ctab_info", "rt_bvh_check",
     "rt_ktime_enable", "rt_ktime_read", "rt_ktime_name",
 )
 
@@ -114,6 +114,8 @@ def _declare(lib):
         "rt_intersect_method": (i, [_P, _P, _FP, _FP, i, f, i, i, _FP, _IP, _IP]),
         "rt_scene_set_accel": (i, [_P, i]),
         "rt_scene_accel_info": (i, [_P, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(ctypes.c_int64)]),
+        "rt_scene_ctab_info": (i, [_P, i, ctypes.POINTER(i), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_uint64)]),
         "rt_bvh_check": (i, [_FP, i, ctypes.POINTER(ctypes.c_int64)]),
         "rt_render": (i, [_P, _P, ctypes.POINTER(RtCamera), ctypes.POINTER(RtParams), i, i, i, i,
                           _FP, _U64P]),
@@ -156,6 +158,7 @@ def _declare(lib):
         "rt_sarsa_set_search": (i, [_P, i]),
         "rt_sarsa_set_sampling": (i, [_P, i]),
         "rt_sarsa_set_td_mode": (i, [_P, i]),
+        "rt_sarsa_set_inframe_lanes": (i, [_P, i]),
         "rt_sarsa_get_td_mode": (i, [_P, _IP]),
         "rt_neuralq_create": (i, [_P, _P, _P, i, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                   ctypes.POINTER(_P)]),

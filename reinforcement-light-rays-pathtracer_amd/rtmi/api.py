@@ -180,6 +180,14 @@ class Scene:
         check(lib().rt_scene_accel_info(self._h, ctypes.byref(nodes), ctypes.byref(depth), ctypes.byref(gl)))
         return {"nodes": nodes.value, "depth": depth.value, "plane_nodes": gl.value}
 
+    def ctab_info(self, hit_rule: int) -> dict:
+        """the bounce-ray candidate table of a hit rule: built, host build + upload seconds,
+        device bytes (rt_scene_ctab_info; zeros until a render takes it)"""
+        built, secs, nbytes = ctypes.c_int(0), ctypes.c_double(0.0), ctypes.c_uint64(0)
+        check(lib().rt_scene_ctab_info(self._h, hit_rule, ctypes.byref(built), ctypes.byref(secs),
+                                       ctypes.byref(nbytes)))
+        return {"built": bool(built.value), "build_s": secs.value, "bytes": int(nbytes.value)}
+
     def normals(self) -> np.ndarray:
         out = np.zeros((self.geom.n_tri, 3), np.float32)
         check(lib().rt_scene_normals(self._h, _fp(out)))

@@ -84,6 +84,23 @@ def synthetic_weights(n_in: int, seed: int = 1984, hidden=HIDDEN, n_out: int = A
     return W, b
 
 
+def glorot_weights(n_in: int, seed: int = 1984, hidden=HIDDEN, n_out: int = ACTIONS) -> Tuple[list, list]:
+    """DyNet's default initialiser, the one the reference's network starts from (FCLayer's
+    model.add_parameters with no initializer, NN_Builders/fc_layer.cu:32-33: ParameterInitGlorot,
+    gain 1): uniform in +-sqrt(6 / sum of the tensor's dims) -- sqrt(6 / (out + in)) for a weight
+    matrix, sqrt(6 / out) for a bias -- here from numpy's PCG64 seeded with `seed` (DyNet's own
+    random stream is not reproducible without DyNet)."""
+    rng = np.random.default_rng(seed)
+    dims = [n_in, *hidden, n_out]
+    W, b = [], []
+    for i in range(4):
+        sw = np.sqrt(6.0 / (dims[i + 1] + dims[i]))
+        W.append(rng.uniform(-sw, sw, (dims[i + 1], dims[i])).astype(np.float32))
+        sb = np.sqrt(6.0 / dims[i + 1])
+        b.append(rng.uniform(-sb, sb, dims[i + 1]).astype(np.float32))
+    return W, b
+
+
 class Dqn:
     def __init__(self, ctx: Context, nn_vertices: np.ndarray, W: Sequence[np.ndarray],
                  b: Sequence[np.ndarray]):

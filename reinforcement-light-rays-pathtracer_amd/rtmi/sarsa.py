@@ -93,6 +93,11 @@ class RadianceMap:
         in-frame read-modify-write, radiance_volume.cu:282-301; racy, one GPU only)."""
         check(lib().rt_sarsa_set_td_mode(self._h, mode))
 
+    def set_inframe_lanes(self, lanes: int) -> None:
+        """paths in flight of the in-frame rule's render (0: the device's full occupancy;
+        the reference's GTX 1070 Ti holds 38,912): rt_sarsa_set_inframe_lanes"""
+        check(lib().rt_sarsa_set_inframe_lanes(self._h, lanes))
+
     @property
     def td_mode(self) -> int:
         """the map's TD rule, read from the library (rt_sarsa_get_td_mode)"""

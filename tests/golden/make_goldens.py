@@ -145,11 +145,15 @@ def nn_training_stats(ref):
     out = {}
     for key, fname, model in (("door_room_12_12", "door_room_12_12_stats.txt", "door_room_12_12.model"),
                               ("cornell_12_12", "cornell_stats_12_12.txt", "cornell_12_12.model"),
-                              ("cornell_no_decay", "cornell_no_decay.txt", "cornell_no_decay.model")):
+                              ("cornell_no_decay", "cornell_no_decay.txt", "cornell_no_decay.model"),
+                              # (runs whose networks the reference does not ship)
+                              ("archway_12_12", "archway_12_12.txt", None),
+                              ("complex_light_room_12_12", "complex_light_room_12_12.txt", None),
+                              ("nn_training_stats", "nn_training_stats.txt", None)):
         rows = [[float(x) for x in line.split()] for line in open(os.path.join(ref, "Radiance_Map_Data", fname))
                 if line.strip()]
         tail = rows[-10:]
-        out[key] = {"file": "Radiance_Map_Data/" + fname, "model": "Radiance_Map_Data/" + model,
+        out[key] = {"file": "Radiance_Map_Data/" + fname, "model": model and "Radiance_Map_Data/" + model,
                     "avg_path_length": [r[0] for r in rows], "loss": [r[1] for r in rows],
                     "zero_contribution_paths": [r[2] for r in rows],
                     "last10_mean_path_length": round(sum(r[0] for r in tail) / len(tail), 4)}

@@ -5,7 +5,6 @@ everything bit-exact against one process).  The file sorts first: the launcher i
 before this pytest process has touched the GPU."""
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -16,12 +15,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.gpu
 def test_two_process_tiles_and_td_exchange(tmp_path):
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
     out = tmp_path / "mp.json"
+    # --standalone: the launcher's rendezvous store binds a free port itself (no probe race)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "tools", "multiproc_gpu_check.py"), "--out", str(out)]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert out.exists(), (r.returncode, r.stdout[-2000:], r.stderr[-4000:])

@@ -94,8 +94,9 @@ def test_ctab_keeps_every_pass(rtmi_mod, oracle_mod, kind, rule):
     cand, stats = rtmi_mod.ctab_candidates(tri, n_surf, surf, o, d, hit_rule=rule)
     assert stats[0] > 0 and stats[2] > 0
     assert cand.shape == (o.shape[0], (tri.shape[0] + 63) // 64)
-    # rule 0: the t_scale the table serves (>= 256); rule 1: any
-    for ts in ((256.0, 512.0, 720.0, 4096.0) if rule == 0 else (1.0, 256.0, 720.0, 1024.0)):
+    # rule 0: the t_scale the table serves (>= 256); rule 1: any -- up to kFiltMaxTScale (16384),
+    # the largest the launchers serve it at, where ET (rt_bounds.hpp) is sized
+    for ts in ((256.0, 512.0, 720.0, 4096.0, 16384.0) if rule == 0 else (0.01, 1.0, 256.0, 720.0, 1024.0, 16384.0)):
         passes = oracle_mod.pass_masks(tri, o, d, ts, rule)
         missed = passes & ~cand
         bad = np.nonzero(missed.any(axis=1))[0]
@@ -132,3 +133,52 @@ def test_ctab_refuses_large_scenes(rtmi_mod):
     with pytest.raises(rtmi_mod.RtError):
         rtmi_mod.ctab_candidates(tri, n_surf, np.zeros(1, np.int32), np.zeros((1, 3), np.float32),
                                  np.asarray([[0.0, 0.0, 1.0]], np.float32), hit_rule=1)
+
+
+# ---------------------------------------------------------------- GPU ----------
+
+def _cornell_frame(rtmi_mod, ctx, sc, preset, yaw_x=0.0):
+    # (t_scale = the height: rule 0's table serves t_scale >= 256)
+    p = rtmi_mod.default_params(preset, width=64, height=256, spp=8, spp_split=4)
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["cornell"])
+    cam.yaw_x = yaw_x
+    return rtmi_mod.render(ctx, sc, cam, p)
+
+
+@pytest.mark.gpu
+def test_gpu_table_upload_failure_keeps_the_image(rtmi_mod, gpu_ctx, monkeypatch):
+    """A table that cannot be uploaded (device memory short: forced by RT_CTAB_TEST_FAIL) is
+    skipped, not an error: the render goes on with the matrix-core image's masks -- the same
+    image and casts bit for bit -- and the scene reports no table."""
+    g = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_CPU)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        ref = _cornell_frame(rtmi_mod, gpu_ctx, sc, rtmi_mod.RT_PRESET_CPU)
+        info = sc.ctab_info(rtmi_mod.RT_HIT_RULE_CPU)
+        assert info["built"] and info["bytes"] > 0 and info["build_s"] > 0, info
+    monkeypatch.setenv("RT_CTAB_TEST_FAIL", "1")
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        img, casts = _cornell_frame(rtmi_mod, gpu_ctx, sc, rtmi_mod.RT_PRESET_CPU)
+        assert not sc.ctab_info(rtmi_mod.RT_HIT_RULE_CPU)["built"]
+        assert casts == ref[1] and np.array_equal(img, ref[0])
+        img2, casts2 = _cornell_frame(rtmi_mod, gpu_ctx, sc, rtmi_mod.RT_PRESET_CPU)  # later calls too
+        assert casts2 == ref[1] and np.array_equal(img2, ref[0])
+
+
+@pytest.mark.gpu
+def test_gpu_table_built_only_for_a_launch_that_takes_it(rtmi_mod, gpu_ctx):
+    """The GPU preset's table route needs the camera inside the image's bound and pitch 0;
+    Cornell's camera (z = -3) is outside, so no render builds a rule-1 table for it."""
+    g = rtmi_mod.cornell_geometry(rtmi_mod.RT_PRESET_GPU)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        _cornell_frame(rtmi_mod, gpu_ctx, sc, rtmi_mod.RT_PRESET_GPU)
+        assert not sc.ctab_info(rtmi_mod.RT_HIT_RULE_GPU)["built"]
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+    cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=32, height=32, spp=4, spp_split=4)
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        cam.yaw_x = 0.1  # pitched: k_render_pq's camera rays cannot take the rectangle cull
+        rtmi_mod.render(gpu_ctx, sc, cam, p)
+        assert not sc.ctab_info(rtmi_mod.RT_HIT_RULE_GPU)["built"]
+        cam.yaw_x = 0.0
+        rtmi_mod.render(gpu_ctx, sc, cam, p)
+        assert sc.ctab_info(rtmi_mod.RT_HIT_RULE_GPU)["built"]

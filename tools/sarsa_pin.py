@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--modes", nargs="*", default=["frame", "inframe"])
     ap.add_argument("--scenes", nargs="*", default=list(SCENES))
     ap.add_argument("--size", type=int, default=720)
+    ap.add_argument("--lanes", type=int, nargs="*", default=[0],
+                    help="in-frame rule: paths in flight (rt_sarsa_set_inframe_lanes; 0 = the whole device)")
     ap.add_argument("--areas", type=float, nargs="*", default=[0.001],
                     help="AREA_PER_SAMPLE values (radiance_volumes_settings.h:12) to sweep")
     ap.add_argument("--final-spp", type=int, default=0,
@@ -67,11 +69,15 @@ def main():
             scene = spec.partition(":")[0]
             cam = rtmi.camera(rtmi.CAMERAS[scene])
             with rtmi.Scene(ctx, g) as sc:
-                for area, mode, spp, seed in itertools.product(args.areas, args.modes, args.spp, args.seeds):
+                for area, mode, spp, seed, lanes in itertools.product(args.areas, args.modes, args.spp, args.seeds,
+                                                                      args.lanes):
+                    if mode != "inframe" and lanes != args.lanes[0]:
+                        continue
                     rm = rtmi.sarsa.RadianceMap(ctx, sc, 1984, area_per_sample=area)  # placement seed fixed
                     try:
                         if mode == "inframe":
                             rm.set_td_mode(rtmi.sarsa.TD_INFRAME)
+                            rm.set_inframe_lanes(lanes)
                         p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=W, height=H, spp=spp,
                                                 spp_split=min(spp, 8), seed=seed)
                         logged, zero, cps, ms = [], [], [], []
@@ -103,6 +109,7 @@ def main():
                                               "block_max_abs_diff": round(float(d.max()), 3)})
                         r = {"scene": spec, "final": final, "mode": mode, "spp": spp, "seed": seed,
                              "area_per_sample": area, "n_volumes": rm.n_volumes,
+                             "inframe_lanes": lanes if mode == "inframe" else None,
                              "logged_avg_path": logged, "zero_paths": zero,
                              "zero_frac": [round(z / (W * H * spp), 5) for z in zero],
                              "casts_per_sample": cps, "ms": ms,
