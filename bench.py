@@ -847,6 +847,15 @@ def main():
             "frame_ms": round(frame_ms, 4),
             "roofline": roofline(args, geom, params, rank_casts / args.steps, kt),
         }
+        # preprocessing outside the timed region, measured in this run: the scene's bounce-ray
+        # candidate table (host build + upload on the first render that takes it, like a BVH
+        # build; device bytes per rank).  The camera rays' cull runs inside every timed frame.
+        tab_rule = rtmi.RT_HIT_RULE_GPU if sampler == "dqn" else params.hit_rule
+        ti = scene.ctab_info(tab_rule)
+        line["config"]["candidate_table"] = {
+            "built": ti["built"], "hit_rule": "cpu_object" if tab_rule == rtmi.RT_HIT_RULE_CPU else "gpu_engine",
+            "table_build_s": round(ti["build_s"], 3), "table_bytes": ti["bytes"],
+            "camera_ray_cull": "in the timed frame"}
         if sampler == "sarsa":  # a learning run: which of its frames the line times
             line["config"]["frames_warmup"] = [0, args.warmup - 1] if args.warmup else []
             line["config"]["frames_timed"] = [args.warmup, args.warmup + args.steps - 1]

@@ -1,6 +1,10 @@
 // rt_ctab.cpp — host build of the bounce-ray candidate table (rt_internal.hpp CtabHost,
-// rt_trace.hpp closest_hit_ctab): the hit rule of the CPU engine (rule 0), scenes of at
-// most 64 triangles, t_scale >= CtabHost::ts_min.
+// rt_trace.hpp closest_hit_ctab): both hit rules -- the CPU engine's (rule 0, t_scale >=
+// CtabHost::ts_min) and the GPU engine's (rule 1, any t_scale) -- for scenes of at most 256
+// triangles (1-4 mask words per entry).  Default size: kCtabPatches = 16,384 patches over the
+// scene x 6 x 16 x 16 direction bins, one 8-B word per entry and mask word: about 200 MB per mask
+// word (Cornell 201 MB, complex_light_room 600 MB at 3 words), built in about 1-5 s on the host's
+// threads on the first render that takes it (rt_scene_ctab_info reports both).
 //
 // The reference tests every triangle for every ray (Ray::closest_intersection,
 // CPU/rays/ray.cpp:14-28); its hit depends only on the triangles that pass the geometric
@@ -34,6 +38,8 @@
 //    patch (the origin's own plane: D ~ 1e-5) is crossed at lambda >= lambda_min only along
 //    directions with |d.n| <= D / lambda_min < theta_g: band directions, so it has no regular
 //    bins.
+// Rule 1 (t >= 0, no lower bound): lambda_min is 0, so the triangles coplanar with the origin's
+// surface join every ray leaving it (cop, cop_th = infinity) and the rest follows with lambda >= 0.
 // Origins: the kernel's patch choice (float dot products) and its check |o.n - c| <= h are
 // covered by widening the patch; directions by widening the bins beyond the kernel's
 // rounding of the cube-map coordinates.  A ray that is outside the table (origin off its
