@@ -398,6 +398,8 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale, bool wante
     t.words = ct.words;
     t.bins = kCtabBins;
     t.graze_n = kCtabGraze;
+    t.gflag = ct.gflag;
+    t.n_gdict = (int)(ct.gdict.size() / (size_t)ct.words);
     sc->ctab_build_s[rule] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     sc->ctab_bytes[rule] = sizeof(uint64_t) * (ct.masks.size() + ct.gdict.size() + ct.cop.size()) +
                            sizeof(uint16_t) * ct.gid.size() + sizeof(float4) * ct.tri.size();

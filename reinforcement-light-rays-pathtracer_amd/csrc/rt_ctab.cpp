@@ -64,6 +64,9 @@ namespace rt {
 namespace {
 
 constexpr double kK = kBvhK;
+#ifndef RT_CTAB_GFOLD
+#define RT_CTAB_GFOLD 1  // 0: no grazing fold (A/B builds)
+#endif
 constexpr int kNc = kCtabBins;    // coarse direction bins per face edge
 constexpr int kNg = kCtabGraze;   // grazing bins per face edge
 using Bins = std::bitset<kNc * kNc>;  // the coarse bins of one face, bit iu * kNc + iv
@@ -684,6 +687,40 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, doub
             h.gid[e] = (uint16_t)it->second;
         }
         std::vector<uint64_t>().swap(h.graze);
+        // The grazing fold (scenes of at most 63 triangles: bit 63 of the one mask word is free).
+        // A coarse bin (f, iu, iv) holds the fine grazing bins (f, gu, gv) with gu >> s = iu,
+        // gv >> s = iv (kNg = kNc << s: the kernel's bin indices are floor(u1 kN / 2) of the same
+        // u1, so a fine bin's coarse bin is its index >> s).  Where they all share one grazing mask,
+        // that mask is OR-ed into every patch's entry of the bin -- the lookup's F = mm | gg is
+        // unchanged -- and elsewhere bit 63 of the entries is set: look the grazing mask up.  A
+        // ray in a folded bin then needs one dependent memory access (its entry), not two.
+        h.gflag = 0;
+        if (RT_CTAB_GFOLD && W == 1 && n <= 63 && kNg % kNc == 0) {
+            const int sh = kNg / kNc;
+            size_t folded = 0;
+            std::vector<int32_t> fold(6 * kNc * kNc, -1);
+            for (int f = 0; f < 6; ++f)
+                for (int iu = 0; iu < kNc; ++iu)
+                    for (int iv = 0; iv < kNc; ++iv) {
+                        const uint16_t g0 = h.gid[(size_t)(f * kNg + iu * sh) * kNg + iv * sh];
+                        bool same = true;
+                        for (int a = 0; a < sh && same; ++a)
+                            for (int b = 0; b < sh && same; ++b)
+                                same = h.gid[(size_t)(f * kNg + iu * sh + a) * kNg + iv * sh + b] == g0;
+                        if (same) {
+                            fold[(size_t)(f * kNc + iu) * kNc + iv] = g0;
+                            ++folded;
+                        }
+                    }
+            const size_t per = (size_t)6 * kNc * kNc;
+            for (size_t e = 0; e < h.masks.size(); ++e) {
+                const int32_t g = fold[e % per];
+                h.masks[e] = g >= 0 ? (h.masks[e] | h.gdict[(size_t)g]) : (h.masks[e] | kCtabGflagBit);
+            }
+            h.gflag = 1;
+            if (getenv("RT_CTAB_VERBOSE"))
+                fprintf(stderr, "rtmi: candidate table: %zu of %zu coarse bins folded\n", folded, per);
+        }
         if (getenv("RT_CTAB_VERBOSE"))
             fprintf(stderr, "rtmi: candidate table: %d triangles, rule %d, %d patches (%.1f MB), %zu distinct grazing masks\n",
                     n, rule, n_patch, h.masks.size() * 8e-6, ids.size());
@@ -724,6 +761,11 @@ void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], u
     const bool cp = fabsf(cn) < h.cop_th;
     const uint64_t* mm = &h.masks[((size_t)patch * 6 * kNc * kNc + (size_t)(f * kNc + bin(u1, kNc)) * kNc + bin(v1, kNc)) * W];
     const uint64_t* gg = &h.gdict[(size_t)h.gid[(size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)] * W];
+    if (h.gflag) {  // the grazing fold (one word): the bin's grazing mask is in the entry unless flagged
+        const uint64_t m = mm[0];
+        out[0] = (m & ~kCtabGflagBit) | ((m & kCtabGflagBit) ? gg[0] : 0ull) | (cp ? h.cop[(size_t)s] : 0ull);
+        return;
+    }
     for (int k = 0; k < W; ++k) out[k] = mm[k] | gg[k] | (cp ? h.cop[(size_t)s * W + k] : 0ull);
 }
 

@@ -1250,7 +1250,10 @@ __global__ __launch_bounds__(256) void k_nq_end_sample(const DqnLaunch a, const 
         const f3 t = ld3(r.total, i);
         st3(r.total, i, make3(t.x + tp.x, t.y + tp.y, t.z + tp.z));
         b = r.bounces[i];
-        z = ((tp.x + tp.y + tp.z) / 3.f < kThroughputThreshold) ? 1u : 0u;
+        // every channel below THROUGHPUT_THRESHOLD (sum_zero_contribution_light_paths,
+        // nn_rendering_helpers.cu:556-568; the Expected-SARSA count tests the channels' mean,
+        // reinforcement_path_tracing.cu:36-42); a NaN channel is not below it
+        z = (tp.x < kThroughputThreshold && tp.y < kThroughputThreshold && tp.z < kThroughputThreshold) ? 1u : 0u;
     }
     const unsigned sb = wave_sum_u(b), sz = wave_sum_u(z);
     if ((threadIdx.x & 63) == 0) {

@@ -150,6 +150,7 @@ constexpr int kCtabGraze = RT_CTAB_GRAZE;
 constexpr float kCtabTsMin = 256.0f;  // the smallest t_scale the table serves
 constexpr float kCtabHemi = 2e-6f;    // directions with d.N_s < -kCtabHemi (off s's hemisphere) keep every triangle
 constexpr int kCtabMaxWords = 4;  // mask words per entry: scenes of at most 256 triangles
+constexpr uint64_t kCtabGflagBit = 1ull << 63;  // (gflag tables: scenes of at most 63 triangles)
 // the render paths that may take the table (rt_capi.cpp ctab_wanted)
 constexpr int kCtabForRender = 0, kCtabForDqn = 1, kCtabForSarsa = 2;
 struct CtabHost {
@@ -167,6 +168,8 @@ struct CtabHost {
     std::vector<uint64_t> gdict;  // [n_gdict][words]
     std::vector<uint16_t> gid;    // [face][gu][gv]
     std::vector<uint64_t> graze;  // the build's uncompressed grazing bins (emptied once indexed)
+    int gflag = 0;                // the grazing fold (rt_ctab.cpp): masks hold their bin's grazing mask
+                                  // unless bit 63 (kCtabGflagBit) says to look it up
 };
 bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, double ts_min, CtabHost* out);
 void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], uint64_t* out);
@@ -181,6 +184,8 @@ struct CtabDev {
     float h = 0.0f, ts_min = 0.0f, cop_th = 0.0f;
     int words = 0;
     int bins = 0, graze_n = 0;  // the build's kCtabBins / kCtabGraze (kernels use the table only if theirs agree)
+    int gflag = 0;              // CtabHost::gflag
+    int n_gdict = 0;            // entries of gdict (words each)
 };
 
 struct DeviceScene {

@@ -1106,6 +1106,29 @@ __global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_
             next = reinterpret_cast<float*>(ls + (shade_lds ? (size_t)n * kShadeF4 : 0));
         }
 #endif
+#if RT_PS_CT_TRI_LDS
+        // the table's surface patch frames (the first link of every bounce cast's lookup chain:
+        // frame -> patch and bin -> mask words): from LDS instead of L1/L2
+        if constexpr (CT) {
+            float4* lt = reinterpret_cast<float4*>(next);
+            const int m = a.scene.n_surf * 4;
+            for (int i = threadIdx.x; i < m; i += 256) lt[i] = a.scene.ctab[RULE].tri[i];
+            ms.ctab[RULE].tri = lt;
+            next = reinterpret_cast<float*>(lt + m);
+        }
+#endif
+#if RT_PS_CT_DICT_LDS
+        // the grazing masks' dictionary (a few dozen words): the last link of the lookup chain in LDS
+        if constexpr (CT) {
+            const CtabDev& T = a.scene.ctab[RULE];
+            if (T.n_gdict <= kPsCtDictLds) {
+                unsigned long long* ld = reinterpret_cast<unsigned long long*>(next);
+                for (int i = threadIdx.x; i < T.n_gdict; i += 256) ld[i] = T.gdict[i];
+                ms.ctab[RULE].gdict = ld;
+            }
+            next += 2 * kPsCtDictLds;
+        }
+#endif
 #if RT_MF_LDS
         if (!CT) {
             const int ng = mf_groups(a.scene.n_tri);
@@ -1114,7 +1137,7 @@ __global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_
             ms.mf_frag = lf;
         }
 #endif
-        if (RT_PS_SCENE_LDS || (RT_MF_LDS && !CT)) __syncthreads();
+        if (RT_PS_SCENE_LDS || (RT_MF_LDS && !CT) || ((RT_PS_CT_TRI_LDS || RT_PS_CT_DICT_LDS) && CT)) __syncthreads();
     }
     const unsigned n_casts =
         (vmask == 0ull) ? 0u : ps_body<SAMPLER, RULE, MF, CT>(a, ms, wl, blk, q, chunk, lane, lx, ly, px, py, valid);
@@ -1265,6 +1288,8 @@ static void launch_render_t(const RenderLaunch& a, hipStream_t stream) {
                     mf_lds += (size_t)a.scene.n_tri *
                               (kIsectF4 + (RT_PS_SHADE_LDS && (!ct || RT_PS_CT_SHADE_LDS) ? kShadeF4 : 0)) * sizeof(float4);
                 if (RT_MF_LDS && !ct) mf_lds += (size_t)mf_groups(a.scene.n_tri) * 64 * sizeof(uint4);
+                if (RT_PS_CT_TRI_LDS && ct) mf_lds += (size_t)a.scene.n_surf * 4 * sizeof(float4);
+                if (RT_PS_CT_DICT_LDS && ct) mf_lds += (size_t)kPsCtDictLds * sizeof(uint64_t);
             }
             const dim3 grid((unsigned)(a.n_blocks * a.split));
             KernelTimer kt(KT_RENDER_PS, stream);

@@ -874,9 +874,19 @@ __device__ __forceinline__ void ctab_candidates(const CtabDev& T, int n_tri, int
     const int gv = min(kCtabGraze - 1, max(0, (int)(v1 * (0.5f * kCtabGraze))));
     const int patch = base + (int)pu * nv + (int)pv;
     const unsigned long long* mm = T.masks + ((size_t)patch * (6 * kCtabBins * kCtabBins) + (f * kCtabBins + iu) * kCtabBins + iv) * W;
-    const unsigned long long* gg = T.gdict + (size_t)T.gid[(f * kCtabGraze + gu) * kCtabGraze + gv] * W;
+    const int gi = (f * kCtabGraze + gu) * kCtabGraze + gv;
     // the triangles coplanar with the surface join near its plane's great circle (rule 0) or always (rule 1)
     const bool cp = fabsf(cn) < T.cop_th;
+    if (NW == 1 && T.gflag) {
+        // the grazing fold (rt_ctab.cpp): the entry holds its bin's grazing mask unless bit 63 asks
+        // for the lookup -- one dependent access for most rays instead of entry + index + mask
+        const uint64_t m = mm[0];
+        uint64_t g = 0ull;
+        if (m & kCtabGflagBit) g = T.gdict[T.gid[gi]];
+        F[0] = (m & ~kCtabGflagBit) | g | (cp ? T.cop[surf] : 0ull);
+        return;
+    }
+    const unsigned long long* gg = T.gdict + (size_t)T.gid[gi] * W;
 #pragma unroll
     for (int k = 0; k < NW; ++k)
         if (k < W) F[k] = mm[k] | gg[k] | (cp ? T.cop[surf * W + k] : 0ull);
@@ -1054,6 +1064,13 @@ __device__ __forceinline__ Hit closest_hit_ctab(const DeviceScene& s, const Ctab
 #endif
 #ifndef RT_PS_SHADE_LDS
 #define RT_PS_SHADE_LDS 1  // 0: with RT_PS_SCENE_LDS, only the isect records in LDS (shading from L1/L2)
+#endif
+#ifndef RT_PS_CT_DICT_LDS
+#define RT_PS_CT_DICT_LDS 0  // 1: the table route's grazing dictionary in LDS (when it has <= kPsCtDictLds words)
+#endif
+constexpr int kPsCtDictLds = 64;
+#ifndef RT_PS_CT_TRI_LDS
+#define RT_PS_CT_TRI_LDS 0  // 1: the table route's surface patch frames (CtabDev::tri) in LDS
 #endif
 #ifndef RT_PS_CT_SHADE_LDS
 // the table-route kernel's shading records: from L1/L2 (0) -- with the shorter pair list it keeps
