@@ -67,8 +67,9 @@ class DeviceScene {
 // GPU/radiance_volumes/radiance_map.cuh: sampled radiance volumes, Q-table, KD tree.
 class RadianceMap {
    public:
-    explicit RadianceMap(DeviceScene& ds, uint64_t seed = 1984) : ds_(ds) {
-        detail::check(rt_sarsa_create(ds.ctx(), ds.scene(), seed, &map_));
+    // area_per_sample: AREA_PER_SAMPLE (GPU/constants/radiance_volumes_settings.h:12), the volume density
+    explicit RadianceMap(DeviceScene& ds, uint64_t seed = 1984, float area_per_sample = 0.001f) : ds_(ds) {
+        detail::check(rt_sarsa_create_density(ds.ctx(), ds.scene(), seed, area_per_sample, &map_));
         detail::check(rt_sarsa_info(map_, &radiance_volumes_count, &radiance_array_size, nullptr));
     }
     ~RadianceMap() {
@@ -97,6 +98,9 @@ class RadianceMap {
     void set_in_frame_td(bool on) {
         detail::check(rt_sarsa_set_td_mode(map_, on ? RT_SARSA_TD_INFRAME : RT_SARSA_TD_FRAME));
     }
+    // paths in flight of the in-frame rule (its races depend on it; the reference's GTX 1070 Ti
+    // held about 4,864: the setting its training logs are matched at); 0: the whole device
+    void set_in_frame_lanes(int lanes) { detail::check(rt_sarsa_set_inframe_lanes(map_, lanes)); }
     // GPU/main.cu:321-339 after a frame: the average path length as the reference computes it
     // (int(sum over pixels of int(path lengths / spp)) / pixels)) and the zero-contribution
     // paths; append_training_stats writes its "avg 0 zero" line.

@@ -143,3 +143,42 @@ def test_trained_network_beats_the_untrained_one(rtmi_mod, gpu_ctx):
     m = {k: float(np.mean(np.abs(v[0] - ref) / np.maximum(ref, 1e-3))) for k, v in out.items()}
     assert m["trained"] < 0.85 * m["synthetic"], m
     assert out["trained"][1] < out["synthetic"][1]
+
+
+# The reference's Neural-Q training run of the door room (Radiance_Map_Data/door_room_12_12_stats.txt,
+# tests/golden/nn_ref_stats.json): one row per training sample (neural_q_pathtracer.cu:545-583), the
+# average path length falling linearly from 50.3 to 33.5 over 100 rows as epsilon decays from 1 by
+# EPSILON_DECAY 0.01 to EPSILON_MIN 0.05 (deep_learning_settings.h:5-8), 720x720, batch 4096
+# (main.cu:116-124), DyNet's Adam defaults, the network from DyNet's default Glorot initialisation.
+# Measured over all 100 rows (tools/nq_pin.py, profiles/r6h/, r6j/): our rows within 0.29 of the log
+# at three seeds (mean difference -0.06 ... +0.09; rows 0-19 within 0.12); a network that does not
+# learn (learning rate 1e-9) drifts 3.5 above it by row 19.  The zero-contribution column is not
+# gated: ours is 1.97-2.12x the log's from row 0 on (epsilon 1, uniform cells), where the equal path
+# lengths already pin the sampling; the statistic counts the paths still bouncing after 80 bounces
+# by their throughput, which depends on settings the row-0 path lengths do not see.
+def _nq_rows(rtmi_mod, ctx, rows, lr):
+    g = rtmi_mod.obj_geometry(os.path.join(MODELS, "door_room.obj"), "door_room")
+    W0, b0 = rtmi_mod.dqn.glorot_weights(g.nn_vertices.size)
+    out = []
+    with rtmi_mod.Scene(ctx, g) as sc, rtmi_mod.dqn.DqnTrainer(ctx, g.nn_vertices, W0, b0, learning_rate=lr) as tr, \
+            rtmi_mod.dqn.NeuralQ(ctx, sc, tr, batch_size=4096, epsilon_start=1.0, epsilon_min=0.05,
+                                 epsilon_decay=0.01) as nq:
+        p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=720, height=720, spp=1)
+        for _ in range(rows):
+            _, st, _ = nq.render_frame(rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"]), p)
+            out.append(float(st[0, 0]))
+    return np.array(out)
+
+
+def test_training_trajectory_matches_reference_log(rtmi_mod, gpu_ctx):
+    """Rows 0-11 of the door room's logged training run (average path length within 0.3 on every
+    row); negative control: the same run with a network that does not learn misses by row 11."""
+    import json
+    from conftest import GOLDEN
+    ref = np.array(json.load(open(os.path.join(GOLDEN, "nn_ref_stats.json")))["door_room_12_12"]["avg_path_length"])
+    rows = _nq_rows(rtmi_mod, gpu_ctx, 12, 1e-3)
+    d = rows - ref[:12]
+    assert np.abs(d).max() <= 0.3, np.round(d, 3)
+    assert rows[-1] < rows[0] - 1.0
+    still = _nq_rows(rtmi_mod, gpu_ctx, 12, 1e-9)
+    assert np.abs(still - ref[:12]).max() > 1.0, np.round(still - ref[:12], 3)

@@ -36,14 +36,14 @@ def geometry(scene):
     return rtmi.obj_geometry(os.path.join(ROOT, "assets", "models", scene + ".obj"), scene)
 
 
-def run(ctx, scene, rows, seed, init, size=720, batch=4096, eps=(1.0, 0.05, 0.01), log=print):
+def run(ctx, scene, rows, seed, init, size=720, batch=4096, eps=(1.0, 0.05, 0.01), lr=1e-3, log=print):
     """one training run: per row (sample) the average path length, loss and zero-contribution paths"""
     g = geometry(scene)
     cam = rtmi.camera(rtmi.CAMERAS[scene])
     n_in = g.nn_vertices.size
     W0, b0 = (rtmi.dqn.glorot_weights if init == "glorot" else rtmi.dqn.synthetic_weights)(n_in, seed=seed)
     out = {"path": [], "loss": [], "zero": [], "s": []}
-    with rtmi.Scene(ctx, g) as sc, rtmi.dqn.DqnTrainer(ctx, g.nn_vertices, W0, b0) as tr, \
+    with rtmi.Scene(ctx, g) as sc, rtmi.dqn.DqnTrainer(ctx, g.nn_vertices, W0, b0, learning_rate=lr) as tr, \
             rtmi.dqn.NeuralQ(ctx, sc, tr, batch_size=batch, epsilon_start=eps[0], epsilon_min=eps[1],
                              epsilon_decay=eps[2]) as nq:
         p = rtmi.default_params(rtmi.RT_PRESET_GPU, width=size, height=size, spp=1, seed=seed)
@@ -64,10 +64,11 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="rows per run (0: the log's length)")
     ap.add_argument("--seeds", type=int, nargs="*", default=[1984])
     ap.add_argument("--init", default="glorot", choices=["glorot", "he"])
+    ap.add_argument("--lr", type=float, default=1e-3, help="Adam's learning rate (DyNet's default 1e-3; 0: a network that never learns)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "nq_pin.json"))
     args = ap.parse_args()
     ref = json.load(open(os.path.join(ROOT, "tests", "golden", "nn_ref_stats.json")))
-    res = {"settings": {"size": 720, "batch": 4096, "epsilon": [1.0, 0.05, 0.01], "init": args.init,
+    res = {"settings": {"size": 720, "batch": 4096, "epsilon": [1.0, 0.05, 0.01], "init": args.init, "lr": args.lr,
                         "preset": "gpu"}, "runs": []}
     os.makedirs(os.path.dirname(os.path.abspath(args.out)), exist_ok=True)
     with rtmi.Context(0) as ctx:
@@ -75,7 +76,7 @@ def main():
             log = ref[LOGS[scene]]
             rows = args.rows or len(log["avg_path_length"])
             for seed in args.seeds:
-                r = run(ctx, scene, rows, seed, args.init, log=lambda m: print(m, flush=True))
+                r = run(ctx, scene, rows, seed, args.init, lr=args.lr, log=lambda m: print(m, flush=True))
                 r.update({"scene": scene, "seed": seed, "ref_path": log["avg_path_length"][:rows],
                           "ref_zero": log["zero_contribution_paths"][:rows]})
                 res["runs"].append(r)
