@@ -687,15 +687,16 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, doub
             h.gid[e] = (uint16_t)it->second;
         }
         std::vector<uint64_t>().swap(h.graze);
-        // The grazing fold (scenes of at most 63 triangles: bit 63 of the one mask word is free).
-        // A coarse bin (f, iu, iv) holds the fine grazing bins (f, gu, gv) with gu >> s = iu,
-        // gv >> s = iv (kNg = kNc << s: the kernel's bin indices are floor(u1 kN / 2) of the same
-        // u1, so a fine bin's coarse bin is its index >> s).  Where they all share one grazing mask,
-        // that mask is OR-ed into every patch's entry of the bin -- the lookup's F = mm | gg is
-        // unchanged -- and elsewhere bit 63 of the entries is set: look the grazing mask up.  A
-        // ray in a folded bin then needs one dependent memory access (its entry), not two.
+        // The grazing fold (scenes whose triangle count is not a multiple of 64: bit 63 of the
+        // last mask word is free).  A coarse bin (f, iu, iv) holds the fine grazing bins (f, gu, gv)
+        // with gu / r = iu, gv / r = iv (kNg = r kNc, r a power of two: the kernel's bin indices are
+        // floor(u1 kN / 2) of the same u1, so a fine bin's coarse bin is its index / r).  Where they
+        // all share one grazing mask, that mask is OR-ed into every patch's entry of the bin -- the
+        // lookup's F = mm | gg is unchanged -- and elsewhere bit 63 of the entries' last word is set:
+        // look the grazing mask up.  A ray in a folded bin then needs one dependent memory access
+        // (its entry), not two.
         h.gflag = 0;
-        if (RT_CTAB_GFOLD && W == 1 && n <= 63 && kNg % kNc == 0) {
+        if (RT_CTAB_GFOLD && n < 64 * W && kNg % kNc == 0) {
             const int sh = kNg / kNc;
             size_t folded = 0;
             std::vector<int32_t> fold(6 * kNc * kNc, -1);
@@ -713,9 +714,15 @@ bool ctab_build(const float4* isect, int n, int n_surf, double B, int rule, doub
                         }
                     }
             const size_t per = (size_t)6 * kNc * kNc;
-            for (size_t e = 0; e < h.masks.size(); ++e) {
+            const size_t entries = h.masks.size() / (size_t)W;
+            for (size_t e = 0; e < entries; ++e) {
                 const int32_t g = fold[e % per];
-                h.masks[e] = g >= 0 ? (h.masks[e] | h.gdict[(size_t)g]) : (h.masks[e] | kCtabGflagBit);
+                uint64_t* m = &h.masks[e * (size_t)W];
+                if (g >= 0) {
+                    for (int w = 0; w < W; ++w) m[w] |= h.gdict[(size_t)g * W + w];
+                } else {
+                    m[W - 1] |= kCtabGflagBit;
+                }
             }
             h.gflag = 1;
             if (getenv("RT_CTAB_VERBOSE"))
@@ -761,9 +768,11 @@ void ctab_lookup(const CtabHost& h, int s, const float o[3], const float d[3], u
     const bool cp = fabsf(cn) < h.cop_th;
     const uint64_t* mm = &h.masks[((size_t)patch * 6 * kNc * kNc + (size_t)(f * kNc + bin(u1, kNc)) * kNc + bin(v1, kNc)) * W];
     const uint64_t* gg = &h.gdict[(size_t)h.gid[(size_t)(f * kNg + bin(u1, kNg)) * kNg + bin(v1, kNg)] * W];
-    if (h.gflag) {  // the grazing fold (one word): the bin's grazing mask is in the entry unless flagged
-        const uint64_t m = mm[0];
-        out[0] = (m & ~kCtabGflagBit) | ((m & kCtabGflagBit) ? gg[0] : 0ull) | (cp ? h.cop[(size_t)s] : 0ull);
+    if (h.gflag) {  // the grazing fold: the bin's grazing mask is in the entry unless flagged
+        const bool look = (mm[W - 1] & kCtabGflagBit) != 0;
+        for (int k = 0; k < W; ++k)
+            out[k] = (mm[k] & (k == W - 1 ? ~kCtabGflagBit : ~0ull)) | (look ? gg[k] : 0ull) |
+                     (cp ? h.cop[(size_t)s * W + k] : 0ull);
         return;
     }
     for (int k = 0; k < W; ++k) out[k] = mm[k] | gg[k] | (cp ? h.cop[(size_t)s * W + k] : 0ull);

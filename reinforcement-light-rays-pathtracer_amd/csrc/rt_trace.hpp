@@ -877,13 +877,23 @@ __device__ __forceinline__ void ctab_candidates(const CtabDev& T, int n_tri, int
     const int gi = (f * kCtabGraze + gu) * kCtabGraze + gv;
     // the triangles coplanar with the surface join near its plane's great circle (rule 0) or always (rule 1)
     const bool cp = fabsf(cn) < T.cop_th;
-    if (NW == 1 && T.gflag) {
-        // the grazing fold (rt_ctab.cpp): the entry holds its bin's grazing mask unless bit 63 asks
-        // for the lookup -- one dependent access for most rays instead of entry + index + mask
-        const uint64_t m = mm[0];
-        uint64_t g = 0ull;
-        if (m & kCtabGflagBit) g = T.gdict[T.gid[gi]];
-        F[0] = (m & ~kCtabGflagBit) | g | (cp ? T.cop[surf] : 0ull);
+    if (T.gflag) {
+        // the grazing fold (rt_ctab.cpp): the entry holds its bin's grazing mask unless bit 63 of
+        // its last word asks for the lookup -- one dependent access for most rays, not three
+        uint64_t m[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) m[k] = (k < W) ? mm[k] : 0ull;
+        uint64_t last = 0ull;
+#pragma unroll
+        for (int k = 0; k < NW; ++k)
+            if (k == W - 1) last = m[k];
+        const bool look = (last & kCtabGflagBit) != 0ull;
+        const unsigned long long* gg = look ? T.gdict + (size_t)T.gid[gi] * W : nullptr;
+#pragma unroll
+        for (int k = 0; k < NW; ++k)
+            if (k < W)
+                F[k] = (m[k] & (k == W - 1 ? ~kCtabGflagBit : ~0ull)) | (look ? gg[k] : 0ull) |
+                       (cp ? T.cop[surf * W + k] : 0ull);
         return;
     }
     const unsigned long long* gg = T.gdict + (size_t)T.gid[gi] * W;
