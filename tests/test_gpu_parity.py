@@ -209,7 +209,7 @@ def test_full_size_properties(rtmi_mod, oracle_mod, gpu_ctx):
 
 def test_config5_rank_tile_sets_assemble_to_single_gpu_frame(rtmi_mod, oracle_mod, gpu_ctx):
     """BASELINE config 5 at its full size on one GPU: complex_light_room 2048x2048, GPU-engine
-    preset (80 bounces), 128 spp at the bench's spp_split 32, rendered through
+    preset (80 bounces), 1024 spp at the bench's spp_split 32 (~8 s per render), rendered through
     render_tiles_device once per rank tile set of the P = 8 partition (rtmi.tiles: 32x32
     tiles dealt by diagonals) and assembled: bit-identical to the single-rank frame, the
     ranks' ray casts sum to its casts, and two tiles bit-exact against the CPU
@@ -218,7 +218,7 @@ def test_config5_rank_tile_sets_assemble_to_single_gpu_frame(rtmi_mod, oracle_mo
     torch = pytest.importorskip("torch")
     geom = rtmi_mod.obj_geometry(os.path.join(MODELS, "complex_light_room.obj"), "complex_light_room")
     W = H = 2048
-    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=W, height=H, spp=128, spp_split=32)
+    p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=W, height=H, spp=1024, spp_split=32)
     assert p.max_bounces == 80
     cam = rtmi_mod.camera(rtmi_mod.CAMERAS["complex_light_room"])
     stream = torch.cuda.current_stream().cuda_stream
