@@ -732,10 +732,12 @@ def main():
         raise SystemExit(f"WORLD_SIZE={world} but --gpus {args.gpus}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group(backend="nccl")
+    # the rank's GPU first, then the process group bound to it (RCCL's communicator is created on
+    # that device, not on whichever device is current when the first collective runs)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group(backend="nccl", device_id=dev)
 
     ctx = rtmi.Context(local_rank)
     scene_kind, sampler, cfg, geom, cam_pos, params = make_workload(args, ctx)
