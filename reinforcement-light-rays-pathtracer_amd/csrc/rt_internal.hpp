@@ -442,7 +442,10 @@ struct SarsaMap {
     unsigned long long* prof = nullptr;    // [8] RT_SARSA_PROF builds: per-phase s_memtime cycles (rt_sarsa.hip)
 };
 #ifndef RT_KD_STACK
-#define RT_KD_STACK 32
+// 30: the SARSA render's 256-lane workgroup then takes 30 KB of LDS and five fit a CU (32 KB held
+// it to four: door_room 512^2 x 256 frames 1-4 108.6 -> 104.9 ms, profiles/r6r/); supports trees
+// of depth 29 (2^29 volumes; rt_sarsa_create_density caps maps at 2^24)
+#define RT_KD_STACK 30
 #endif
 constexpr int kKdStack = RT_KD_STACK;  // traversal stack entries per lane (LDS); tree depth <= kKdStack - 1
 
