@@ -587,9 +587,15 @@ __global__ __launch_bounds__(256) void k_fold_chunks(const RenderLaunch a) {
 // k_render<0, ...> (oracle/ parity); PRESET 0 paths are 1-3 casts, so about 37% of the
 // casts of the frame move from the full-scene scan to a few exact tests.
 //
-// LDS: per wave and sample slot k, four 64-lane rows (lane-contiguous: conflict-free):
+// LDS: per wave and sample slot k, three 64-lane float rows (lane-contiguous: conflict-free)
+// and one int16 row of hit codes:
 //   continuing: the hit point x, y, z, triangle;  ended: L.x, L.y, L.z, -1.
-constexpr int kPsFields = 4;
+// (int16 codes: 13 KB of slots per 256-lane workgroup at 4 samples per lane instead of 16 KB --
+// with the table route's pair list that is 25.6 KB per workgroup, six per CU)
+#ifndef RT_PS_CODE16
+#define RT_PS_CODE16 1  // the slots' hit codes as int16 beside three float rows (0: a fourth float row)
+#endif
+constexpr int kPsFields = RT_PS_CODE16 ? 3 : 4;  // float rows per sample slot
 
 #ifndef RT_PS_PRIM_BATCH
 #define RT_PS_PRIM_BATCH 4  // samples per candidate pass of phase P (1: one sample at a time)
@@ -607,7 +613,7 @@ constexpr int kPsSplitLights = 8;  // the light pre-test runs when the scene has
 // floats of LDS per wave: the sample slots, then (RT_PS_STEAL) the wave's queue of
 // continuing samples, one u16 (k << 6 | lane) per slot
 __host__ __device__ constexpr int ps_wave_floats(int pc) {
-    return pc * kPsFields * 64 + (RT_PS_STEAL ? pc * 32 : 0);
+    return pc * kPsFields * 64 + (RT_PS_CODE16 ? pc * 32 : 0) + (RT_PS_STEAL ? pc * 32 : 0);
 }
 
 
@@ -659,6 +665,15 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     const int pc = a.per_chunk;
     float* const wslots = s_ps + (size_t)(threadIdx.x >> 6) * ps_wave_floats(pc);
     float* const slots = wslots + lane;
+    // a slot's hit code: the triangle a continuing path's primary hit is on, or -1 (ended)
+#if RT_PS_CODE16
+    int16_t* const wcodes = reinterpret_cast<int16_t*>(wslots + pc * kPsFields * 64);
+    auto code_at = [&](int kk, int ln) -> int { return (int)wcodes[kk * 64 + ln]; };
+    auto set_code_at = [&](int kk, int ln, int c) { wcodes[kk * 64 + ln] = (int16_t)c; };
+#else
+    auto code_at = [&](int kk, int ln) -> int { return __float_as_int(wslots[(kk * kPsFields + 3) * 64 + ln]); };
+    auto set_code_at = [&](int kk, int ln, int c) { wslots[(kk * kPsFields + 3) * 64 + ln] = __int_as_float(c); };
+#endif
     const f3 cam = make3(a.cam_x, a.cam_y, a.cam_z);
 
     // ---- candidate triangles of the wave's pixel rectangle (rect_cull, rt_cull.hpp) ----
@@ -696,7 +711,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
         sl[0 * 64] = v0;
         sl[1 * 64] = v1;
         sl[2 * 64] = v2;
-        sl[3 * 64] = __int_as_float(code);
+        set_code_at(k, lane, code);
     };
 #if RT_PS_PRIM_BATCH > 1
     // The primary rays all start at the camera, so the cofactors of the exact test that
@@ -797,10 +812,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     // only its own: the wave runs ceil(casts / 64) trips instead of its busiest lane's.
     // A finished sample's value goes back into its slot; every lane then sums its own
     // slots in sample order (the fixed-chunk sum: the image is unchanged).
-    uint16_t* const queue = reinterpret_cast<uint16_t*>(wslots + pc * kPsFields * 64);
+    uint16_t* const queue = reinterpret_cast<uint16_t*>(wslots + pc * kPsFields * 64 + (RT_PS_CODE16 ? pc * 32 : 0));
     int q_total = 0;
     for (int kk = 0; kk < pc; ++kk) {
-        const bool cont = valid && __float_as_int(slots[kk * kPsFields * 64 + 3 * 64]) >= 0;
+        const bool cont = valid && code_at(kk, lane) >= 0;
         const uint64_t m = __ballot(cont);
         if (cont) queue[q_total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint16_t)((kk << 6) | lane);
@@ -820,7 +835,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
             const int ol = (int)(e & 63u), kk = (int)(e >> 6);
             own = wslots + kk * kPsFields * 64 + ol;
             pos = make3(own[0 * 64], own[1 * 64], own[2 * 64]);
-            hit_tri = __float_as_int(own[3 * 64]);
+            hit_tri = code_at(kk, ol);
             depth = 0;
             const int oq = q - (lane >> a.split_log2) + (ol >> a.split_log2);  // the lane's pixel
             lpix = (uint32_t)(blk.py0 + (oq >> 4)) * (uint32_t)a.width + (uint32_t)(blk.px0 + (oq & 15));
@@ -834,7 +849,7 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
     auto fetch = [&]() -> bool {
         while (k < pc) {
             const float* sl = slots + k * kPsFields * 64;
-            const int code = __float_as_int(sl[3 * 64]);
+            const int code = code_at(k, lane);
             if (code < 0) {
                 acc.x = acc.x + sl[0 * 64];
                 acc.y = acc.y + sl[1 * 64];
@@ -1054,7 +1069,10 @@ __device__ __forceinline__ unsigned ps_body(const RenderLaunch& a, const DeviceS
 #define RT_PS_MIN_WAVES 4  // the matrix-core filter's operands: ~99 VGPRs
 #endif
 #ifndef RT_PS_CT_WAVES
-#define RT_PS_CT_WAVES 4  // occupancy floor of the table-route variant (85 VGPRs: 5 waves; Cornell 512^2 x 256: 2.64 ms, 6 waves 2.67, 8 waves 3.00 with spills)
+// occupancy floor of the table-route variant: 6 (80 VGPRs, 7 spilled) -- with the int16 slot codes
+// its workgroup takes 26.7 KB of LDS and six fit a CU (Cornell 512^2 x 256: 2.39 -> 2.24 ms,
+// profiles/r6v/; at the 28.7-KB layout LDS held it to five and 6 only added spills)
+#define RT_PS_CT_WAVES 6
 #endif
 template <int SAMPLER, int RULE, int MF, bool CT = false>
 __global__ __launch_bounds__(256, CT ? RT_PS_CT_WAVES : RT_PS_MIN_WAVES) void k_render_ps(const RenderLaunch a) {
