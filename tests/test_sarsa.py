@@ -385,6 +385,31 @@ def test_gpu_volume_density_equals_oracle(rtmi_mod, oracle_mod, gpu_ctx, scene, 
         sc.close()
 
 
+@pytest.mark.gpu
+def test_gpu_inframe_lanes_cap(rtmi_mod, gpu_ctx):
+    """rt_sarsa_set_inframe_lanes caps the persistent render's workgroups: under the
+    frame-synchronous rule (order-free integer TD sums) a capped launch renders and learns
+    bit for bit what the whole-device launch does; a negative count is refused."""
+    g = geometry(rtmi_mod, "door_room")
+    with rtmi_mod.Scene(gpu_ctx, g) as sc:
+        maps = [rtmi_mod.sarsa.RadianceMap(gpu_ctx, sc, 1984) for _ in range(2)]
+        try:
+            with pytest.raises(rtmi_mod.RtError):
+                maps[0].set_inframe_lanes(-1)
+            maps[1].set_inframe_lanes(300)  # two workgroups
+            p = rtmi_mod.default_params(rtmi_mod.RT_PRESET_GPU, width=96, height=64, spp=8, spp_split=4)
+            cam = rtmi_mod.camera(rtmi_mod.CAMERAS["door_room"])
+            for _ in range(2):
+                (ia, ca), (ib, cb) = [m.render(cam, p, 1) for m in maps]
+                assert ca == cb and np.array_equal(ia, ib)
+                for a, b in zip(maps[0].read(), maps[1].read()):
+                    assert np.array_equal(a, b)
+                assert maps[0].frame_stats() == maps[1].frame_stats()
+        finally:
+            for m in maps:
+                m.close()
+
+
 def test_density_argument_refused(rtmi_mod):
     """area_per_sample must be finite and > 0 (checked before any device work)."""
     import ctypes
