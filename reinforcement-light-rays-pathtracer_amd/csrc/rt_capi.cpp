@@ -10,6 +10,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <chrono>
 #include <mutex>
 #include <string>
@@ -378,12 +379,10 @@ int scene_ensure_ctab(const rt_scene* scene, int rule, float t_scale, bool wante
         if (dc) (void)hipFree(dc);
         if (dt) (void)hipFree(dt);
         (void)hipGetLastError();  // the failed allocation must not fail the render's own launches
-        static bool warned = false;
-        if (!warned) {
-            warned = true;
+        static std::atomic<bool> warned{false};
+        if (!warned.exchange(true))
             fprintf(stderr, "rtmi: candidate table upload failed (%s); the bounce casts stay on the matrix-core image\n",
                     hipGetErrorString(e));
-        }
         return RT_OK;
     }
     CtabDev& t = sc->dev.ctab[rule];
