@@ -8,6 +8,7 @@ Prints one JSON line: MLP TFLOP/s against the bf16 dense MFMA peak (2.5 PF),
 render ms per sample and Mrays/s.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -100,7 +101,8 @@ def main():
                      "ms_per_step": round(dt / args.steps * 1e3, 2), "ray_casts": c,
                      "mrays_s": round(c / dt / 1e6, 2),
                      "casts_per_sample_per_pixel": round(c / (args.steps * args.spp * args.width ** 2), 3),
-                     "image_mean": float(out.mean().item())}
+                     "image_mean": float(out.mean().item()),
+                     "image_sha1": hashlib.sha1(out.cpu().numpy().tobytes()).hexdigest()[:16]}
     print(json.dumps(res), flush=True)
     net.close()
     sc.close()
